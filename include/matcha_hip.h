@@ -1,0 +1,141 @@
+/*
+ * matcha_hip.h — C ABI of the MI355X-native (gfx950) Matcha-TTS synthesis path.
+ *
+ * The reference (Lounes78/matcha-tts) has no native code and no FFI: its hot path is the
+ * PyTorch module call surface that main.py uses. Each entry point below replaces the ATen
+ * work under one of those calls (reference file:line in /root/reference):
+ *
+ *   mt_durations + mt_alignment  <- MatchaTTS.synthesize duration/index path  model.py:1273-1289
+ *                                   (sequence_mask :42-46, generate_path :64-76)
+ *   mt_cfm_solve                 <- CFM.forward / BASECFM.forward Euler|midpoint loop
+ *                                   model.py:1084-1109, 1136-1145, estimator Decoder.forward :964-1048
+ *   mt_decoder_step              <- one Decoder.forward (estimator) call  model.py:964-1048
+ *   mt_denorm_crop               <- denormalize + crop  model.py:106-125, 1295-1298
+ *   mt_vocoder_forward           <- hifigan.models.Generator.forward  hifigan/models.py:181-197
+ *   mt_denoise                   <- hifigan.denoiser.Denoiser.forward hifigan/denoiser.py:62-68
+ *
+ * Conventions
+ *  - Every pointer argument is DEVICE memory owned by the caller (PyTorch), except the
+ *    host-side handles and name/shape buffers. The library never allocates device memory
+ *    and keeps no global device state.
+ *  - `stream` is a hipStream_t passed as void*; all work is enqueued on it, asynchronously.
+ *  - Tensors use the reference layouts at the boundary: mel/mu/z [B][80][T] fp32, masks
+ *    [B][1][T] fp32 (0/1), wav [B][1][L] fp32. Internally activations are [B][T][C].
+ *  - Return 0 on success; a negative value on error, with a message in mt_last_error()
+ *    (thread-local).
+ *  - dtype selects the arithmetic of the conv/GEMM/attention kernels: MT_DTYPE_F32 (exact fp32
+ *    MFMA, parity mode) or MT_DTYPE_BF16 (bf16 MFMA, fp32 accumulate, perf mode). Norm
+ *    statistics, the time-embedding MLP and the ODE state are always fp32.
+ */
+#ifndef MATCHA_HIP_H
+#define MATCHA_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MT_DTYPE_F32 0
+#define MT_DTYPE_BF16 1
+#define MT_SOLVER_EULER 0
+#define MT_SOLVER_MIDPOINT 1
+
+const char* mt_last_error(void);
+int mt_abi_version(void);
+
+/* ---------------------------------------------------------------------------------------
+ * U-Net estimator + CFM solver. Hyper-parameters are those of main.py:67-76
+ * (channels=(256,256), attention_head_dim=64); c_cond = 2*n_feats (+ spk_emb_dim).
+ * ------------------------------------------------------------------------------------- */
+typedef struct mt_decoder mt_decoder;
+int mt_decoder_create(int c_cond, int n_mid_blocks, int n_blocks, int num_heads, int dtype,
+                      mt_decoder** out);
+void mt_decoder_destroy(mt_decoder* d);
+/* Reference state_dict tensors the packer needs, in canonical order, named relative to the
+ * estimator (e.g. "down_blocks.0.0.block1.block.0.weight"); "_sinus_freq" is the fp32
+ * frequency table exp(arange(c_cond/2) * -ln(1e4)/(c_cond/2-1)) of model.py:757-759. */
+int mt_decoder_num_params(const mt_decoder* d);
+int mt_decoder_param_name(const mt_decoder* d, int i, char* buf, int buflen);
+int mt_decoder_param_shape(const mt_decoder* d, int i, int64_t* shape, int maxdim); /* -> ndim */
+size_t mt_decoder_packed_bytes(const mt_decoder* d);
+/* params[i]: device fp32 tensor in reference layout for parameter i. */
+int mt_decoder_pack(const mt_decoder* d, const float* const* params, void* packed, void* stream);
+
+size_t mt_cfm_workspace_bytes(const mt_decoder* d, int B, int T, int n_timesteps, int solver);
+/* z_noise: randn [B,80,T] (z = z_noise*temperature, model.py:1085); mu_y [B,80,T]; mask [B,1,T];
+ * spks [B,spk_dim] or NULL; z_out [B,80,T] (may alias z_noise). T must be even. */
+int mt_cfm_solve(const mt_decoder* d, const void* packed, const float* z_noise, float temperature,
+                 const float* mu_y, const float* mask, const float* spks, int B, int T,
+                 int n_timesteps, int solver, float* z_out, void* ws, size_t ws_bytes, void* stream);
+
+size_t mt_decoder_step_workspace_bytes(const mt_decoder* d, int B, int T);
+/* one estimator evaluation: out = Decoder.forward(x, mask, mu_y, t, spks) [B,80,T] */
+int mt_decoder_step(const mt_decoder* d, const void* packed, const float* x, const float* mu_y,
+                    const float* mask, const float* spks, float t, int B, int T, float* out, void* ws,
+                    size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * HiFi-GAN Generator (hifigan/models.py:148-206). Parameters are the folded weights
+ * ("conv_pre.weight", "ups.0.weight", "resblocks.4.convs1.1.weight", ...) i.e. after
+ * remove_weight_norm (hifigan/models.py:199-206).
+ * ------------------------------------------------------------------------------------- */
+typedef struct mt_vocoder mt_vocoder;
+/* rb_dils: n_kernels x n_dils row-major */
+int mt_vocoder_create(int resblock, int n_ups, const int* up_rates, const int* up_kernels,
+                      int up_init_channel, int n_kernels, const int* rb_kernels, int n_dils,
+                      const int* rb_dils, int dtype, mt_vocoder** out);
+void mt_vocoder_destroy(mt_vocoder* v);
+int mt_vocoder_num_params(const mt_vocoder* v);
+int mt_vocoder_param_name(const mt_vocoder* v, int i, char* buf, int buflen);
+int mt_vocoder_param_shape(const mt_vocoder* v, int i, int64_t* shape, int maxdim);
+size_t mt_vocoder_packed_bytes(const mt_vocoder* v);
+int mt_vocoder_pack(const mt_vocoder* v, const float* const* params, void* packed, void* stream);
+size_t mt_vocoder_workspace_bytes(const mt_vocoder* v, int B, int T);
+/* mel [B,80,T] fp32 -> wav [B,1,T*prod(up_rates)] fp32 */
+int mt_vocoder_forward(const mt_vocoder* v, const void* packed, const float* mel, int B, int T,
+                       float* wav, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Duration -> alignment index path (bit-exact given logw).
+ * ------------------------------------------------------------------------------------- */
+/* w_ceil = ceil(exp(logw)*x_mask*length_scale) [B,Tx]; cum = cumsum(w_ceil) [B,Tx];
+ * y_lengths = max(sum(w_ceil), 1) int64 [B]. */
+int mt_durations(const float* logw, const float* x_mask, float length_scale, int B, int Tx,
+                 float* w_ceil, float* cum, int64_t* y_lengths, void* stream);
+/* attn [B,1,Tx,T] one-hot path (may be NULL); mu_y[b,c,j] = mu[b,c,token(j)] [B,C,T] (may be NULL);
+ * y_mask [B,1,T] = (j < y_lengths[b]) (may be NULL) */
+int mt_alignment(const float* cum, const int64_t* y_lengths, int B, int Tx, int T, const float* mu, int C,
+                 float* attn, float* mu_y, float* y_mask, void* stream);
+/* mel[b,c,t] = z[b,c,t]*std[c] + mean[c] for t < Ty; z [B,C,T] -> mel [B,C,Ty] */
+int mt_denorm_crop(const float* z, const float* mean, const float* std, int B, int C, int T, int Ty,
+                   float* mel, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Denoiser (hifigan/denoiser.py): STFT n_fft 1024 / hop 256 / Hann, magnitude - strength*bias,
+ * clamp >= 0, iSTFT. audio [B,L] -> out [B, 256*(L/256)]; bias_spec [513].
+ * ------------------------------------------------------------------------------------- */
+size_t mt_denoise_workspace_bytes(int B, int L);
+int mt_denoise(const float* audio, int B, int L, const float* bias_spec, float strength, float* out,
+               void* ws, size_t ws_bytes, void* stream);
+/* |STFT| (same framing) of every frame: mag [B][1+L/256][513] (bias spectrum, denoiser.py:57-60) */
+int mt_stft_magnitude(const float* audio, int B, int L, float* mag, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Op-level entry points (per-kernel parity tests)
+ * ------------------------------------------------------------------------------------- */
+/* y = conv(act(x)), x [B][Tin][Cin], y [B][Tout][Cout] in dtype; W fp32 reference layout
+ * (Conv1d [Cout][Cin][k]; transposed: ConvTranspose1d [Cin][Cout][k]); slope < 0: no act. */
+size_t mt_op_conv1d_workspace_bytes(int dtype, int cin, int cout, int k, int stride, int transposed);
+int mt_op_conv1d(int dtype, const void* x, int B, int Tin, int cin, const float* W, const float* bias,
+                 int cout, int k, int stride, int pad, int dil, int transposed, float slope, void* y,
+                 int Tout, void* ws, size_t ws_bytes, void* stream);
+/* qkv [B][T][3*heads*64], mask [B][T] -> out [B][T][heads*64], reference mask semantics */
+int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
+                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MATCHA_HIP_H */

@@ -1,0 +1,207 @@
+// C ABI (include/matcha_hip.h) over the decoder / vocoder drivers and the op kernels.
+#include <string.h>
+
+#include <new>
+
+#include "../../include/matcha_hip.h"
+#include "mt_model.h"
+
+namespace mt {
+const char* last_error();
+int denoise(const float* audio, int B, int L, const float* bias_spec, float strength, float* out, void* ws,
+            size_t ws_bytes, hipStream_t st);
+size_t denoise_workspace_bytes(int B, int L);
+int stft_magnitude(const float* audio, int B, int L, float* mag, hipStream_t st);
+}  // namespace mt
+
+struct mt_decoder {
+  mt::Decoder d;
+};
+struct mt_vocoder {
+  mt::Vocoder v;
+};
+
+using mt::set_error;
+
+static int param_name(const mt::ParamList& L, int i, char* buf, int buflen) {
+  MT_REQUIRE(i >= 0 && i < (int)L.names.size(), "param index %d out of range", i);
+  MT_REQUIRE(buf && buflen > (int)L.names[i].size(), "param name buffer too small");
+  memcpy(buf, L.names[i].c_str(), L.names[i].size() + 1);
+  return 0;
+}
+static int param_shape(const mt::ParamList& L, int i, int64_t* shape, int maxdim) {
+  MT_REQUIRE(i >= 0 && i < (int)L.names.size(), "param index %d out of range", i);
+  const auto& s = L.shapes[i];
+  MT_REQUIRE((int)s.size() <= maxdim, "shape buffer too small");
+  for (size_t k = 0; k < s.size(); ++k) shape[k] = s[k];
+  return (int)s.size();
+}
+
+extern "C" {
+
+const char* mt_last_error(void) { return mt::last_error(); }
+int mt_abi_version(void) { return 1; }
+
+// ---- decoder ----
+int mt_decoder_create(int c_cond, int n_mid, int n_blocks, int heads, int dtype, mt_decoder** out) {
+  MT_REQUIRE(out, "null out");
+  mt_decoder* h = new (std::nothrow) mt_decoder();
+  MT_REQUIRE(h, "out of host memory");
+  int rc = h->d.init(c_cond, n_mid, n_blocks, heads, dtype);
+  if (rc) {
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return 0;
+}
+void mt_decoder_destroy(mt_decoder* d) { delete d; }
+int mt_decoder_num_params(const mt_decoder* d) { return d ? (int)d->d.params.names.size() : -1; }
+int mt_decoder_param_name(const mt_decoder* d, int i, char* buf, int buflen) {
+  MT_REQUIRE(d, "null decoder");
+  return param_name(d->d.params, i, buf, buflen);
+}
+int mt_decoder_param_shape(const mt_decoder* d, int i, int64_t* shape, int maxdim) {
+  MT_REQUIRE(d, "null decoder");
+  return param_shape(d->d.params, i, shape, maxdim);
+}
+size_t mt_decoder_packed_bytes(const mt_decoder* d) { return d ? d->d.packed_bytes : 0; }
+int mt_decoder_pack(const mt_decoder* d, const float* const* params, void* packed, void* stream) {
+  MT_REQUIRE(d && params && packed, "decoder_pack: null argument");
+  return d->d.pack(params, packed, (hipStream_t)stream);
+}
+size_t mt_cfm_workspace_bytes(const mt_decoder* d, int B, int T, int n_timesteps, int solver) {
+  if (!d) return 0;
+  return d->d.workspace_bytes(B, T, solver == 1 ? 2 * n_timesteps : n_timesteps);
+}
+int mt_cfm_solve(const mt_decoder* d, const void* packed, const float* z_noise, float temperature,
+                 const float* mu_y, const float* mask, const float* spks, int B, int T, int n_timesteps,
+                 int solver, float* z_out, void* ws, size_t ws_bytes, void* stream) {
+  MT_REQUIRE(d && packed && z_noise && mu_y && mask && z_out && ws, "cfm_solve: null argument");
+  return d->d.solve(packed, z_noise, temperature, mu_y, mask, spks, B, T, n_timesteps, solver, z_out, ws,
+                    ws_bytes, (hipStream_t)stream);
+}
+size_t mt_decoder_step_workspace_bytes(const mt_decoder* d, int B, int T) {
+  return d ? d->d.workspace_bytes(B, T, 1) : 0;
+}
+int mt_decoder_step(const mt_decoder* d, const void* packed, const float* x, const float* mu_y,
+                    const float* mask, const float* spks, float t, int B, int T, float* out, void* ws,
+                    size_t ws_bytes, void* stream) {
+  MT_REQUIRE(d && packed && x && mu_y && mask && out && ws, "decoder_step: null argument");
+  return d->d.step(packed, x, mu_y, mask, spks, t, B, T, out, ws, ws_bytes, (hipStream_t)stream);
+}
+
+// ---- vocoder ----
+int mt_vocoder_create(int resblock, int n_ups, const int* up_rates, const int* up_kernels, int up_init,
+                      int n_kernels, const int* rb_kernels, int n_dils, const int* rb_dils, int dtype,
+                      mt_vocoder** out) {
+  MT_REQUIRE(out && up_rates && up_kernels && rb_kernels && rb_dils && n_ups > 0 && n_kernels > 0 &&
+                 n_dils > 0,
+             "vocoder_create: bad arguments");
+  std::vector<int> ur(up_rates, up_rates + n_ups), uk(up_kernels, up_kernels + n_ups);
+  std::vector<int> rk(rb_kernels, rb_kernels + n_kernels);
+  std::vector<std::vector<int>> rd;
+  for (int j = 0; j < n_kernels; ++j) rd.emplace_back(rb_dils + j * n_dils, rb_dils + (j + 1) * n_dils);
+  mt_vocoder* h = new (std::nothrow) mt_vocoder();
+  MT_REQUIRE(h, "out of host memory");
+  int rc = h->v.init(resblock, ur, uk, up_init, rk, rd, dtype);
+  if (rc) {
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return 0;
+}
+void mt_vocoder_destroy(mt_vocoder* v) { delete v; }
+int mt_vocoder_num_params(const mt_vocoder* v) { return v ? (int)v->v.params.names.size() : -1; }
+int mt_vocoder_param_name(const mt_vocoder* v, int i, char* buf, int buflen) {
+  MT_REQUIRE(v, "null vocoder");
+  return param_name(v->v.params, i, buf, buflen);
+}
+int mt_vocoder_param_shape(const mt_vocoder* v, int i, int64_t* shape, int maxdim) {
+  MT_REQUIRE(v, "null vocoder");
+  return param_shape(v->v.params, i, shape, maxdim);
+}
+size_t mt_vocoder_packed_bytes(const mt_vocoder* v) { return v ? v->v.packed_bytes : 0; }
+int mt_vocoder_pack(const mt_vocoder* v, const float* const* params, void* packed, void* stream) {
+  MT_REQUIRE(v && params && packed, "vocoder_pack: null argument");
+  return v->v.pack(params, packed, (hipStream_t)stream);
+}
+size_t mt_vocoder_workspace_bytes(const mt_vocoder* v, int B, int T) {
+  return v ? v->v.workspace_bytes(B, T) : 0;
+}
+int mt_vocoder_forward(const mt_vocoder* v, const void* packed, const float* mel, int B, int T, float* wav,
+                       void* ws, size_t ws_bytes, void* stream) {
+  MT_REQUIRE(v && packed && mel && wav && ws, "vocoder_forward: null argument");
+  return v->v.forward(packed, mel, B, T, wav, ws, ws_bytes, (hipStream_t)stream);
+}
+
+// ---- index path ----
+int mt_durations(const float* logw, const float* x_mask, float length_scale, int B, int Tx, float* w_ceil,
+                 float* cum, int64_t* y_lengths, void* stream) {
+  MT_REQUIRE(logw && x_mask && w_ceil && cum && y_lengths, "durations: null argument");
+  return mt::durations(logw, x_mask, length_scale, B, Tx, w_ceil, cum, (long long*)y_lengths,
+                       (hipStream_t)stream);
+}
+int mt_alignment(const float* cum, const int64_t* y_lengths, int B, int Tx, int T, const float* mu, int C,
+                 float* attn, float* mu_y, float* y_mask, void* stream) {
+  MT_REQUIRE(cum && (mu || !mu_y) && (y_lengths || !y_mask), "alignment: null argument");
+  return mt::alignment(cum, (const long long*)y_lengths, B, Tx, T, mu, C, attn, mu_y, y_mask,
+                       (hipStream_t)stream);
+}
+int mt_denorm_crop(const float* z, const float* mean, const float* stdv, int B, int C, int T, int Ty,
+                   float* mel, void* stream) {
+  MT_REQUIRE(z && mean && stdv && mel, "denorm_crop: null argument");
+  return mt::denorm_crop(z, mean, stdv, B, C, T, Ty, mel, (hipStream_t)stream);
+}
+
+// ---- denoiser ----
+size_t mt_denoise_workspace_bytes(int B, int L) { return mt::denoise_workspace_bytes(B, L); }
+int mt_denoise(const float* audio, int B, int L, const float* bias_spec, float strength, float* out, void* ws,
+               size_t ws_bytes, void* stream) {
+  MT_REQUIRE(audio && bias_spec && out, "denoise: null argument");
+  return mt::denoise(audio, B, L, bias_spec, strength, out, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int mt_stft_magnitude(const float* audio, int B, int L, float* mag, void* stream) {
+  MT_REQUIRE(audio && mag, "stft_magnitude: null argument");
+  return mt::stft_magnitude(audio, B, L, mag, (hipStream_t)stream);
+}
+
+// ---- op level ----
+size_t mt_op_conv1d_workspace_bytes(int dtype, int cin, int cout, int k, int stride, int transposed) {
+  mt::Packer pk;
+  const int es = dtype == MT_DTYPE_BF16 ? 2 : 4;
+  if (transposed)
+    mt::make_convT(cin, cout, k, stride, 0, 0, 1, es, pk);
+  else
+    mt::make_conv(cout, cin, k, stride, 0, 1, {0}, 1, es, pk);
+  return pk.off;
+}
+int mt_op_conv1d(int dtype, const void* x, int B, int Tin, int cin, const float* W, const float* bias,
+                 int cout, int k, int stride, int pad, int dil, int transposed, float slope, void* y, int Tout,
+                 void* ws, size_t ws_bytes, void* stream) {
+  MT_REQUIRE(x && W && y && ws, "op_conv1d: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  const int es = dtype == MT_DTYPE_BF16 ? 2 : 4;
+  mt::Packer pk;
+  mt::GemmW g = transposed ? mt::make_convT(cin, cout, k, stride, pad, 0, bias ? 1 : -1, es, pk)
+                           : mt::make_conv(cout, cin, k, stride, pad, dil, {0}, bias ? 1 : -1, es, pk);
+  MT_REQUIRE(ws_bytes >= pk.off, "op_conv1d: workspace %zu < %zu", ws_bytes, pk.off);
+  const float* params[2] = {W, bias};
+  int rc = mt::pack_gemm(g, dtype, params, (char*)ws, st);
+  if (rc) return rc;
+  mt::ConvArgs a = mt::gemm_args(g, (const char*)ws, B, Tin);
+  MT_REQUIRE(a.Tout == Tout, "op_conv1d: Tout %d != expected %d", Tout, a.Tout);
+  a.x0 = x;
+  a.y = y;
+  a.slope = slope;
+  return mt::launch_conv_op(dtype, slope >= 0.f ? mt::PF_LRELU : 0, a, st);
+}
+int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
+                    void* stream) {
+  MT_REQUIRE(qkv && mask && out, "op_attention: null argument");
+  return mt::launch_attention(dtype, qkv, mask, out, B, T, heads, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,138 @@
+// Common device/host definitions for the MI355X (gfx950) Matcha-TTS synthesis path.
+//
+// Activation layout in HBM is frame-major, channel-contiguous: [B][T][C]. A Conv1d
+// over that layout is an implicit GEMM with K = taps x C_in contiguous per tap, which
+// feeds MFMA fragments with 16-byte loads (DESIGN.md "Data layout").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mt {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+typedef __bf16 bf16;
+
+enum DType { F32 = 0, BF16 = 1 };
+
+// ---------------------------------------------------------------------------
+// element conversions
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <class T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// A 16-byte vector of T viewed as floats: bf16 -> 8 values, f32 -> 4 values.
+template <class T> struct Vec16;
+template <> struct Vec16<float> {
+  static constexpr int N = 4;
+  f32x4 v;
+  __device__ __forceinline__ float get(int i) const { return v[i]; }
+  __device__ __forceinline__ void set(int i, float x) { v[i] = x; }
+};
+template <> struct Vec16<bf16> {
+  static constexpr int N = 8;
+  bf16x8 v;
+  __device__ __forceinline__ float get(int i) const { return (float)v[i]; }
+  __device__ __forceinline__ void set(int i, float x) { v[i] = (bf16)x; }
+};
+
+template <class T>
+__device__ __forceinline__ Vec16<T> load16(const T* p) {
+  Vec16<T> r;
+  r.v = *reinterpret_cast<const decltype(r.v)*>(p);
+  return r;
+}
+template <class T>
+__device__ __forceinline__ void store16(T* p, const Vec16<T>& r) {
+  *reinterpret_cast<decltype(r.v)*>(p) = r.v;
+}
+template <class T>
+__device__ __forceinline__ Vec16<T> zero16() {
+  Vec16<T> r;
+#pragma unroll
+  for (int i = 0; i < Vec16<T>::N; ++i) r.set(i, 0.f);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// MFMA: one 16-byte fragment pair (A row-slab, B col-slab) of 64 bytes of K per row.
+//   bf16: v_mfma_f32_16x16x32_bf16 — lane l holds A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15]
+//   f32 : v_mfma_f32_16x16x4_f32 x4 — lane group g=l>>4 supplies k = 4g+s on step s, i.e.
+//         the 16 channels of a 64-byte chunk are visited in the permuted order
+//         {s, 4+s, 8+s, 12+s}; A and B use the same permutation so the sum is the same.
+// C/D: col = l&15, row = 4(l>>4)+i (cdna_hip_programming.md §3).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(const f32x4& a, const f32x4& b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+  return c;
+}
+
+// channels per 64-byte K chunk
+template <class T> struct Chunk { static constexpr int CH = 64 / sizeof(T); };
+
+// ---------------------------------------------------------------------------
+// math helpers (reference semantics: torch.nn.Mish, F.leaky_relu, SiLU)
+// ---------------------------------------------------------------------------
+// mish(x) = x * tanh(softplus(x)); with e = exp(x): tanh(log1p(e)) = e(e+2) / (e(e+2)+2).
+// torch's softplus uses threshold 20 (returns x), where tanh(.) == 1 in fp32 anyway.
+__device__ __forceinline__ float mish_f(float x) {
+  if (x > 20.f) return x;
+  float e = __expf(x);
+  float n = e * (e + 2.f);
+  return x * __fdividef(n, n + 2.f);
+}
+__device__ __forceinline__ float lrelu_f(float x, float slope) { return x > 0.f ? x : x * slope; }
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace mt
+
+// ---------------------------------------------------------------------------
+// error plumbing shared by the C ABI
+// ---------------------------------------------------------------------------
+namespace mt {
+void set_error(const char* fmt, ...);
+}
+#define MT_CHECK_HIP(expr)                                                         \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) {                                                        \
+      ::mt::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),       \
+                      __FILE__, __LINE__);                                         \
+      return -(int)_e - 1000;                                                      \
+    }                                                                              \
+  } while (0)
+#define MT_REQUIRE(cond, ...)                                                      \
+  do {                                                                             \
+    if (!(cond)) {                                                                 \
+      ::mt::set_error(__VA_ARGS__);                                                \
+      return -1;                                                                   \
+    }                                                                              \
+  } while (0)

@@ -1,0 +1,486 @@
+// Implicit-GEMM Conv1d kernel for gfx950 (see mt_conv.h for the op coverage).
+//
+// Workgroup = 256 threads = 4 waves (wave64). Tile = BM output rows x BN output positions.
+// Per K-stage (one 64-byte channel chunk = 32 bf16 / 16 f32 channels, and a group of up to
+// TG taps) the workgroup stages into LDS
+//   Ws[tap][BM][64B]   packed weight rows,
+//   Xs[RB][64B]        the input frames the tile needs for all taps of the group (halo
+//                      included), with the prologue transform applied once per element,
+// then every wave issues FM x FN MFMAs per tap (bf16: v_mfma_f32_16x16x32_bf16, f32: 4 x
+// v_mfma_f32_16x16x4_f32 = an exact fp32 fmaf chain). LDS rows are padded to 80 bytes so the
+// 16-lane ds_read_b128 groups hit 16 distinct 4-bank slots (conflict-free).
+#include "mt_conv.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace mt {
+
+static constexpr int ROWB = 80;
+
+template <class E>
+__device__ __forceinline__ float mish_e(float x) {
+  if constexpr (std::is_same<E, float>::value) {
+    if (x > 20.f) return x;
+    const float e = expf(x);
+    const float n = e * (e + 2.f);
+    return x * (n / (n + 2.f));
+  } else {
+    return mish_f(x);
+  }
+}
+
+// TAG only renames the symbol: TAG=1 is the op-level entry (mt_op_conv1d) used by bench.py's
+// roofline leg, so its launches get their own rocprof row; the code is identical.
+template <class E, int BM, int BN, int WAVES_M, int PF, int EF, int TAG = 0>
+__global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int tg_max) {
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int FM = WM / 16, FN = WN / 16;
+  constexpr int CH = Chunk<E>::CH;
+  constexpr int VN = Vec16<E>::N;
+  static_assert(CH / VN == 4, "64-byte chunk = 4 x 16-byte vectors");
+  constexpr bool NEED_GN = (PF & PF_GN) || (EF & EF_GNADD);
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+  const int ntiles = (a.Ncols + BN - 1) / BN;
+  const int b = blockIdx.x / ntiles, nt = blockIdx.x - b * ntiles;
+  const int n0 = nt * BN, m0 = blockIdx.y * BM;
+
+  const int RBmax = (BN - 1) * a.stride + (tg_max - 1) * a.dil + 1;
+  char* Ws = smem;
+  char* Xs = smem + tg_max * BM * ROWB;
+  float* ga = reinterpret_cast<float*>(Xs + RBmax * ROWB);  // [256]
+  float* gsh = ga + 256;                                     // [256]
+  float* lnm = gsh + 256;                                    // [BN]
+  float* lnr = lnm + BN;                                     // [BN]
+
+  // ---- pre-phase: GroupNorm coefficients for utterance b (merged tile partials) ----
+  if constexpr (NEED_GN) {
+    const int C = (PF & PF_GN) ? a.cin : a.cout;
+    const int G = C >> 5;
+    if (tid < G) {
+      const double* p = a.gn_in + (size_t)(b * G + tid) * a.gn_ntiles * 2;
+      double s1 = 0.0, s2 = 0.0;
+      for (int i = 0; i < a.gn_ntiles; ++i) {
+        s1 += p[2 * i];
+        s2 += p[2 * i + 1];
+      }
+      const double n = 32.0 * (double)a.gn_T;
+      const double mean = s1 / n;
+      double var = s2 / n - mean * mean;
+      var = var < 0.0 ? 0.0 : var;
+      lnm[tid] = (float)mean;
+      lnr[tid] = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+      const int g = c >> 5;
+      const float sc = lnr[g] * a.gn_g[c];
+      ga[c] = sc;
+      gsh[c] = -sc * lnm[g] + a.gn_b[c];
+    }
+    __syncthreads();
+  }
+
+  // ---- pre-phase: LayerNorm row statistics (k=1 GEMMs only: rows n0..n0+BN-1) ----
+  if constexpr (PF & PF_LN) {
+    const E* x0 = reinterpret_cast<const E*>(a.x0);
+    for (int r = wave; r < BN; r += 4) {
+      const int f = n0 + r;
+      float mean = 0.f, rstd = 0.f;
+      if (f < a.Tin) {
+        const E* row = x0 + (size_t)(b * a.Tin + f) * a.cin;
+        float xv[8];
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int c = lane + i * 64;
+          xv[i] = (c < a.cin) ? to_f(row[c]) : 0.f;
+          s += xv[i];
+        }
+        mean = wave_sum(s) / (float)a.cin;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int c = lane + i * 64;
+          const float d = xv[i] - mean;
+          q += (c < a.cin) ? d * d : 0.f;
+        }
+        const float var = wave_sum(q) / (float)a.cin;
+        rstd = 1.f / sqrtf(var + a.ln_eps);
+      }
+      if (lane == 0) {
+        lnm[r] = mean;
+        lnr[r] = rstd;
+      }
+    }
+    __syncthreads();
+  }
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const E* x0p = reinterpret_cast<const E*>(a.x0);
+  const E* x1p = reinterpret_cast<const E*>(a.x1);
+  const E* wp = reinterpret_cast<const E*>(a.w);
+  const int c1 = a.cin - a.c0;
+  const int nchunks = a.cin_pad / CH;
+
+  for (int tg0 = 0; tg0 < a.taps; tg0 += tg_max) {
+    const int ntg = min(tg_max, a.taps - tg0);
+    const int RB = (BN - 1) * a.stride + (ntg - 1) * a.dil + 1;
+    const int fbase = n0 * a.stride - a.pad + tg0 * a.dil;
+    for (int c = 0; c < nchunks; ++c) {
+      const int cbase = c * CH;
+      // ---- stage input rows (+prologue) ----
+      for (int v = tid; v < RB * 4; v += 256) {
+        const int r = v >> 2, s = v & 3;
+        const int f = fbase + r;
+        const int ch = cbase + s * VN;
+        Vec16<E> val = zero16<E>();
+        if (f >= 0 && f < a.Tin && ch < a.cin) {
+          const size_t row = (size_t)b * a.Tin + f;
+          const E* src = (ch < a.c0) ? x0p + row * a.c0 + ch : x1p + row * c1 + (ch - a.c0);
+          val = load16(src);
+          if constexpr (PF != 0) {
+            float mk = 1.f, lm = 0.f, lr = 1.f;
+            if constexpr ((PF & PF_MASK) != 0) mk = a.pmask[row];
+            if constexpr ((PF & PF_LN) != 0) {
+              lm = lnm[f - n0];
+              lr = lnr[f - n0];
+            }
+#pragma unroll
+            for (int i = 0; i < VN; ++i) {
+              float x = val.get(i);
+              const int cc = ch + i;
+              if constexpr ((PF & PF_LN) != 0) x = (x - lm) * lr * a.ln_g[cc] + a.ln_b[cc];
+              if constexpr ((PF & PF_GN) != 0) x = mish_e<E>(x * ga[cc] + gsh[cc]);
+              if constexpr ((PF & PF_TB) != 0) x = x + a.tb[cc];
+              if constexpr ((PF & PF_LRELU) != 0) x = lrelu_f(x, a.slope);
+              if constexpr ((PF & PF_MASK) != 0) x = x * mk;
+              val.set(i, x);
+            }
+          }
+        }
+        store16(reinterpret_cast<E*>(Xs + r * ROWB + s * 16), val);
+      }
+      // ---- stage weight rows for the taps of this group ----
+      for (int v = tid; v < ntg * BM * 4; v += 256) {
+        const int rr = v >> 2, s = v & 3;
+        const int t = rr / BM, m = rr - t * BM;
+        Vec16<E> val = zero16<E>();
+        if (m0 + m < a.Mpad)
+          val = load16(wp + ((size_t)(m0 + m) * a.taps + (tg0 + t)) * a.cin_pad + cbase + s * VN);
+        store16(reinterpret_cast<E*>(Ws + rr * ROWB + s * 16), val);
+      }
+      __syncthreads();
+      // ---- MFMA over the taps of this group ----
+      for (int t = 0; t < ntg; ++t) {
+        Vec16<E> af[FM], bfg[FN];
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+          af[fm] = load16(reinterpret_cast<const E*>(
+              Ws + (t * BM + wm * WM + fm * 16 + (lane & 15)) * ROWB + (lane >> 4) * 16));
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int col = wn * WN + fn * 16 + (lane & 15);
+          bfg[fn] = load16(reinterpret_cast<const E*>(
+              Xs + (col * a.stride + t * a.dil) * ROWB + (lane >> 4) * 16));
+        }
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(af[fm].v, bfg[fn].v, acc[fm][fn]);
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue ----
+  double g1[FM], g2[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) g1[i] = g2[i] = 0.0;
+
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int mr = m0 + wm * WM + fm * 16 + 4 * (lane >> 4);
+      const int n = n0 + wn * WN + fn * 16 + (lane & 15);
+      if (n >= a.Ncols || mr >= a.M) continue;
+      const int ph = mr / a.cout;
+      const int ch = mr - ph * a.cout;
+      const int fr = n * a.ups + ph - a.opad;
+      if (fr < 0 || fr >= a.Tout) continue;
+      const size_t orow = (size_t)b * a.Tout + fr;
+      float em = 1.f;
+      if constexpr ((EF & (EF_MASK | EF_GNADD)) != 0) em = a.emask[orow];
+      bool ok[4];
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ok[r] = (mr + r) < a.M;
+        v[r] = acc[fm][fn][r] + (ok[r] ? a.bias[mr + r] : 0.f);
+      }
+      if constexpr ((EF & EF_SNAKE) != 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (!ok[r]) continue;
+          const float sn = sinf(v[r] * a.snake_alpha[ch + r]);
+          v[r] = v[r] + a.snake_ibeta[ch + r] * (sn * sn);
+        }
+      }
+      if constexpr ((EF & EF_GNSTATS) != 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (ok[r]) {
+            g1[fm] += (double)v[r];
+            g2[fm] += (double)v[r] * (double)v[r];
+          }
+      }
+      if constexpr ((EF & EF_GNADD) != 0) {
+        const E* gy = reinterpret_cast<const E*>(a.gy) + orow * a.cout + ch;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (ok[r]) v[r] = mish_e<E>(to_f(gy[r]) * ga[ch + r] + gsh[ch + r]) * em + v[r];
+      }
+      if constexpr ((EF & EF_MASK) != 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] * em;
+      }
+      if constexpr ((EF & EF_RESID) != 0) {
+        const E* rp = reinterpret_cast<const E*>(a.resid) + orow * a.ldr + ch;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (ok[r]) v[r] = v[r] + to_f(rp[r]);
+      }
+      if constexpr ((EF & EF_ACCUM) != 0) {
+        const E* yp = reinterpret_cast<const E*>(a.y) + orow * a.ldy + ch;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (ok[r]) v[r] = to_f(yp[r]) + v[r];
+      }
+      if constexpr ((EF & EF_DIV) != 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] / a.div;
+      }
+      if constexpr ((EF & EF_TANH) != 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = tanhf(v[r]);
+      }
+      if constexpr ((EF & EF_EULER) != 0) {
+        E* xz = reinterpret_cast<E*>(a.xin_z) + orow * a.ld_xin + ch;
+        float* zp = a.zmaster + orow * a.cout + ch;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (!ok[r]) continue;
+          float inc = v[r] * a.dt;
+          if (a.half_step) inc = inc * 0.5f;
+          const float zn = zp[r] + inc;
+          if (a.update_master) zp[r] = zn;
+          xz[r] = from_f<E>(zn);
+        }
+      } else if constexpr ((EF & EF_OUTF32) != 0) {
+        float* yp = reinterpret_cast<float*>(a.y) + orow * a.ldy + ch;
+        if (ok[3] && ((a.ldy & 3) == 0)) {
+          *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (ok[r]) yp[r] = v[r];
+        }
+      } else {
+        E* yp = reinterpret_cast<E*>(a.y) + orow * a.ldy + ch;
+        if constexpr (std::is_same<E, float>::value) {
+          if (ok[3] && ((a.ldy & 3) == 0)) {
+            *reinterpret_cast<f32x4*>(yp) = f32x4{v[0], v[1], v[2], v[3]};
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (ok[r]) yp[r] = v[r];
+          }
+        } else {
+          if (ok[3] && ((a.ldy & 3) == 0)) {
+            bf16x4 o;
+            o[0] = (bf16)v[0];
+            o[1] = (bf16)v[1];
+            o[2] = (bf16)v[2];
+            o[3] = (bf16)v[3];
+            *reinterpret_cast<bf16x4*>(yp) = o;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (ok[r]) yp[r] = (bf16)v[r];
+          }
+        }
+      }
+    }
+  }
+
+  // ---- GroupNorm partial statistics of this tile: [b][group][nt] ----
+  if constexpr ((EF & EF_GNSTATS) != 0) {
+    static_assert(WM >= 32, "GN stats need >= 32 rows per wave");
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(smem);  // [4][FM][2]
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const double s1 = wave_sum_d(g1[fm]);
+      const double s2 = wave_sum_d(g2[fm]);
+      if (lane == 0) {
+        red[(wave * FM + fm) * 2] = s1;
+        red[(wave * FM + fm) * 2 + 1] = s2;
+      }
+    }
+    __syncthreads();
+    constexpr int LG = BM / 32;
+    if (tid < LG) {
+      const int wmg = (tid * 32) / WM;
+      const int fmg = ((tid * 32) % WM) / 16;
+      double s1 = 0.0, s2 = 0.0;
+      for (int w2 = 0; w2 < WAVES_N; ++w2) {
+        const int wv = wmg + w2 * WAVES_M;
+        for (int q = 0; q < 2; ++q) {
+          s1 += red[(wv * FM + fmg + q) * 2];
+          s2 += red[(wv * FM + fmg + q) * 2 + 1];
+        }
+      }
+      const int G = a.M >> 5;
+      const int g = (m0 >> 5) + tid;
+      if (g < G) {
+        double* o = a.gn_out + ((size_t)(b * G + g) * ntiles + nt) * 2;
+        o[0] = s1;
+        o[1] = s2;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------
+enum : int { CFG_128x128 = 1, CFG_128x64 = 2, CFG_64x128 = 4, CFG_32x256 = 8, CFG_16x256 = 16 };
+
+template <class E, int BM, int BN, int WAVES_M, int PF, int EF, int TAG = 0>
+static int launch_tile(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
+  const int tgmax = BM >= 256 ? 2 : 4;
+  const int tg = std::min(a.taps, tgmax);
+  const int RBmax = (BN - 1) * a.stride + (tg - 1) * a.dil + 1;
+  size_t lds = (size_t)tg * BM * ROWB + (size_t)RBmax * ROWB + (512 + 2 * BN) * sizeof(float);
+  lds = std::max(lds, (size_t)4 * 8 * 2 * sizeof(double));
+  MT_REQUIRE(lds <= 65536, "conv: LDS request %zu too large (taps %d dil %d stride %d)", lds, a.taps,
+             a.dil, a.stride);
+  const int ntiles = (a.Ncols + BN - 1) / BN;
+  dim3 grid((unsigned)(ntiles * a.B), (unsigned)((a.M + BM - 1) / BM));
+  hipLaunchKernelGGL((conv_kernel<E, BM, BN, WAVES_M, PF, EF, TAG>), grid, dim3(256), lds, stream, a, tg);
+  MT_CHECK_HIP(hipGetLastError());
+  if (ntiles_out) *ntiles_out = ntiles;
+  return 0;
+}
+
+static int check_args(const ConvArgs& a, int esize, int pf, int ef) {
+  const int VN = 16 / esize, CH = 64 / esize;
+  MT_REQUIRE(a.B > 0 && a.Tin > 0 && a.Tout > 0 && a.Ncols > 0, "conv: empty geometry");
+  MT_REQUIRE(a.cin % VN == 0 && a.c0 % VN == 0 && a.c0 <= a.cin && a.c0 > 0,
+             "conv: channel split %d/%d not 16-byte aligned", a.c0, a.cin);
+  MT_REQUIRE(a.cin_pad % CH == 0 && a.cin_pad >= a.cin, "conv: cin_pad %d", a.cin_pad);
+  MT_REQUIRE(a.Mpad >= a.M && a.M > 0 && a.cout > 0 && a.M % a.cout == 0, "conv: M %d cout %d", a.M,
+             a.cout);
+  MT_REQUIRE(a.taps >= 1 && a.dil >= 1 && a.stride >= 1 && a.ups >= 1, "conv: taps/dil/stride");
+  MT_REQUIRE(a.x0 && a.w && a.bias && (a.y || (ef & EF_EULER)), "conv: null pointer");
+  MT_REQUIRE(a.c0 == a.cin || a.x1, "conv: second source missing");
+  if (pf & PF_LN) MT_REQUIRE(a.taps == 1 && a.stride == 1 && a.pad == 0 && a.c0 == a.cin && a.cin <= 512,
+                             "conv: LN prologue needs a single-source 1x1 GEMM with cin<=512");
+  if (pf & PF_GN) MT_REQUIRE(a.cin <= 256 && a.cin % 32 == 0 && a.gn_in, "conv: GN prologue");
+  if (ef & EF_GNADD) MT_REQUIRE(a.cout <= 256 && a.cout % 32 == 0 && a.gn_in && a.gy, "conv: GN epilogue");
+  if (ef & EF_GNSTATS) MT_REQUIRE(a.M % 32 == 0 && a.gn_out && a.ups == 1, "conv: GN stats");
+  if (pf & PF_MASK) MT_REQUIRE(a.pmask, "conv: pmask");
+  if (ef & (EF_MASK | EF_GNADD)) MT_REQUIRE(a.emask, "conv: emask");
+  if (ef & EF_RESID) MT_REQUIRE(a.resid, "conv: resid");
+  if (ef & EF_EULER) MT_REQUIRE(a.zmaster && a.xin_z, "conv: euler buffers");
+  if (ef & EF_SNAKE) MT_REQUIRE(a.snake_alpha && a.snake_ibeta, "conv: snake params");
+  return 0;
+}
+
+template <class E, int PF, int EF, int CFGS, int TAG = 0>
+static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
+  int rc = check_args(a, (int)sizeof(E), PF, EF);
+  if (rc) return rc;
+  const int M = a.M;
+  auto wgs = [&](int bm, int bn) {
+    return (long)a.B * ((a.Ncols + bn - 1) / bn) * ((M + bm - 1) / bm);
+  };
+  if constexpr ((CFGS & CFG_16x256) != 0)
+    if (M <= 16) return launch_tile<E, 16, 256, 1, PF, EF, TAG>(a, stream, ntiles_out);
+  if constexpr ((CFGS & CFG_32x256) != 0)
+    if (M <= 32) return launch_tile<E, 32, 256, 1, PF, EF, TAG>(a, stream, ntiles_out);
+  if constexpr ((CFGS & CFG_64x128) != 0)
+    if (M <= 64) return launch_tile<E, 64, 128, 1, PF, EF, TAG>(a, stream, ntiles_out);
+  if constexpr ((CFGS & CFG_128x128) != 0 && (CFGS & CFG_128x64) != 0) {
+    if (wgs(128, 128) >= 1024) return launch_tile<E, 128, 128, 2, PF, EF, TAG>(a, stream, ntiles_out);
+    return launch_tile<E, 128, 64, 2, PF, EF, TAG>(a, stream, ntiles_out);
+  } else if constexpr ((CFGS & CFG_128x128) != 0) {
+    return launch_tile<E, 128, 128, 2, PF, EF, TAG>(a, stream, ntiles_out);
+  } else if constexpr ((CFGS & CFG_128x64) != 0) {
+    return launch_tile<E, 128, 64, 2, PF, EF, TAG>(a, stream, ntiles_out);
+  }
+  set_error("conv: no tile configuration for M=%d (pf %d ef %d)", M, PF, EF);
+  return -1;
+}
+
+// (PF, EF, tile configs) combinations used by the decoder and the vocoder.
+#define MT_CONV_COMBOS(X)                                                              \
+  X(PF_MASK, EF_GNSTATS, CFG_128x128 | CFG_128x64)                                     \
+  X(PF_GN | PF_TB | PF_MASK, EF_GNSTATS, CFG_128x128 | CFG_128x64)                     \
+  X(PF_MASK, EF_GNADD, CFG_128x128 | CFG_128x64)                                       \
+  X(PF_LN, 0, CFG_128x128 | CFG_128x64)                                                \
+  X(0, EF_RESID, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256)                   \
+  X(PF_LN, EF_SNAKE, CFG_128x128 | CFG_128x64)                                         \
+  X(PF_MASK, 0, CFG_128x128 | CFG_128x64)                                              \
+  X(PF_GN | PF_MASK, EF_MASK | EF_EULER, CFG_128x128 | CFG_128x64)                     \
+  X(0, 0, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256 | CFG_16x256)             \
+  X(PF_LRELU, 0, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256 | CFG_16x256)      \
+  X(PF_LRELU, EF_RESID, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256)            \
+  X(PF_LRELU, EF_RESID | EF_ACCUM, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256) \
+  X(PF_LRELU, EF_RESID | EF_ACCUM | EF_DIV,                                            \
+    CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256)                                \
+  X(PF_LRELU, EF_RESID | EF_DIV, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256)   \
+  X(PF_LRELU, EF_TANH | EF_OUTF32, CFG_16x256 | CFG_32x256)
+
+#define MT_DEFINE_LAUNCH(PFV, EFV, CFGV)                                                    \
+  template <>                                                                             \
+  int launch_conv<float, (PFV), (EFV)>(const ConvArgs& a, hipStream_t s, int* nt) {        \
+    return launch_sel<float, (PFV), (EFV), (CFGV)>(a, s, nt);                              \
+  }                                                                                       \
+  template <>                                                                             \
+  int launch_conv<bf16, (PFV), (EFV)>(const ConvArgs& a, hipStream_t s, int* nt) {         \
+    return launch_sel<bf16, (PFV), (EFV), (CFGV)>(a, s, nt);                               \
+  }
+MT_CONV_COMBOS(MT_DEFINE_LAUNCH)
+
+int launch_conv_op(int dtype, int pf, const ConvArgs& a, hipStream_t stream) {
+  constexpr int ALL = CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256 | CFG_16x256;
+  if (pf == PF_LRELU)
+    return dtype == BF16 ? launch_sel<bf16, PF_LRELU, 0, ALL, 1>(a, stream, nullptr)
+                         : launch_sel<float, PF_LRELU, 0, ALL, 1>(a, stream, nullptr);
+  return dtype == BF16 ? launch_sel<bf16, 0, 0, ALL, 1>(a, stream, nullptr)
+                       : launch_sel<float, 0, 0, ALL, 1>(a, stream, nullptr);
+}
+
+int launch_conv_dyn(int dtype, int pf, int ef, const ConvArgs& a, hipStream_t stream, int* nt) {
+#define MT_DYN_CASE(PFV, EFV, CFGV)                                                        \
+  if (pf == (PFV) && ef == (EFV))                                                          \
+    return dtype == BF16 ? launch_conv<bf16, (PFV), (EFV)>(a, stream, nt)                   \
+                         : launch_conv<float, (PFV), (EFV)>(a, stream, nt);
+  MT_CONV_COMBOS(MT_DYN_CASE)
+#undef MT_DYN_CASE
+  set_error("conv: prologue/epilogue combination pf=%d ef=%d is not compiled in", pf, ef);
+  return -1;
+}
+
+}  // namespace mt

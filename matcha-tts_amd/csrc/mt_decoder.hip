@@ -1,0 +1,625 @@
+// U-Net estimator + CFM ODE solver driver (model.py:834-1048, 1084-1109).
+//
+// One estimator evaluation = 54 kernel launches on the caller's stream (all activations
+// [B][T][C] in the element type, GN/LN statistics and the Euler state in fp32):
+//   ResnetBlock1D  = K1 conv3(x*m)+GN-partials | K2 conv3((mish(GN(y1))+tb)*m)+GN-partials |
+//                    K3 res1x1(x*m) + mish(GN(y2))*m
+//   Transformer    = QKV(LN1 prologue) | attention | out-proj(+x) | FF1(LN3, SnakeBeta) | FF2(+x)
+//   final          = final_block conv3 + GN-partials | final_proj(mish(GN)*m)*m fused with the
+//                    Euler/midpoint update z += pred*dt written to the fp32 master and to the
+//                    estimator input slot for the next evaluation.
+#include <math.h>
+
+#include <algorithm>
+
+#include "mt_model.h"
+
+namespace mt {
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+GemmW make_conv(int cout, int cin, int k, int stride, int pad, int dil, std::vector<int> w, int b,
+                int esize, Packer& pk) {
+  GemmW g;
+  g.kind = 0;
+  g.cin = cin;
+  g.cout = cout;
+  g.k = k;
+  g.s = stride;
+  g.pad = pad;
+  g.dil = dil;
+  g.M = cout;
+  g.Mpad = round_up(cout, 16);
+  g.taps = k;
+  g.cin_pad = round_up(cin, 64 / esize);
+  g.gpad = pad;
+  g.ups = 1;
+  g.opad = 0;
+  g.wsrc = std::move(w);
+  g.bsrc = b;
+  g.w_off = pk.take((size_t)g.Mpad * g.taps * g.cin_pad * esize);
+  g.b_off = pk.take((size_t)g.M * sizeof(float));
+  return g;
+}
+
+GemmW make_convT(int cin, int cout, int k, int s, int pad, int w, int b, int esize, Packer& pk) {
+  GemmW g;
+  g.kind = 1;
+  g.cin = cin;
+  g.cout = cout;
+  g.k = k;
+  g.s = s;
+  g.pad = pad;
+  g.dil = 1;
+  g.M = s * cout;
+  g.Mpad = round_up(g.M, 16);
+  g.taps = k / s;
+  g.cin_pad = round_up(cin, 64 / esize);
+  g.gpad = g.taps - 1;
+  g.ups = s;
+  g.opad = pad;
+  g.wsrc = {w};
+  g.bsrc = b;
+  g.w_off = pk.take((size_t)g.Mpad * g.taps * g.cin_pad * esize);
+  g.b_off = pk.take((size_t)g.M * sizeof(float));
+  return g;
+}
+
+int pack_gemm(const GemmW& g, int dtype, const float* const* params, char* P, hipStream_t st) {
+  int rc;
+  void* wdst = P + g.w_off;
+  if (g.kind == 0) {
+    const int rows_per = g.cout / (int)g.wsrc.size();
+    for (size_t i = 0; i < g.wsrc.size(); ++i) {
+      rc = pack_conv(dtype, params[g.wsrc[i]], 0, rows_per, g.cin, g.k, 1, (int)i * rows_per, rows_per,
+                     g.Mpad, g.taps, g.cin_pad, wdst, st);
+      if (rc) return rc;
+    }
+    const int rest = g.Mpad - g.cout;  // zero pad rows
+    if (rest > 0) {
+      rc = pack_conv(dtype, nullptr, 0, 0, g.cin, g.k, 1, g.cout, rest, g.Mpad, g.taps, g.cin_pad, wdst, st);
+      if (rc) return rc;
+    }
+  } else {
+    rc = pack_conv(dtype, params[g.wsrc[0]], 1, g.cout, g.cin, g.k, g.s, 0, g.Mpad, g.Mpad, g.taps,
+                   g.cin_pad, wdst, st);
+    if (rc) return rc;
+  }
+  return pack_vec(g.bsrc >= 0 ? params[g.bsrc] : nullptr, g.cout, g.M, 0, (float*)(P + g.b_off), st);
+}
+
+void gemm_geom(const GemmW& g, int Tin, int* Tout, int* Ncols) {
+  if (g.kind == 0) {
+    *Tout = (Tin + 2 * g.pad - g.dil * (g.k - 1) - 1) / g.s + 1;
+    *Ncols = *Tout;
+  } else {
+    *Tout = (Tin - 1) * g.s - 2 * g.pad + g.k;
+    *Ncols = (*Tout - 1 + g.pad) / g.s + 1;
+  }
+}
+
+ConvArgs gemm_args(const GemmW& g, const char* P, int B, int Tin) {
+  ConvArgs a{};
+  a.B = B;
+  a.Tin = Tin;
+  a.c0 = a.cin = g.cin;
+  a.w = P + g.w_off;
+  a.bias = (const float*)(P + g.b_off);
+  a.M = g.M;
+  a.Mpad = g.Mpad;
+  a.cout = g.cout;
+  a.taps = g.taps;
+  a.dil = g.dil;
+  a.pad = g.gpad;
+  a.stride = g.kind == 0 ? g.s : 1;
+  a.cin_pad = g.cin_pad;
+  a.ups = g.ups;
+  a.opad = g.opad;
+  gemm_geom(g, Tin, &a.Tout, &a.Ncols);
+  a.ldy = g.cout;
+  a.slope = 0.1f;
+  a.ln_eps = 1e-5f;
+  a.gn_eps = 1e-5f;
+  a.div = 1.f;
+  return a;
+}
+
+// -------------------------------------------------------------------------------------
+int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_) {
+  MT_REQUIRE(c_cond_ % 32 == 0 && c_cond_ >= 160, "decoder: c_cond %d must be a multiple of 32 >= 160",
+             c_cond_);
+  MT_REQUIRE(n_mid_ >= 0 && n_blocks_ >= 1 && heads_ >= 1 && heads_ <= 8, "decoder: bad config");
+  MT_REQUIRE(dtype_ == F32 || dtype_ == BF16, "decoder: dtype");
+  c_cond = c_cond_;
+  n_mid = n_mid_;
+  n_blocks = n_blocks_;
+  heads = heads_;
+  dtype = dtype_;
+  esize = dtype == BF16 ? 2 : 4;
+  inner = heads * 64;
+  n_res = 4 + n_mid;
+  Packer pk;
+  ParamList& L = params;
+  L = ParamList();
+  res.clear();
+  tbs.clear();
+  const long long Cc = c_cond;
+
+  t1w = L.add("time_mlp.linear_1.weight", {TE, Cc});
+  t1b = L.add("time_mlp.linear_1.bias", {TE});
+  t2w = L.add("time_mlp.linear_2.weight", {TE, TE});
+  t2b = L.add("time_mlp.linear_2.bias", {TE});
+  freq = L.add("_sinus_freq", {Cc / 2});  // exp(arange(half) * -ln(1e4)/(half-1)), host-computed
+  t1w_off = pk.take((size_t)TE * Cc * 4);
+  t1b_off = pk.take(TE * 4);
+  t2w_off = pk.take((size_t)TE * TE * 4);
+  t2b_off = pk.take(TE * 4);
+  freq_off = pk.take(Cc / 2 * 4);
+
+  auto add_res = [&](const std::string& p, int dim_in) {
+    Res R;
+    R.dim_in = dim_in;
+    R.mlp_w = L.add(p + ".mlp.1.weight", {C, TE});
+    R.mlp_b = L.add(p + ".mlp.1.bias", {C});
+    int w1 = L.add(p + ".block1.block.0.weight", {C, dim_in, 3});
+    int b1 = L.add(p + ".block1.block.0.bias", {C});
+    R.gn1g = L.add(p + ".block1.block.1.weight", {C});
+    R.gn1b = L.add(p + ".block1.block.1.bias", {C});
+    int w2 = L.add(p + ".block2.block.0.weight", {C, C, 3});
+    int b2 = L.add(p + ".block2.block.0.bias", {C});
+    R.gn2g = L.add(p + ".block2.block.1.weight", {C});
+    R.gn2b = L.add(p + ".block2.block.1.bias", {C});
+    int wr = L.add(p + ".res_conv.weight", {C, dim_in, 1});
+    int br = L.add(p + ".res_conv.bias", {C});
+    R.c1 = make_conv(C, dim_in, 3, 1, 1, 1, {w1}, b1, esize, pk);
+    R.c2 = make_conv(C, C, 3, 1, 1, 1, {w2}, b2, esize, pk);
+    R.res = make_conv(C, dim_in, 1, 1, 0, 1, {wr}, br, esize, pk);
+    R.gn1_off = pk.take(2 * C * 4);
+    R.gn2_off = pk.take(2 * C * 4);
+    R.mlp_w_off = pk.take((size_t)C * TE * 4);
+    R.mlp_b_off = pk.take(C * 4);
+    res.push_back(R);
+  };
+  auto add_tbs = [&](const std::string& p) {
+    std::vector<TB> v;
+    for (int j = 0; j < n_blocks; ++j) {
+      const std::string q = p + "." + std::to_string(j);
+      TB t;
+      t.ln1g = L.add(q + ".norm1.weight", {C});
+      t.ln1b = L.add(q + ".norm1.bias", {C});
+      int wq = L.add(q + ".attn1.to_q.weight", {inner, C});
+      int wk = L.add(q + ".attn1.to_k.weight", {inner, C});
+      int wv = L.add(q + ".attn1.to_v.weight", {inner, C});
+      int wo = L.add(q + ".attn1.to_out.0.weight", {C, inner});
+      int bo = L.add(q + ".attn1.to_out.0.bias", {C});
+      t.ln3g = L.add(q + ".norm3.weight", {C});
+      t.ln3b = L.add(q + ".norm3.bias", {C});
+      int w1 = L.add(q + ".ff.net.0.proj.weight", {TE, C});
+      int b1 = L.add(q + ".ff.net.0.proj.bias", {TE});
+      t.alpha = L.add(q + ".ff.net.0.alpha", {TE});
+      t.beta = L.add(q + ".ff.net.0.beta", {TE});
+      int w2 = L.add(q + ".ff.net.2.weight", {C, TE});
+      int b2 = L.add(q + ".ff.net.2.bias", {C});
+      t.qkv = make_conv(3 * inner, C, 1, 1, 0, 1, {wq, wk, wv}, -1, esize, pk);
+      t.out = make_conv(C, inner, 1, 1, 0, 1, {wo}, bo, esize, pk);
+      t.ff1 = make_conv(TE, C, 1, 1, 0, 1, {w1}, b1, esize, pk);
+      t.ff2 = make_conv(C, TE, 1, 1, 0, 1, {w2}, b2, esize, pk);
+      t.ln1_off = pk.take(2 * C * 4);
+      t.ln3_off = pk.take(2 * C * 4);
+      t.snake_off = pk.take(2 * TE * 4);
+      v.push_back(t);
+    }
+    tbs.push_back(v);
+  };
+
+  // down blocks (channels = (256, 256))
+  add_res("down_blocks.0.0", c_cond);
+  add_tbs("down_blocks.0.1");
+  {
+    int w = L.add("down_blocks.0.2.conv.weight", {C, C, 3});
+    int b = L.add("down_blocks.0.2.conv.bias", {C});
+    down0 = make_conv(C, C, 3, 2, 1, 1, {w}, b, esize, pk);
+  }
+  add_res("down_blocks.1.0", C);
+  add_tbs("down_blocks.1.1");
+  {
+    int w = L.add("down_blocks.1.2.weight", {C, C, 3});
+    int b = L.add("down_blocks.1.2.bias", {C});
+    down1 = make_conv(C, C, 3, 1, 1, 1, {w}, b, esize, pk);
+  }
+  for (int i = 0; i < n_mid; ++i) {
+    add_res("mid_blocks." + std::to_string(i) + ".0", C);
+    add_tbs("mid_blocks." + std::to_string(i) + ".1");
+  }
+  add_res("up_blocks.0.0", 2 * C);
+  add_tbs("up_blocks.0.1");
+  {
+    int w = L.add("up_blocks.0.2.conv.weight", {C, C, 4});
+    int b = L.add("up_blocks.0.2.conv.bias", {C});
+    up0 = make_convT(C, C, 4, 2, 1, w, b, esize, pk);
+  }
+  add_res("up_blocks.1.0", 2 * C);
+  add_tbs("up_blocks.1.1");
+  {
+    int w = L.add("up_blocks.1.2.weight", {C, C, 3});
+    int b = L.add("up_blocks.1.2.bias", {C});
+    up1 = make_conv(C, C, 3, 1, 1, 1, {w}, b, esize, pk);
+  }
+  {
+    int w = L.add("final_block.block.0.weight", {C, C, 3});
+    int b = L.add("final_block.block.0.bias", {C});
+    fgn_g = L.add("final_block.block.1.weight", {C});
+    fgn_b = L.add("final_block.block.1.bias", {C});
+    fconv = make_conv(C, C, 3, 1, 1, 1, {w}, b, esize, pk);
+    fgn_off = pk.take(2 * C * 4);
+    int wp = L.add("final_proj.weight", {NF, C, 1});
+    int bp = L.add("final_proj.bias", {NF});
+    fproj = make_conv(NF, C, 1, 1, 0, 1, {wp}, bp, esize, pk);
+  }
+  packed_bytes = pk.off;
+  return 0;
+}
+
+int Decoder::pack(const float* const* p, void* packed, hipStream_t st) const {
+  char* P = (char*)packed;
+  int rc;
+#define PK(expr) \
+  if ((rc = (expr)) != 0) return rc
+  PK(pack_vec(p[t1w], TE * c_cond, TE * c_cond, 0, (float*)(P + t1w_off), st));
+  PK(pack_vec(p[t1b], TE, TE, 0, (float*)(P + t1b_off), st));
+  PK(pack_vec(p[t2w], TE * TE, TE * TE, 0, (float*)(P + t2w_off), st));
+  PK(pack_vec(p[t2b], TE, TE, 0, (float*)(P + t2b_off), st));
+  PK(pack_vec(p[freq], c_cond / 2, c_cond / 2, 0, (float*)(P + freq_off), st));
+  for (size_t r = 0; r < res.size(); ++r) {
+    const Res& R = res[r];
+    PK(pack_gemm(R.c1, dtype, p, P, st));
+    PK(pack_gemm(R.c2, dtype, p, P, st));
+    PK(pack_gemm(R.res, dtype, p, P, st));
+    PK(pack_vec(p[R.gn1g], C, C, 0, (float*)(P + R.gn1_off), st));
+    PK(pack_vec(p[R.gn1b], C, C, 0, (float*)(P + R.gn1_off) + C, st));
+    PK(pack_vec(p[R.gn2g], C, C, 0, (float*)(P + R.gn2_off), st));
+    PK(pack_vec(p[R.gn2b], C, C, 0, (float*)(P + R.gn2_off) + C, st));
+    PK(pack_vec(p[R.mlp_w], C * TE, C * TE, 0, (float*)(P + R.mlp_w_off), st));
+    PK(pack_vec(p[R.mlp_b], C, C, 0, (float*)(P + R.mlp_b_off), st));
+    for (const TB& t : tbs[r]) {
+      PK(pack_gemm(t.qkv, dtype, p, P, st));
+      PK(pack_gemm(t.out, dtype, p, P, st));
+      PK(pack_gemm(t.ff1, dtype, p, P, st));
+      PK(pack_gemm(t.ff2, dtype, p, P, st));
+      PK(pack_vec(p[t.ln1g], C, C, 0, (float*)(P + t.ln1_off), st));
+      PK(pack_vec(p[t.ln1b], C, C, 0, (float*)(P + t.ln1_off) + C, st));
+      PK(pack_vec(p[t.ln3g], C, C, 0, (float*)(P + t.ln3_off), st));
+      PK(pack_vec(p[t.ln3b], C, C, 0, (float*)(P + t.ln3_off) + C, st));
+      PK(pack_vec(p[t.alpha], TE, TE, 1, (float*)(P + t.snake_off), st));
+      PK(pack_vec(p[t.beta], TE, TE, 2, (float*)(P + t.snake_off) + TE, st));
+    }
+  }
+  PK(pack_gemm(down0, dtype, p, P, st));
+  PK(pack_gemm(down1, dtype, p, P, st));
+  PK(pack_gemm(up0, dtype, p, P, st));
+  PK(pack_gemm(up1, dtype, p, P, st));
+  PK(pack_gemm(fconv, dtype, p, P, st));
+  PK(pack_vec(p[fgn_g], C, C, 0, (float*)(P + fgn_off), st));
+  PK(pack_vec(p[fgn_b], C, C, 0, (float*)(P + fgn_off) + C, st));
+  PK(pack_gemm(fproj, dtype, p, P, st));
+#undef PK
+  return 0;
+}
+
+size_t Decoder::workspace_bytes(int B, int T, int S) const {
+  const size_t BT = (size_t)B * T;
+  const size_t ntl = (size_t)(T + 63) / 64;
+  size_t n = 0;
+  n += align256(BT * c_cond * esize);                 // xin
+  n += 8 * align256(BT * C * esize);                  // H0 H1 XA XB XC U XF + y1
+  n += align256(BT * C * esize);                      // y2
+  n += align256(BT * 3 * inner * esize);              // qkv
+  n += align256(BT * inner * esize);                  // ob
+  n += align256(BT * TE * esize);                     // ff
+  n += align256(BT * NF * 4);                         // zm
+  n += align256((size_t)B * ((T + 1) / 2) * 4);       // m1
+  n += 2 * align256((size_t)B * 8 * ntl * 2 * 8);     // gn1 gn2
+  n += align256((size_t)S * c_cond * 4);              // emb
+  n += 2 * align256((size_t)S * TE * 4);              // h1 h2
+  n += align256((size_t)S * n_res * C * 4);           // tb
+  return n;
+}
+
+Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
+  const size_t BT = (size_t)B * T;
+  const size_t ntl = (size_t)(T + 63) / 64;
+  char* p = (char*)ws;
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += align256(bytes);
+    return r;
+  };
+  Work w;
+  w.xin = take(BT * c_cond * esize);
+  w.H0 = take(BT * C * esize);
+  w.H1 = take(BT * C * esize);
+  w.XA = take(BT * C * esize);
+  w.XB = take(BT * C * esize);
+  w.XC = take(BT * C * esize);
+  w.U = take(BT * C * esize);
+  w.XF = take(BT * C * esize);
+  w.y1 = take(BT * C * esize);
+  w.y2 = take(BT * C * esize);
+  w.qkv = take(BT * 3 * inner * esize);
+  w.ob = take(BT * inner * esize);
+  w.ff = take(BT * TE * esize);
+  w.zm = (float*)take(BT * NF * 4);
+  w.m1 = (float*)take((size_t)B * ((T + 1) / 2) * 4);
+  w.gn1 = (double*)take((size_t)B * 8 * ntl * 2 * 8);
+  w.gn2 = (double*)take((size_t)B * 8 * ntl * 2 * 8);
+  w.emb = (float*)take((size_t)S * c_cond * 4);
+  w.h1 = (float*)take((size_t)S * TE * 4);
+  w.h2 = (float*)take((size_t)S * TE * 4);
+  w.tb = (float*)take((size_t)S * n_res * C * 4);
+  w.m0 = nullptr;
+  return w;
+}
+
+int Decoder::time_embed(const char* P, const Work& w, const TimeSched& ts, int S, hipStream_t st) const {
+  int rc;
+  if ((rc = sinus_embed(ts, S, (const float*)(P + freq_off), c_cond / 2, w.emb, st))) return rc;
+  if ((rc = rowdot(w.emb, c_cond, (const float*)(P + t1w_off), (const float*)(P + t1b_off), w.h1, TE, 0, S,
+                   TE, c_cond, 0, 1, st)))
+    return rc;
+  if ((rc = rowdot(w.h1, TE, (const float*)(P + t2w_off), (const float*)(P + t2b_off), w.h2, TE, 0, S, TE, TE,
+                   0, 0, st)))
+    return rc;
+  for (int r = 0; r < n_res; ++r) {
+    if ((rc = rowdot(w.h2, TE, (const float*)(P + res[r].mlp_w_off), (const float*)(P + res[r].mlp_b_off),
+                     w.tb, n_res * C, r * C, S, C, TE, 1, 0, st)))
+      return rc;
+  }
+  return 0;
+}
+
+template <class E>
+int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, const void* x1, int c0,
+                    int cin, void* out, const float* mask, int B, int Tl, const float* tb,
+                    hipStream_t st) const {
+  int rc, nt1 = 0, nt2 = 0;
+  ConvArgs a = gemm_args(R.c1, P, B, Tl);
+  a.x0 = x0;
+  a.x1 = x1;
+  a.c0 = c0;
+  a.cin = cin;
+  a.y = w.y1;
+  a.pmask = mask;
+  a.gn_out = w.gn1;
+  if ((rc = launch_conv<E, PF_MASK, EF_GNSTATS>(a, st, &nt1))) return rc;
+
+  ConvArgs b = gemm_args(R.c2, P, B, Tl);
+  b.x0 = w.y1;
+  b.y = w.y2;
+  b.pmask = mask;
+  b.gn_in = w.gn1;
+  b.gn_ntiles = nt1;
+  b.gn_T = Tl;
+  b.gn_g = (const float*)(P + R.gn1_off);
+  b.gn_b = (const float*)(P + R.gn1_off) + C;
+  b.tb = tb;
+  b.gn_out = w.gn2;
+  if ((rc = launch_conv<E, PF_GN | PF_TB | PF_MASK, EF_GNSTATS>(b, st, &nt2))) return rc;
+
+  ConvArgs c = gemm_args(R.res, P, B, Tl);
+  c.x0 = x0;
+  c.x1 = x1;
+  c.c0 = c0;
+  c.cin = cin;
+  c.y = out;
+  c.pmask = mask;
+  c.emask = mask;
+  c.gy = w.y2;
+  c.gn_in = w.gn2;
+  c.gn_ntiles = nt2;
+  c.gn_T = Tl;
+  c.gn_g = (const float*)(P + R.gn2_off);
+  c.gn_b = (const float*)(P + R.gn2_off) + C;
+  return launch_conv<E, PF_MASK, EF_GNADD>(c, st);
+}
+
+template <class E>
+int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, int B, int Tl,
+                    hipStream_t st) const {
+  int rc;
+  ConvArgs q = gemm_args(t.qkv, P, B, Tl);
+  q.x0 = x;
+  q.y = w.qkv;
+  q.ln_g = (const float*)(P + t.ln1_off);
+  q.ln_b = (const float*)(P + t.ln1_off) + C;
+  if ((rc = launch_conv<E, PF_LN, 0>(q, st))) return rc;
+  if ((rc = launch_attention(dtype, w.qkv, mask, w.ob, B, Tl, heads, st))) return rc;
+  ConvArgs o = gemm_args(t.out, P, B, Tl);
+  o.x0 = w.ob;
+  o.y = x;
+  o.resid = x;
+  o.ldr = C;
+  if ((rc = launch_conv<E, 0, EF_RESID>(o, st))) return rc;
+  ConvArgs f1 = gemm_args(t.ff1, P, B, Tl);
+  f1.x0 = x;
+  f1.y = w.ff;
+  f1.ln_g = (const float*)(P + t.ln3_off);
+  f1.ln_b = (const float*)(P + t.ln3_off) + C;
+  f1.snake_alpha = (const float*)(P + t.snake_off);
+  f1.snake_ibeta = (const float*)(P + t.snake_off) + TE;
+  if ((rc = launch_conv<E, PF_LN, EF_SNAKE>(f1, st))) return rc;
+  ConvArgs f2 = gemm_args(t.ff2, P, B, Tl);
+  f2.x0 = w.ff;
+  f2.y = x;
+  f2.resid = x;
+  f2.ldr = C;
+  return launch_conv<E, 0, EF_RESID>(f2, st);
+}
+
+template <class E>
+int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Euler& eu, hipStream_t st) const {
+  int rc;
+  const int T1 = T / 2;
+  const float* m0 = w.m0;
+  const float* m1 = w.m1;
+  auto tbp = [&](int r) { return w.tb + ((size_t)ev * n_res + r) * C; };
+  auto tblocks = [&](int r, void* x, const float* m, int Tl) -> int {
+    for (const TB& t : tbs[r]) {
+      int e = tblock<E>(P, w, t, x, m, B, Tl, st);
+      if (e) return e;
+    }
+    return 0;
+  };
+  auto plain = [&](const GemmW& g, const void* x, const float* m, int Tl, void* out) -> int {
+    ConvArgs a = gemm_args(g, P, B, Tl);
+    a.x0 = x;
+    a.y = out;
+    a.pmask = m;
+    return launch_conv<E, PF_MASK, 0>(a, st);
+  };
+  // down 0 @T
+  if ((rc = resnet<E>(P, w, res[0], w.xin, nullptr, c_cond, c_cond, w.H0, m0, B, T, tbp(0), st))) return rc;
+  if ((rc = tblocks(0, w.H0, m0, T))) return rc;
+  if ((rc = plain(down0, w.H0, m0, T, w.XA))) return rc;
+  // down 1 @T/2
+  if ((rc = resnet<E>(P, w, res[1], w.XA, nullptr, C, C, w.H1, m1, B, T1, tbp(1), st))) return rc;
+  if ((rc = tblocks(1, w.H1, m1, T1))) return rc;
+  if ((rc = plain(down1, w.H1, m1, T1, w.XB))) return rc;
+  char* half[3] = {w.XA, w.XB, w.XC};
+  int cur = 1;
+  for (int i = 0; i < n_mid; ++i) {
+    const int nx = (cur + 1) % 3;
+    if ((rc = resnet<E>(P, w, res[2 + i], half[cur], nullptr, C, C, half[nx], m1, B, T1, tbp(2 + i), st)))
+      return rc;
+    if ((rc = tblocks(2 + i, half[nx], m1, T1))) return rc;
+    cur = nx;
+  }
+  // up 0 @T/2: cat(x, skip=H1)
+  {
+    const int nx = (cur + 1) % 3;
+    const int r = 2 + n_mid;
+    if ((rc = resnet<E>(P, w, res[r], half[cur], w.H1, C, 2 * C, half[nx], m1, B, T1, tbp(r), st))) return rc;
+    if ((rc = tblocks(r, half[nx], m1, T1))) return rc;
+    if ((rc = plain(up0, half[nx], m1, T1, w.U))) return rc;  // ConvTranspose1d k4 s2 p1 -> T
+  }
+  // up 1 @T: cat(U, skip=H0)
+  {
+    const int r = 3 + n_mid;
+    if ((rc = resnet<E>(P, w, res[r], w.U, w.H0, C, 2 * C, w.XF, m0, B, T, tbp(r), st))) return rc;
+    if ((rc = tblocks(r, w.XF, m0, T))) return rc;
+    if ((rc = plain(up1, w.XF, m0, T, w.U))) return rc;
+  }
+  // final block + projection + ODE update
+  int ntf = 0;
+  {
+    ConvArgs a = gemm_args(fconv, P, B, T);
+    a.x0 = w.U;
+    a.y = w.y1;
+    a.pmask = m0;
+    a.gn_out = w.gn1;
+    if ((rc = launch_conv<E, PF_MASK, EF_GNSTATS>(a, st, &ntf))) return rc;
+  }
+  ConvArgs f = gemm_args(fproj, P, B, T);
+  f.x0 = w.y1;
+  f.y = nullptr;
+  f.pmask = m0;
+  f.emask = m0;
+  f.gn_in = w.gn1;
+  f.gn_ntiles = ntf;
+  f.gn_T = T;
+  f.gn_g = (const float*)(P + fgn_off);
+  f.gn_b = (const float*)(P + fgn_off) + C;
+  f.zmaster = w.zm;
+  f.xin_z = w.xin;
+  f.ld_xin = c_cond;
+  f.dt = eu.dt;
+  f.half_step = eu.half_step;
+  f.update_master = eu.update_master;
+  return launch_conv<E, PF_GN | PF_MASK, EF_MASK | EF_EULER>(f, st);
+}
+
+int Decoder::init_inputs(const Work& w, const float* z, float temperature, const float* mu_y,
+                         const float* spks, int B, int T, hipStream_t st) const {
+  int rc;
+  if ((rc = bct_to_btc(F32, z, B, NF, T, temperature, w.zm, NF, 0, st))) return rc;
+  if ((rc = bct_to_btc(dtype, z, B, NF, T, temperature, w.xin, c_cond, 0, st))) return rc;
+  if ((rc = bct_to_btc(dtype, mu_y, B, NF, T, 1.f, w.xin, c_cond, NF, st))) return rc;
+  if (c_cond > 2 * NF) {
+    MT_REQUIRE(spks != nullptr, "decoder: c_cond %d needs speaker embeddings", c_cond);
+    if ((rc = spk_fill(dtype, spks, B, c_cond - 2 * NF, T, w.xin, c_cond, 2 * NF, st))) return rc;
+  }
+  return mask_half(w.m0, B, T, w.m1, st);
+}
+
+static int check_geom(int B, int T) {
+  MT_REQUIRE(B > 0 && T > 0, "decoder: empty batch");
+  MT_REQUIRE(T % 2 == 0, "decoder: T=%d must be even (synthesize pads to a multiple of 4)", T);
+  return 0;
+}
+
+int Decoder::solve(const void* packed, const float* z_noise, float temperature, const float* mu_y,
+                   const float* mask, const float* spks, int B, int T, int n_steps, int solver, float* z_out,
+                   void* ws, size_t ws_bytes, hipStream_t st) const {
+  int rc;
+  if ((rc = check_geom(B, T))) return rc;
+  MT_REQUIRE(n_steps >= 1, "cfm: n_timesteps must be >= 1");
+  MT_REQUIRE(solver == 0 || solver == 1, "cfm: solver must be 0 (euler) or 1 (midpoint)");
+  const int S = solver == 0 ? n_steps : 2 * n_steps;
+  MT_REQUIRE(S <= TimeSched::MAX, "cfm: too many evaluations (%d)", S);
+  MT_REQUIRE(ws_bytes >= workspace_bytes(B, T, S), "cfm: workspace %zu < %zu", ws_bytes,
+             workspace_bytes(B, T, S));
+  const char* P = (const char*)packed;
+  Work w = carve(ws, B, T, S);
+  w.m0 = mask;
+  // evaluation times exactly as the reference forms them in fp32 (model.py:1086-1104)
+  TimeSched ts{};
+  const float dt = (float)(1.0 / (double)n_steps);
+  for (int i = 0; i < n_steps; ++i) {
+    const float t = (float)((double)i / (double)n_steps);
+    if (solver == 0) {
+      ts.t[i] = t;
+    } else {
+      ts.t[2 * i] = t;
+      ts.t[2 * i + 1] = t + dt * 0.5f;
+    }
+  }
+  if ((rc = time_embed(P, w, ts, S, st))) return rc;
+  if ((rc = init_inputs(w, z_noise, temperature, mu_y, spks, B, T, st))) return rc;
+  for (int i = 0; i < n_steps; ++i) {
+    if (solver == 0) {
+      Euler eu{dt, 0, 1};
+      rc = dtype == BF16 ? eval<bf16>(P, w, B, T, i, eu, st) : eval<float>(P, w, B, T, i, eu, st);
+      if (rc) return rc;
+    } else {
+      Euler e1{dt, 1, 0}, e2{dt, 0, 1};
+      rc = dtype == BF16 ? eval<bf16>(P, w, B, T, 2 * i, e1, st) : eval<float>(P, w, B, T, 2 * i, e1, st);
+      if (rc) return rc;
+      rc = dtype == BF16 ? eval<bf16>(P, w, B, T, 2 * i + 1, e2, st)
+                         : eval<float>(P, w, B, T, 2 * i + 1, e2, st);
+      if (rc) return rc;
+    }
+  }
+  return btc_to_bct(F32, w.zm, NF, 0, B, NF, T, z_out, st);
+}
+
+int Decoder::step(const void* packed, const float* x, const float* mu_y, const float* mask, const float* spks,
+                  float t, int B, int T, float* out, void* ws, size_t ws_bytes, hipStream_t st) const {
+  int rc;
+  if ((rc = check_geom(B, T))) return rc;
+  MT_REQUIRE(ws_bytes >= workspace_bytes(B, T, 1), "decoder: workspace too small");
+  const char* P = (const char*)packed;
+  Work w = carve(ws, B, T, 1);
+  w.m0 = mask;
+  TimeSched ts{};
+  ts.t[0] = t;
+  if ((rc = time_embed(P, w, ts, 1, st))) return rc;
+  if ((rc = init_inputs(w, x, 1.f, mu_y, spks, B, T, st))) return rc;
+  MT_CHECK_HIP(hipMemsetAsync(w.zm, 0, (size_t)B * T * NF * 4, st));
+  Euler eu{1.f, 0, 1};  // z = 0 + pred * 1  ==  pred exactly
+  rc = dtype == BF16 ? eval<bf16>(P, w, B, T, 0, eu, st) : eval<float>(P, w, B, T, 0, eu, st);
+  if (rc) return rc;
+  return btc_to_bct(F32, w.zm, NF, 0, B, NF, T, out, st);
+}
+
+}  // namespace mt

@@ -1,0 +1,37 @@
+#pragma once
+#include "mt_common.h"
+
+namespace mt {
+
+// solver evaluation times, passed by value to the time-embedding kernel
+struct TimeSched {
+  static constexpr int MAX = 128;
+  float t[MAX];
+};
+
+int pack_conv(int dtype, const float* W, int kind, int cout, int cin, int k, int s, int row0, int Mrows,
+              int Mpad, int taps, int cin_pad, void* out, hipStream_t st);
+int pack_vec(const float* src, int period, int n, int op, float* out, hipStream_t st);
+
+int bct_to_btc(int dtype, const float* src, int B, int C, int T, float scale, void* dst, int ld, int coff,
+               hipStream_t st);
+int btc_to_bct(int dtype, const void* src, int ld, int coff, int B, int C, int T, float* dst,
+               hipStream_t st);
+int spk_fill(int dtype, const float* spks, int B, int C, int T, void* dst, int ld, int coff, hipStream_t st);
+int mask_half(const float* m0, int B, int T0, float* m1, hipStream_t st);
+
+int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* emb, hipStream_t st);
+int rowdot(const float* x, int ldx, const float* W, const float* bias, float* y, int ldy, int yoff, int S,
+           int O, int I, int pre, int post, hipStream_t st);
+
+int durations(const float* logw, const float* xmask, float ls, int B, int Tx, float* w_ceil, float* cum,
+              long long* ylen, hipStream_t st);
+int alignment(const float* cum, const long long* ylen, int B, int Tx, int T, const float* mu, int C, float* attn,
+              float* mu_y, float* y_mask, hipStream_t st);
+int denorm_crop(const float* z, const float* mean, const float* stdv, int B, int C, int T, int Ty, float* mel,
+                hipStream_t st);
+
+int launch_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
+                     hipStream_t stream);
+
+}  // namespace mt

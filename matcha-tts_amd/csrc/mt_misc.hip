@@ -1,0 +1,322 @@
+// Support kernels: weight packing, layout transposes, time-embedding MLP, the
+// duration -> alignment index path, denormalize/crop.
+#include "mt_misc.h"
+
+#include <algorithm>
+
+namespace mt {
+
+// ------------------------------------------------------------------------------------
+// weight packing: reference fp32 layouts -> [Mpad][taps][cin_pad] element type
+//   kind 0: Conv1d  W[cout][cin][k]       -> taps = k,   row m = co
+//   kind 1: ConvT   W[cin][cout][k], s    -> taps = k/s, row m = phase*cout + co,
+//                                            tap t <-> kernel index phase + (taps-1-t)*s
+// rows >= M and channels >= cin are zero.
+// ------------------------------------------------------------------------------------
+template <class E>
+__global__ void pack_conv_kernel(const float* __restrict__ W, int kind, int cout, int cin, int k,
+                                 int s, int row0, int Mpad, int taps, int cin_pad, int Mrows,
+                                 E* __restrict__ out) {
+  const size_t total = (size_t)Mrows * taps * cin_pad;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % cin_pad);
+    const int t = (int)((i / cin_pad) % taps);
+    const int m = (int)(i / ((size_t)cin_pad * taps));
+    float v = 0.f;
+    if (ci < cin) {
+      if (kind == 0) {
+        if (m < cout) v = W[((size_t)m * cin + ci) * k + t];
+      } else {
+        const int ph = m / cout, co = m % cout;
+        if (ph < s) {
+          const int kk = ph + (taps - 1 - t) * s;
+          v = W[((size_t)ci * cout + co) * k + kk];
+        }
+      }
+    }
+    out[((size_t)(row0 + m) * taps + t) * cin_pad + ci] = from_f<E>(v);
+  }
+  (void)Mpad;
+}
+
+int pack_conv(int dtype, const float* W, int kind, int cout, int cin, int k, int s, int row0,
+              int Mrows, int Mpad, int taps, int cin_pad, void* out, hipStream_t st) {
+  const size_t total = (size_t)Mrows * taps * cin_pad;
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 65535);
+  if (dtype == BF16)
+    hipLaunchKernelGGL(pack_conv_kernel<bf16>, dim3(blocks), dim3(256), 0, st, W, kind, cout, cin, k, s,
+                       row0, Mpad, taps, cin_pad, Mrows, (bf16*)out);
+  else
+    hipLaunchKernelGGL(pack_conv_kernel<float>, dim3(blocks), dim3(256), 0, st, W, kind, cout, cin, k,
+                       s, row0, Mpad, taps, cin_pad, Mrows, (float*)out);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// out[m] = src ? src[m % period] : 0, m < n ; op 1: exp(src); op 2: 1/(exp(src)+1e-9)
+__global__ void vec_kernel(const float* __restrict__ src, int period, int n, int op,
+                           float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = src ? src[i % period] : 0.f;
+  if (op == 1) v = expf(v);
+  if (op == 2) v = 1.0f / (expf(v) + 1e-9f);
+  out[i] = v;
+}
+
+int pack_vec(const float* src, int period, int n, int op, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(vec_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, period, n, op, out);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// layout transposes  [B][C][T] fp32  <->  [B][T][ld] (column offset coff)
+// ------------------------------------------------------------------------------------
+template <class E>
+__global__ void bct_to_btc_kernel(const float* __restrict__ src, int C, int T, float scale,
+                                  E* __restrict__ dst, int ld, int coff) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z, c0 = blockIdx.y * 32, t0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, t = t0 + tx;
+    tile[i][tx] = (c < C && t < T) ? src[((size_t)b * C + c) * T + t] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int t = t0 + i, c = c0 + tx;
+    if (c < C && t < T) dst[((size_t)b * T + t) * ld + coff + c] = from_f<E>(tile[tx][i] * scale);
+  }
+}
+
+template <class E>
+__global__ void btc_to_bct_kernel(const E* __restrict__ src, int ld, int coff, int C, int T,
+                                  float* __restrict__ dst) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z, c0 = blockIdx.y * 32, t0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int t = t0 + i, c = c0 + tx;
+    tile[i][tx] = (c < C && t < T) ? to_f(src[((size_t)b * T + t) * ld + coff + c]) : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, t = t0 + tx;
+    if (c < C && t < T) dst[((size_t)b * C + c) * T + t] = tile[tx][i];
+  }
+}
+
+int bct_to_btc(int dtype, const float* src, int B, int C, int T, float scale, void* dst, int ld,
+               int coff, hipStream_t st) {
+  dim3 grid((T + 31) / 32, (C + 31) / 32, B);
+  if (dtype == BF16)
+    hipLaunchKernelGGL(bct_to_btc_kernel<bf16>, grid, dim3(256), 0, st, src, C, T, scale, (bf16*)dst, ld,
+                       coff);
+  else
+    hipLaunchKernelGGL(bct_to_btc_kernel<float>, grid, dim3(256), 0, st, src, C, T, scale, (float*)dst,
+                       ld, coff);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int btc_to_bct(int dtype, const void* src, int ld, int coff, int B, int C, int T, float* dst,
+               hipStream_t st) {
+  dim3 grid((T + 31) / 32, (C + 31) / 32, B);
+  if (dtype == BF16)
+    hipLaunchKernelGGL(btc_to_bct_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)src, ld, coff, C, T,
+                       dst);
+  else
+    hipLaunchKernelGGL(btc_to_bct_kernel<float>, grid, dim3(256), 0, st, (const float*)src, ld, coff, C,
+                       T, dst);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// speaker embedding broadcast into the estimator input: dst[b][t][coff + c] = spks[b][c]
+template <class E>
+__global__ void spk_fill_kernel(const float* __restrict__ spks, int C, int T, E* __restrict__ dst,
+                                int ld, int coff) {
+  const int b = blockIdx.y;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < T * C; i += gridDim.x * blockDim.x) {
+    const int t = i / C, c = i % C;
+    dst[((size_t)b * T + t) * ld + coff + c] = from_f<E>(spks[(size_t)b * C + c]);
+  }
+}
+
+int spk_fill(int dtype, const float* spks, int B, int C, int T, void* dst, int ld, int coff,
+             hipStream_t st) {
+  dim3 grid(std::min((T * C + 255) / 256, 4096), B);
+  if (dtype == BF16)
+    hipLaunchKernelGGL(spk_fill_kernel<bf16>, grid, dim3(256), 0, st, spks, C, T, (bf16*)dst, ld, coff);
+  else
+    hipLaunchKernelGGL(spk_fill_kernel<float>, grid, dim3(256), 0, st, spks, C, T, (float*)dst, ld, coff);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// mask at half resolution: m1[b][t] = m0[b][2t]  (model.py:1003 mask[:, :, ::2])
+__global__ void mask_half_kernel(const float* __restrict__ m0, int T0, int T1, int B,
+                                 float* __restrict__ m1) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * T1) return;
+  const int b = i / T1, t = i % T1;
+  m1[i] = m0[(size_t)b * T0 + 2 * t];
+}
+
+int mask_half(const float* m0, int B, int T0, float* m1, hipStream_t st) {
+  const int T1 = (T0 + 1) / 2;
+  hipLaunchKernelGGL(mask_half_kernel, dim3((B * T1 + 255) / 256), dim3(256), 0, st, m0, T0, T1, B, m1);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// time embedding (model.py:747-762, 819-832, 780): per solver evaluation s
+//   emb[s] = [sin(1000 t_s f_k), cos(1000 t_s f_k)]  (f_k = exp(-k ln(1e4)/(half-1)), host table)
+// ------------------------------------------------------------------------------------
+__global__ void sinus_kernel(TimeSched ts, const float* __restrict__ freq, int half,
+                             float* __restrict__ emb) {
+  const int s = blockIdx.x;
+  const float st = 1000.f * ts.t[s];
+  for (int k = threadIdx.x; k < 2 * half; k += blockDim.x) {
+    const float a = st * freq[k % half];
+    emb[(size_t)s * 2 * half + k] = k < half ? sinf(a) : cosf(a);
+  }
+}
+
+int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* emb, hipStream_t st) {
+  MT_REQUIRE(S > 0 && S <= TimeSched::MAX, "time schedule length %d", S);
+  hipLaunchKernelGGL(sinus_kernel, dim3(S), dim3(256), 0, st, ts, freq, half, emb);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// y[s][yoff + o] = post( sum_i W[o][i] * pre(x[s][i]) + bias[o] ); one wave per output o.
+// pre: 0 none, 1 mish ; post: 0 none, 1 silu
+__global__ void rowdot_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ W,
+                              const float* __restrict__ bias, float* __restrict__ y, int ldy,
+                              int yoff, int S, int O, int I, int pre, int post) {
+  const int lane = threadIdx.x & 63;
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (o >= O) return;
+  const float* w = W + (size_t)o * I;
+  for (int s = 0; s < S; ++s) {
+    const float* xs = x + (size_t)s * ldx;
+    float acc = 0.f;
+    for (int i = lane; i < I; i += 64) {
+      float xv = xs[i];
+      if (pre == 1) xv = xv * tanhf(log1pf(expf(xv)));
+      acc += w[i] * xv;
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) {
+      float v = acc + (bias ? bias[o] : 0.f);
+      if (post == 1) v = v / (1.f + expf(-v));
+      y[(size_t)s * ldy + yoff + o] = v;
+    }
+  }
+}
+
+int rowdot(const float* x, int ldx, const float* W, const float* bias, float* y, int ldy, int yoff,
+           int S, int O, int I, int pre, int post, hipStream_t st) {
+  hipLaunchKernelGGL(rowdot_kernel, dim3((O + 3) / 4), dim3(256), 0, st, x, ldx, W, bias, y, ldy, yoff,
+                     S, O, I, pre, post);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// duration -> alignment index path (model.py:1273-1289, 42-76). Bit-exact: every value is
+// an integer-valued fp32 (< 2^24), so sums and prefix sums are exact in any order.
+// ------------------------------------------------------------------------------------
+__global__ void durations_kernel(const float* __restrict__ logw, const float* __restrict__ xmask,
+                                 float ls, int Tx, float* __restrict__ w_ceil,
+                                 float* __restrict__ cum, long long* __restrict__ ylen) {
+  const int b = blockIdx.x;
+  for (int x = threadIdx.x; x < Tx; x += blockDim.x) {
+    const size_t i = (size_t)b * Tx + x;
+    const float w = (expf(logw[i]) * xmask[i]) * ls;
+    w_ceil[i] = ceilf(w);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float c = 0.f;
+    for (int x = 0; x < Tx; ++x) {
+      c += w_ceil[(size_t)b * Tx + x];
+      cum[(size_t)b * Tx + x] = c;
+    }
+    ylen[b] = (long long)(c < 1.f ? 1.f : c);
+  }
+}
+
+int durations(const float* logw, const float* xmask, float ls, int B, int Tx, float* w_ceil, float* cum,
+              long long* ylen, hipStream_t st) {
+  MT_REQUIRE(B > 0 && Tx > 0, "durations: empty input");
+  hipLaunchKernelGGL(durations_kernel, dim3(B), dim3(256), 0, st, logw, xmask, ls, Tx, w_ceil, cum, ylen);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// frame j of utterance b belongs to the first token x with cum[x] > j (if j < cum[Tx-1]).
+// attn[b][x][j] one-hot (optional), mu_y[b][c][j] = mu[b][c][x] (an exact gather).
+__global__ void alignment_kernel(const float* __restrict__ cum, const long long* __restrict__ ylen, int Tx,
+                                 int T, const float* __restrict__ mu, int C, float* __restrict__ attn,
+                                 float* __restrict__ mu_y, float* __restrict__ y_mask) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= T) return;
+  const float* cb = cum + (size_t)b * Tx;
+  const float jf = (float)j;
+  int tok = -1;
+  if (jf < cb[Tx - 1]) {
+    int lo = 0, hi = Tx - 1;  // first index with cb[x] > j
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cb[mid] > jf) hi = mid; else lo = mid + 1;
+    }
+    tok = lo;
+  }
+  if (attn) {
+    float* ab = attn + (size_t)b * Tx * T + j;
+    for (int x = 0; x < Tx; ++x) ab[(size_t)x * T] = (x == tok) ? 1.f : 0.f;
+  }
+  if (y_mask) y_mask[(size_t)b * T + j] = (long long)j < ylen[b] ? 1.f : 0.f;
+  if (mu_y) {
+    for (int c = 0; c < C; ++c)
+      mu_y[((size_t)b * C + c) * T + j] = tok >= 0 ? mu[((size_t)b * C + c) * Tx + tok] : 0.f;
+  }
+}
+
+int alignment(const float* cum, const long long* ylen, int B, int Tx, int T, const float* mu, int C, float* attn,
+              float* mu_y, float* y_mask, hipStream_t st) {
+  MT_REQUIRE(B > 0 && Tx > 0 && T > 0, "alignment: empty input");
+  dim3 grid((T + 255) / 256, B);
+  hipLaunchKernelGGL(alignment_kernel, grid, dim3(256), 0, st, cum, ylen, Tx, T, mu, C, attn, mu_y, y_mask);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// mel[b][c][t] = z[b][c][t] * std[c] + mean[c], t < Ty   (model.py:106-125, 1295-1298)
+__global__ void denorm_crop_kernel(const float* __restrict__ z, const float* __restrict__ mean,
+                                   const float* __restrict__ stdv, int C, int T, int Ty,
+                                   float* __restrict__ mel) {
+  const int bc = blockIdx.y;
+  const int c = bc % C;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < Ty; t += gridDim.x * blockDim.x) {
+    const float v = z[(size_t)bc * T + t] * stdv[c];
+    mel[(size_t)bc * Ty + t] = v + mean[c];
+  }
+}
+
+int denorm_crop(const float* z, const float* mean, const float* stdv, int B, int C, int T, int Ty,
+                float* mel, hipStream_t st) {
+  MT_REQUIRE(Ty <= T && Ty > 0, "denorm_crop: Ty %d > T %d", Ty, T);
+  dim3 grid(std::min((Ty + 255) / 256, 64), B * C);
+  hipLaunchKernelGGL(denorm_crop_kernel, grid, dim3(256), 0, st, z, mean, stdv, C, T, Ty, mel);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace mt

@@ -1,0 +1,141 @@
+// Host-side model descriptions shared by the decoder (U-Net estimator + CFM solver) and
+// the HiFi-GAN vocoder drivers. A model lists the reference state_dict tensors it needs
+// (names and shapes, canonical order) and the byte layout of its packed weight buffer.
+// The caller (PyTorch) owns every device buffer; these objects hold host metadata only.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "mt_conv.h"
+#include "mt_misc.h"
+
+namespace mt {
+
+struct ParamList {
+  std::vector<std::string> names;
+  std::vector<std::vector<long long>> shapes;
+  int add(const std::string& n, std::vector<long long> s) {
+    names.push_back(n);
+    shapes.push_back(std::move(s));
+    return (int)names.size() - 1;
+  }
+};
+
+struct Packer {
+  size_t off = 0;
+  size_t take(size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  }
+};
+
+// A packed GEMM layer (Conv1d / Linear / ConvTranspose1d) — see mt_conv.h for the mapping.
+struct GemmW {
+  int kind = 0;  // 0 Conv1d / Linear, 1 ConvTranspose1d
+  int cin = 0, cout = 0, k = 1, s = 1, pad = 0, dil = 1;
+  int M = 0, Mpad = 0, taps = 1, cin_pad = 0, gpad = 0, ups = 1, opad = 0;
+  std::vector<int> wsrc;  // weight params (several = rows stacked, e.g. Q|K|V)
+  int bsrc = -1;          // bias param or -1 (zeros)
+  size_t w_off = 0, b_off = 0;
+};
+
+GemmW make_conv(int cout, int cin, int k, int stride, int pad, int dil, std::vector<int> w, int b,
+                int esize, Packer& pk);
+GemmW make_convT(int cin, int cout, int k, int s, int pad, int w, int b, int esize, Packer& pk);
+int pack_gemm(const GemmW& g, int dtype, const float* const* params, char* P, hipStream_t st);
+// output geometry for an input of Tin frames
+void gemm_geom(const GemmW& g, int Tin, int* Tout, int* Ncols);
+// ConvArgs with the weight/geometry fields of g filled in
+ConvArgs gemm_args(const GemmW& g, const char* P, int B, int Tin);
+size_t align256(size_t x);
+
+// -------------------------------------------------------------------------------------
+// U-Net estimator (model.py:834-1048) + CFM solver (model.py:1084-1109)
+// -------------------------------------------------------------------------------------
+struct Decoder {
+  int c_cond = 160, n_mid = 2, n_blocks = 1, heads = 2, dtype = BF16;
+  static constexpr int C = 256, TE = 1024, NF = 80;
+  int inner = 128, n_res = 0, esize = 2;
+  ParamList params;
+  size_t packed_bytes = 0;
+
+  struct Res {
+    int dim_in;
+    GemmW c1, c2, res;
+    int gn1g, gn1b, gn2g, gn2b, mlp_w, mlp_b;
+    size_t gn1_off, gn2_off, mlp_w_off, mlp_b_off;
+  };
+  struct TB {
+    int ln1g, ln1b, ln3g, ln3b, alpha, beta;
+    size_t ln1_off, ln3_off, snake_off;
+    GemmW qkv, out, ff1, ff2;
+  };
+  std::vector<Res> res;                // down0, down1, mid..., up0, up1
+  std::vector<std::vector<TB>> tbs;    // per resnet
+  GemmW down0, down1, up0, up1, fconv, fproj;
+  int fgn_g, fgn_b, t1w, t1b, t2w, t2b, freq;
+  size_t fgn_off, t1w_off, t1b_off, t2w_off, t2b_off, freq_off;
+
+  int init(int c_cond, int n_mid, int n_blocks, int heads, int dtype);
+  int pack(const float* const* p, void* packed, hipStream_t st) const;
+  size_t workspace_bytes(int B, int T, int S) const;
+
+  struct Work {
+    char *xin, *H0, *H1, *XA, *XB, *XC, *U, *XF, *y1, *y2, *qkv, *ob, *ff;
+    float *zm, *m1, *emb, *h1, *h2, *tb;
+    double *gn1, *gn2;
+    const float* m0;
+  };
+  Work carve(void* ws, int B, int T, int S) const;
+  int time_embed(const char* P, const Work& w, const TimeSched& ts, int S, hipStream_t st) const;
+
+  struct Euler {
+    float dt;
+    int half_step, update_master;
+  };
+  template <class E>
+  int eval(const char* P, const Work& w, int B, int T, int ev, const Euler& eu, hipStream_t st) const;
+  template <class E>
+  int resnet(const char* P, const Work& w, const Res& R, const void* x0, const void* x1, int c0, int cin,
+             void* out, const float* mask, int B, int Tl, const float* tb, hipStream_t st) const;
+  template <class E>
+  int tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, int B, int Tl,
+             hipStream_t st) const;
+
+  int init_inputs(const Work& w, const float* z, float temperature, const float* mu_y, const float* spks,
+                  int B, int T, hipStream_t st) const;
+  int solve(const void* packed, const float* z_noise, float temperature, const float* mu_y,
+            const float* mask, const float* spks, int B, int T, int n_steps, int solver, float* z_out,
+            void* ws, size_t ws_bytes, hipStream_t st) const;
+  int step(const void* packed, const float* x, const float* mu_y, const float* mask, const float* spks,
+           float t, int B, int T, float* out, void* ws, size_t ws_bytes, hipStream_t st) const;
+};
+
+// -------------------------------------------------------------------------------------
+// HiFi-GAN Generator (hifigan/models.py:148-206)
+// -------------------------------------------------------------------------------------
+struct Vocoder {
+  int resblock = 1, dtype = BF16, esize = 2;
+  std::vector<int> up_rates, up_kernels, rb_kernels;
+  std::vector<std::vector<int>> rb_dils;
+  int up_init = 512, n_mels = 80;
+  ParamList params;
+  size_t packed_bytes = 0;
+  GemmW pre, post;
+  std::vector<GemmW> ups;
+  // resblocks[i*nk+j]: first convs (c1 / convs), second convs (c2, resblock 1 only)
+  std::vector<std::vector<GemmW>> rb1, rb2;
+
+  int init(int resblock, const std::vector<int>& up_rates, const std::vector<int>& up_kernels, int up_init,
+           const std::vector<int>& rb_kernels, const std::vector<std::vector<int>>& rb_dils, int dtype);
+  int pack(const float* const* p, void* packed, hipStream_t st) const;
+  size_t frame_elems() const;  // max over stages of (samples per mel frame) x channels
+  size_t workspace_bytes(int B, int T) const;
+  int forward(const void* packed, const float* mel, int B, int T, float* wav, void* ws, size_t ws_bytes,
+              hipStream_t st) const;
+  template <class E>
+  int forward_t(const char* P, const float* mel, int B, int T, float* wav, char* ws, hipStream_t st) const;
+};
+
+}  // namespace mt

@@ -1,0 +1,210 @@
+// HiFi-GAN Generator driver (hifigan/models.py:148-206; ResBlock1 :90-97, ResBlock2 :133-138).
+//
+//   mel [B,80,T] fp32 -> [B][T][80] -> conv_pre k7 -> per stage i:
+//     lrelu(0.1) -> ConvTranspose1d (polyphase GEMM) -> X
+//     for resblock j: chain of (lrelu -> conv(k, d) -> lrelu -> conv(k, 1) -> + x) pairs,
+//                     the last conv of the chain accumulates into XS (xs += ...; / nk fused)
+//   -> lrelu(0.01) -> conv_post k7 -> tanh -> wav [B,1,256T] fp32
+// Buffers (each B x T x frame_elems elements): XS (stage input / resblock sum), X (upsampled),
+// Tb (first conv of a pair), R (resblock chain state, updated in place).
+#include <algorithm>
+
+#include "mt_model.h"
+
+namespace mt {
+
+int Vocoder::init(int resblock_, const std::vector<int>& ur, const std::vector<int>& uk, int up_init_,
+                  const std::vector<int>& rk, const std::vector<std::vector<int>>& rd, int dtype_) {
+  MT_REQUIRE(resblock_ == 1 || resblock_ == 2, "vocoder: resblock must be 1 or 2");
+  MT_REQUIRE(ur.size() == uk.size() && !ur.empty(), "vocoder: upsample config");
+  MT_REQUIRE(rk.size() == rd.size() && !rk.empty(), "vocoder: resblock config");
+  MT_REQUIRE(dtype_ == F32 || dtype_ == BF16, "vocoder: dtype");
+  resblock = resblock_;
+  up_rates = ur;
+  up_kernels = uk;
+  up_init = up_init_;
+  rb_kernels = rk;
+  rb_dils = rd;
+  dtype = dtype_;
+  esize = dtype == BF16 ? 2 : 4;
+  params = ParamList();
+  ups.clear();
+  rb1.clear();
+  rb2.clear();
+  Packer pk;
+  ParamList& L = params;
+  {
+    int w = L.add("conv_pre.weight", {up_init, n_mels, 7});
+    int b = L.add("conv_pre.bias", {up_init});
+    pre = make_conv(up_init, n_mels, 7, 1, 3, 1, {w}, b, esize, pk);
+  }
+  int ch = up_init;
+  for (size_t i = 0; i < ur.size(); ++i) {
+    const int cin = up_init >> i, cout = up_init >> (i + 1);
+    MT_REQUIRE(uk[i] % ur[i] == 0 && (uk[i] - ur[i]) % 2 == 0,
+               "vocoder: upsample kernel %d must be a multiple of rate %d", uk[i], ur[i]);
+    MT_REQUIRE(cout % 32 == 0 || cout % 4 == 0, "vocoder: channels");
+    const std::string p = "ups." + std::to_string(i);
+    int w = L.add(p + ".weight", {cin, cout, uk[i]});
+    int b = L.add(p + ".bias", {cout});
+    ups.push_back(make_convT(cin, cout, uk[i], ur[i], (uk[i] - ur[i]) / 2, w, b, esize, pk));
+    ch = cout;
+  }
+  const int nk = (int)rk.size();
+  for (size_t i = 0; i < ur.size(); ++i) {
+    const int c = up_init >> (i + 1);
+    for (int j = 0; j < nk; ++j) {
+      const std::string p = "resblocks." + std::to_string(i * nk + j);
+      std::vector<GemmW> v1, v2;
+      const int k = rk[j];
+      for (size_t q = 0; q < rd[j].size(); ++q) {
+        const int d = rd[j][q];
+        if (resblock == 1) {
+          int w1 = L.add(p + ".convs1." + std::to_string(q) + ".weight", {c, c, k});
+          int b1 = L.add(p + ".convs1." + std::to_string(q) + ".bias", {c});
+          v1.push_back(make_conv(c, c, k, 1, (k * d - d) / 2, d, {w1}, b1, esize, pk));
+        } else {
+          int w1 = L.add(p + ".convs." + std::to_string(q) + ".weight", {c, c, k});
+          int b1 = L.add(p + ".convs." + std::to_string(q) + ".bias", {c});
+          v1.push_back(make_conv(c, c, k, 1, (k * d - d) / 2, d, {w1}, b1, esize, pk));
+        }
+      }
+      if (resblock == 1) {
+        for (size_t q = 0; q < rd[j].size(); ++q) {
+          int w2 = L.add(p + ".convs2." + std::to_string(q) + ".weight", {c, c, k});
+          int b2 = L.add(p + ".convs2." + std::to_string(q) + ".bias", {c});
+          v2.push_back(make_conv(c, c, k, 1, (k - 1) / 2, 1, {w2}, b2, esize, pk));
+        }
+      }
+      rb1.push_back(v1);
+      rb2.push_back(v2);
+    }
+  }
+  {
+    int w = L.add("conv_post.weight", {1, ch, 7});
+    int b = L.add("conv_post.bias", {1});
+    post = make_conv(1, ch, 7, 1, 3, 1, {w}, b, esize, pk);
+  }
+  packed_bytes = pk.off;
+  return 0;
+}
+
+int Vocoder::pack(const float* const* p, void* packed, hipStream_t st) const {
+  char* P = (char*)packed;
+  int rc;
+  if ((rc = pack_gemm(pre, dtype, p, P, st))) return rc;
+  for (const GemmW& g : ups)
+    if ((rc = pack_gemm(g, dtype, p, P, st))) return rc;
+  for (size_t i = 0; i < rb1.size(); ++i) {
+    for (const GemmW& g : rb1[i])
+      if ((rc = pack_gemm(g, dtype, p, P, st))) return rc;
+    for (const GemmW& g : rb2[i])
+      if ((rc = pack_gemm(g, dtype, p, P, st))) return rc;
+  }
+  return pack_gemm(post, dtype, p, P, st);
+}
+
+size_t Vocoder::frame_elems() const {
+  size_t m = (size_t)up_init;  // conv_pre output
+  size_t rate = 1;
+  for (size_t i = 0; i < up_rates.size(); ++i) {
+    rate *= up_rates[i];
+    m = std::max(m, rate * (size_t)(up_init >> (i + 1)));
+  }
+  return m;
+}
+
+size_t Vocoder::workspace_bytes(int B, int T) const {
+  const size_t big = align256((size_t)B * T * frame_elems() * esize);
+  return 4 * big + align256((size_t)B * T * n_mels * esize);
+}
+
+template <class E>
+int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav, char* ws,
+                       hipStream_t st) const {
+  int rc;
+  const size_t big = align256((size_t)B * T * frame_elems() * esize);
+  char* XS = ws;
+  char* X = ws + big;
+  char* Tb = ws + 2 * big;
+  char* R = ws + 3 * big;
+  char* xm = ws + 4 * big;
+  if ((rc = bct_to_btc(dtype, mel, B, n_mels, T, 1.f, xm, n_mels, 0, st))) return rc;
+  {
+    ConvArgs a = gemm_args(pre, P, B, T);
+    a.x0 = xm;
+    a.y = XS;
+    if ((rc = launch_conv<E, 0, 0>(a, st))) return rc;
+  }
+  int L = T;
+  const int nk = (int)rb_kernels.size();
+  for (size_t i = 0; i < ups.size(); ++i) {
+    ConvArgs u = gemm_args(ups[i], P, B, L);
+    u.x0 = XS;
+    u.y = X;
+    u.slope = 0.1f;
+    if ((rc = launch_conv<E, PF_LRELU, 0>(u, st))) return rc;
+    L = u.Tout;
+    for (int j = 0; j < nk; ++j) {
+      const std::vector<GemmW>& c1 = rb1[i * nk + j];
+      const std::vector<GemmW>& c2 = rb2[i * nk + j];
+      const int np = (int)c1.size();
+      const bool acc = j > 0, div = j == nk - 1;
+      const char* state = X;  // chain state entering each pair
+      for (int q = 0; q < np; ++q) {
+        const bool last = q == np - 1;
+        const char* xin = state;
+        // ResBlock1: the second conv reads Tb, so R may be updated in place. ResBlock2's conv
+        // reads the chain state itself (with a halo), so it ping-pongs R <-> Tb.
+        char* dst = last ? XS : (resblock == 1 ? R : (state == R ? Tb : R));
+        state = dst;
+        const char* src = xin;
+        if (resblock == 1) {
+          ConvArgs a = gemm_args(c1[q], P, B, L);
+          a.x0 = xin;
+          a.y = Tb;
+          a.slope = 0.1f;
+          if ((rc = launch_conv<E, PF_LRELU, 0>(a, st))) return rc;
+          src = Tb;
+        }
+        const GemmW& g = resblock == 1 ? c2[q] : c1[q];
+        ConvArgs b = gemm_args(g, P, B, L);
+        b.x0 = src;
+        b.y = dst;
+        b.slope = 0.1f;
+        b.resid = xin;
+        b.ldr = g.cout;
+        b.div = (float)nk;
+        if (!last) {
+          rc = launch_conv<E, PF_LRELU, EF_RESID>(b, st);
+        } else if (acc && div) {
+          rc = launch_conv<E, PF_LRELU, EF_RESID | EF_ACCUM | EF_DIV>(b, st);
+        } else if (acc) {
+          rc = launch_conv<E, PF_LRELU, EF_RESID | EF_ACCUM>(b, st);
+        } else if (div) {
+          rc = launch_conv<E, PF_LRELU, EF_RESID | EF_DIV>(b, st);
+        } else {
+          rc = launch_conv<E, PF_LRELU, EF_RESID>(b, st);
+        }
+        if (rc) return rc;
+      }
+    }
+  }
+  ConvArgs c = gemm_args(post, P, B, L);
+  c.x0 = XS;
+  c.y = wav;
+  c.ldy = 1;
+  c.slope = 0.01f;
+  return launch_conv<E, PF_LRELU, EF_TANH | EF_OUTF32>(c, st);
+}
+
+int Vocoder::forward(const void* packed, const float* mel, int B, int T, float* wav, void* ws, size_t ws_bytes,
+                     hipStream_t st) const {
+  MT_REQUIRE(B > 0 && T > 0, "vocoder: empty input");
+  MT_REQUIRE(ws_bytes >= workspace_bytes(B, T), "vocoder: workspace %zu < %zu", ws_bytes,
+             workspace_bytes(B, T));
+  if (dtype == BF16) return forward_t<bf16>((const char*)packed, mel, B, T, wav, (char*)ws, st);
+  return forward_t<float>((const char*)packed, mel, B, T, wav, (char*)ws, st);
+}
+
+}  // namespace mt

@@ -1,0 +1,146 @@
+"""Drop-in HiFi-GAN Generator (``from hifigan.models import Generator``, main.py:136).
+
+Same module tree and state_dict keys as the reference hifigan/models.py:14-206
+(weight-norm ``weight_g``/``weight_v`` before ``remove_weight_norm``, ``weight`` after),
+so ``Generator(AttrDict(v1)).load_state_dict(state["generator"])`` works unchanged.
+``forward`` is the HIP vocoder (matcha_hip ``mt_vocoder_forward``); the conv modules
+only hold parameters. The GAN discriminators/losses (hifigan/models.py:209-368) are
+training-only and outside the synthesis hot path.
+"""
+from __future__ import annotations
+
+import warnings
+
+import torch
+import torch.nn as nn
+from torch.nn import Conv1d, ConvTranspose1d
+
+from matcha_hip import runtime as rt
+
+from .xutils import get_padding
+
+LRELU_SLOPE = 0.1
+
+
+def _wn(m):
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", FutureWarning)
+        return torch.nn.utils.weight_norm(m)
+
+
+def _unwn(m):
+    if hasattr(m, "weight_g"):
+        torch.nn.utils.remove_weight_norm(m)
+
+
+def _folded_weight(m) -> torch.Tensor:
+    """W = g * v / ||v|| (norm over all dims but 0), or the plain weight after folding."""
+    if hasattr(m, "weight_g"):
+        return torch._weight_norm(m.weight_v, m.weight_g, 0)
+    return m.weight
+
+
+class ResBlock1(nn.Module):
+    """3 x [lrelu -> conv(k, d) -> lrelu -> conv(k, 1) -> + x] (hifigan/models.py:14-103)."""
+
+    def __init__(self, h, channels, kernel_size=3, dilation=(1, 3, 5)):
+        super().__init__()
+        self.h = h
+        self.convs1 = nn.ModuleList([
+            _wn(Conv1d(channels, channels, kernel_size, 1, dilation=d, padding=get_padding(kernel_size, d)))
+            for d in dilation])
+        self.convs2 = nn.ModuleList([
+            _wn(Conv1d(channels, channels, kernel_size, 1, dilation=1, padding=get_padding(kernel_size, 1)))
+            for _ in dilation])
+
+    def forward(self, x):
+        raise RuntimeError("ResBlock1 is evaluated inside the HIP vocoder (Generator.forward)")
+
+    def remove_weight_norm(self):
+        for m in list(self.convs1) + list(self.convs2):
+            _unwn(m)
+
+
+class ResBlock2(nn.Module):
+    """n x [lrelu -> conv(k, d) -> + x] (hifigan/models.py:106-145)."""
+
+    def __init__(self, h, channels, kernel_size=3, dilation=(1, 3)):
+        super().__init__()
+        self.h = h
+        self.convs = nn.ModuleList([
+            _wn(Conv1d(channels, channels, kernel_size, 1, dilation=d, padding=get_padding(kernel_size, d)))
+            for d in dilation])
+
+    def forward(self, x):
+        raise RuntimeError("ResBlock2 is evaluated inside the HIP vocoder (Generator.forward)")
+
+    def remove_weight_norm(self):
+        for m in self.convs:
+            _unwn(m)
+
+
+class Generator(nn.Module):
+    """mel [B,80,T] -> wav [B,1,T*prod(upsample_rates)] (hifigan/models.py:148-206)."""
+
+    def __init__(self, h, precision: str = "fp32"):
+        super().__init__()
+        self.h = h
+        self.num_kernels = len(h.resblock_kernel_sizes)
+        self.num_upsamples = len(h.upsample_rates)
+        self.conv_pre = _wn(Conv1d(80, h.upsample_initial_channel, 7, 1, padding=3))
+        rb = ResBlock1 if h.resblock == "1" else ResBlock2
+        self.ups = nn.ModuleList()
+        for i, (u, k) in enumerate(zip(h.upsample_rates, h.upsample_kernel_sizes)):
+            self.ups.append(_wn(ConvTranspose1d(h.upsample_initial_channel // (2 ** i),
+                                                h.upsample_initial_channel // (2 ** (i + 1)), k, u,
+                                                padding=(k - u) // 2)))
+        self.resblocks = nn.ModuleList()
+        ch = h.upsample_initial_channel
+        for i in range(len(self.ups)):
+            ch = h.upsample_initial_channel // (2 ** (i + 1))
+            for k, d in zip(h.resblock_kernel_sizes, h.resblock_dilation_sizes):
+                self.resblocks.append(rb(h, ch, k, d))
+        self.conv_post = _wn(Conv1d(ch, 1, 7, 1, padding=3))
+        for m in list(self.ups) + [self.conv_post]:
+            with torch.no_grad():
+                m.weight_v.normal_(0.0, 0.01)
+        self.precision = precision
+        self._engines = {}
+
+    # ---- HIP plumbing ----
+    def set_precision(self, precision: str):
+        rt.dtype_code(precision)
+        self.precision = precision
+        return self
+
+    def engine(self) -> rt.VocoderEngine:
+        if self.precision not in self._engines:
+            self._engines[self.precision] = rt.VocoderEngine(dict(self.h), self.precision)
+        return self._engines[self.precision]
+
+    def folded_state(self):
+        out = {}
+        for name, m in self.named_modules():
+            if isinstance(m, (Conv1d, ConvTranspose1d)):
+                out[name + ".weight"] = _folded_weight(m)
+                out[name + ".bias"] = m.bias
+        return out
+
+    def packed(self, device):
+        src = list(self.state_dict(keep_vars=True).values())
+        return self.engine().pack(self.folded_state, src, device)
+
+    def forward(self, x):
+        rt.require_gpu(x, what="Generator.forward")
+        x = rt.f32c(x)
+        with torch.no_grad():
+            return self.engine().forward(self.packed(x.device), x)
+
+    def remove_weight_norm(self):
+        print("Removing weight norm...")
+        for m in self.ups:
+            _unwn(m)
+        for m in self.resblocks:
+            m.remove_weight_norm()
+        _unwn(self.conv_pre)
+        _unwn(self.conv_post)

@@ -1,0 +1,96 @@
+"""ctypes binding of libmatcha_hip.so (C ABI: include/matcha_hip.h).
+
+The library is built in-tree (``make -C matcha-tts_amd`` or ``__graft_entry__.build()``)
+and loaded from ``matcha-tts_amd/libmatcha_hip.so``. There is no fallback: if the
+library is missing, every HIP entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int64, c_size_t, c_void_p
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libmatcha_hip.so")
+
+DTYPE_F32 = 0
+DTYPE_BF16 = 1
+SOLVER_EULER = 0
+SOLVER_MIDPOINT = 1
+
+P = c_void_p  # device pointer / opaque handle
+
+# name -> (restype, argtypes); mirrors include/matcha_hip.h one to one
+SIGNATURES = {
+    "mt_last_error": (c_char_p, []),
+    "mt_abi_version": (c_int, []),
+    "mt_decoder_create": (c_int, [c_int, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "mt_decoder_destroy": (None, [P]),
+    "mt_decoder_num_params": (c_int, [P]),
+    "mt_decoder_param_name": (c_int, [P, c_int, c_char_p, c_int]),
+    "mt_decoder_param_shape": (c_int, [P, c_int, POINTER(c_int64), c_int]),
+    "mt_decoder_packed_bytes": (c_size_t, [P]),
+    "mt_decoder_pack": (c_int, [P, POINTER(c_void_p), P, P]),
+    "mt_cfm_workspace_bytes": (c_size_t, [P, c_int, c_int, c_int, c_int]),
+    "mt_cfm_solve": (c_int, [P, P, P, c_float, P, P, P, c_int, c_int, c_int, c_int, P, P, c_size_t, P]),
+    "mt_decoder_step_workspace_bytes": (c_size_t, [P, c_int, c_int]),
+    "mt_decoder_step": (c_int, [P, P, P, P, P, P, c_float, c_int, c_int, P, P, c_size_t, P]),
+    "mt_vocoder_create": (c_int, [c_int, c_int, POINTER(c_int), POINTER(c_int), c_int, c_int,
+                                  POINTER(c_int), c_int, POINTER(c_int), c_int, POINTER(c_void_p)]),
+    "mt_vocoder_destroy": (None, [P]),
+    "mt_vocoder_num_params": (c_int, [P]),
+    "mt_vocoder_param_name": (c_int, [P, c_int, c_char_p, c_int]),
+    "mt_vocoder_param_shape": (c_int, [P, c_int, POINTER(c_int64), c_int]),
+    "mt_vocoder_packed_bytes": (c_size_t, [P]),
+    "mt_vocoder_pack": (c_int, [P, POINTER(c_void_p), P, P]),
+    "mt_vocoder_workspace_bytes": (c_size_t, [P, c_int, c_int]),
+    "mt_vocoder_forward": (c_int, [P, P, P, c_int, c_int, P, P, c_size_t, P]),
+    "mt_durations": (c_int, [P, P, c_float, c_int, c_int, P, P, P, P]),
+    "mt_alignment": (c_int, [P, P, c_int, c_int, c_int, P, c_int, P, P, P, P]),
+    "mt_denorm_crop": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P]),
+    "mt_denoise_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "mt_denoise": (c_int, [P, c_int, c_int, P, c_float, P, P, c_size_t, P]),
+    "mt_stft_magnitude": (c_int, [P, c_int, c_int, P, P]),
+    "mt_op_conv1d_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    "mt_op_conv1d": (c_int, [c_int, P, c_int, c_int, c_int, P, P, c_int, c_int, c_int, c_int, c_int,
+                             c_int, c_float, P, c_int, P, c_size_t, P]),
+    "mt_op_attention": (c_int, [c_int, P, P, P, c_int, c_int, c_int, P]),
+}
+
+_lib = None
+
+
+class HipPathError(RuntimeError):
+    """Raised when the native library is unavailable or a C entry point fails."""
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipPathError(
+                f"{LIB_PATH} is missing: build it with `make -C matcha-tts_amd` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().mt_last_error().decode(errors="replace")
+        raise HipPathError(f"matcha_hip {what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,321 @@
+"""Host runtime over the C ABI: handles, packed-weight caches and workspaces.
+
+PyTorch owns every device buffer (inputs, outputs, packed weights, workspaces); the
+library only enqueues kernels on the current stream. All entry points require CUDA
+(ROCm) tensors and raise ``HipPathError`` otherwise — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import math
+from ctypes import byref, c_char_p, c_int, c_int64, c_void_p, create_string_buffer
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from ._lib import (DTYPE_BF16, DTYPE_F32, SOLVER_EULER, SOLVER_MIDPOINT, HipPathError, check, lib,
+                   ptr, stream_handle)
+
+_DTYPES = {"fp32": DTYPE_F32, "float32": DTYPE_F32, "f32": DTYPE_F32,
+           "bf16": DTYPE_BF16, "bfloat16": DTYPE_BF16}
+
+
+def dtype_code(precision: str) -> int:
+    try:
+        return _DTYPES[precision]
+    except KeyError:
+        raise ValueError(f"precision must be one of {sorted(set(_DTYPES))}, got {precision!r}")
+
+
+def require_gpu(*tensors, what: str = "matcha_hip") -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise HipPathError(
+                f"{what}: the synthesis path runs on the MI355X (ROCm) device only; got a tensor on "
+                f"{t.device}. Move the model and inputs to 'cuda'.")
+
+
+def f32c(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if t is None:
+        return None
+    return t.detach().to(torch.float32).contiguous()
+
+
+class _Workspace:
+    """Grow-only device scratch per (device, stream)."""
+
+    _bufs: Dict[Tuple[int, int], torch.Tensor] = {}
+
+    @classmethod
+    def get(cls, nbytes: int, device: torch.device) -> torch.Tensor:
+        key = (device.index if device.index is not None else torch.cuda.current_device(),
+               stream_handle(device))
+        buf = cls._bufs.get(key)
+        if buf is None or buf.numel() < nbytes:
+            cls._bufs.pop(key, None)
+            buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+            cls._bufs[key] = buf
+        return buf
+
+
+def _param_list(h, num_fn, name_fn, shape_fn) -> List[Tuple[str, Tuple[int, ...]]]:
+    L = lib()
+    n = getattr(L, num_fn)(h)
+    out = []
+    buf = create_string_buffer(256)
+    shp = (c_int64 * 8)()
+    for i in range(n):
+        check(getattr(L, name_fn)(h, i, buf, 256), name_fn)
+        nd = getattr(L, shape_fn)(h, i, shp, 8)
+        if nd < 0:
+            check(nd, shape_fn)
+        out.append((buf.value.decode(), tuple(int(shp[k]) for k in range(nd))))
+    return out
+
+
+def fingerprint(tensors: List[torch.Tensor]) -> Tuple:
+    return tuple((t.data_ptr(), t._version, tuple(t.shape), str(t.device)) for t in tensors)
+
+
+def sinus_freq(c_cond: int) -> torch.Tensor:
+    """model.py:757-759 frequency table, formed exactly as the reference does (fp32, CPU)."""
+    half = c_cond // 2
+    e = math.log(10000) / (half - 1)
+    return torch.exp(torch.arange(half).float() * -e)
+
+
+class DecoderEngine:
+    """mt_decoder handle: U-Net estimator + CFM solver for one (c_cond, dtype)."""
+
+    def __init__(self, c_cond: int, n_mid: int, n_blocks: int, heads: int, precision: str):
+        self.c_cond, self.dtype = c_cond, dtype_code(precision)
+        h = c_void_p()
+        check(lib().mt_decoder_create(c_cond, n_mid, n_blocks, heads, self.dtype, byref(h)),
+              "decoder_create")
+        self.h = h
+        self.specs = _param_list(h, "mt_decoder_num_params", "mt_decoder_param_name",
+                                 "mt_decoder_param_shape")
+        self.packed_bytes = lib().mt_decoder_packed_bytes(h)
+        self._packed = None
+        self._fp = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().mt_decoder_destroy(self.h)
+        except Exception:
+            pass
+
+    def pack(self, params: Dict[str, torch.Tensor], device: torch.device) -> torch.Tensor:
+        """params: estimator-relative reference keys -> tensors (any device/dtype)."""
+        tensors = []
+        for name, shape in self.specs:
+            if name == "_sinus_freq":
+                t = sinus_freq(self.c_cond)
+            else:
+                if name not in params:
+                    raise KeyError(f"estimator parameter {name!r} missing")
+                t = params[name]
+            if tuple(t.shape) != shape:
+                raise ValueError(f"{name}: shape {tuple(t.shape)} != expected {shape}")
+            tensors.append(t)
+        fp = fingerprint([t for (n, _), t in zip(self.specs, tensors) if n != "_sinus_freq"]) + (str(device),)
+        if self._packed is not None and fp == self._fp:
+            return self._packed
+        dev = [t.detach().to(device=device, dtype=torch.float32).contiguous() for t in tensors]
+        packed = torch.empty(self.packed_bytes, dtype=torch.uint8, device=device)
+        arr = (c_void_p * len(dev))(*[t.data_ptr() for t in dev])
+        check(lib().mt_decoder_pack(self.h, arr, packed.data_ptr(), stream_handle(device)), "decoder_pack")
+        torch.cuda.current_stream(device).synchronize()  # staging copies die with `dev`
+        self._packed, self._fp = packed, fp
+        return packed
+
+    def solve(self, packed, z_noise, temperature, mu_y, mask, spks, n_timesteps, solver="euler",
+              out=None):
+        B, C, T = mu_y.shape
+        s = SOLVER_EULER if solver == "euler" else SOLVER_MIDPOINT if solver == "midpoint" else None
+        if s is None:
+            raise NotImplementedError(f"Solver {solver} not implemented")
+        out = torch.empty_like(mu_y) if out is None else out
+        L = lib()
+        nbytes = L.mt_cfm_workspace_bytes(self.h, B, T, n_timesteps, s)
+        ws = _Workspace.get(nbytes, mu_y.device)
+        check(L.mt_cfm_solve(self.h, packed.data_ptr(), ptr(z_noise), float(temperature), ptr(mu_y),
+                             ptr(mask), ptr(spks), B, T, int(n_timesteps), s, ptr(out), ws.data_ptr(),
+                             ws.numel(), stream_handle(mu_y.device)), "cfm_solve")
+        return out
+
+    def step(self, packed, x, mu_y, mask, spks, t: float, out=None):
+        B, C, T = mu_y.shape
+        out = torch.empty_like(mu_y) if out is None else out
+        L = lib()
+        nbytes = L.mt_decoder_step_workspace_bytes(self.h, B, T)
+        ws = _Workspace.get(nbytes, mu_y.device)
+        check(L.mt_decoder_step(self.h, packed.data_ptr(), ptr(x), ptr(mu_y), ptr(mask), ptr(spks), float(t),
+                                B, T, ptr(out), ws.data_ptr(), ws.numel(), stream_handle(mu_y.device)),
+              "decoder_step")
+        return out
+
+
+class VocoderEngine:
+    """mt_vocoder handle: HiFi-GAN Generator for one config and dtype."""
+
+    def __init__(self, h: dict, precision: str):
+        self.dtype = dtype_code(precision)
+        ur, uk = list(h["upsample_rates"]), list(h["upsample_kernel_sizes"])
+        rk = list(h["resblock_kernel_sizes"])
+        rd = [list(d) for d in h["resblock_dilation_sizes"]]
+        nd = len(rd[0])
+        if any(len(d) != nd for d in rd):
+            raise ValueError("resblock dilation lists must have equal length")
+        flat = [x for d in rd for x in d]
+        ci = lambda v: (c_int * len(v))(*v)  # noqa: E731
+        hdl = c_void_p()
+        check(lib().mt_vocoder_create(1 if str(h["resblock"]) == "1" else 2, len(ur), ci(ur), ci(uk),
+                                      int(h["upsample_initial_channel"]), len(rk), ci(rk), nd, ci(flat),
+                                      self.dtype, byref(hdl)), "vocoder_create")
+        self.h = hdl
+        self.hop = int(math.prod(ur))
+        self.specs = _param_list(hdl, "mt_vocoder_num_params", "mt_vocoder_param_name",
+                                 "mt_vocoder_param_shape")
+        self.packed_bytes = lib().mt_vocoder_packed_bytes(hdl)
+        self._packed = None
+        self._fp = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().mt_vocoder_destroy(self.h)
+        except Exception:
+            pass
+
+    def pack(self, params_fn, src: List[torch.Tensor], device: torch.device) -> torch.Tensor:
+        """params_fn() -> folded reference-keyed weights; repacked only when ``src`` changes."""
+        fp = fingerprint(src) + (str(device),)
+        if self._packed is not None and fp == self._fp:
+            return self._packed
+        params = params_fn()
+        tensors = []
+        for name, shape in self.specs:
+            if name not in params:
+                raise KeyError(f"vocoder parameter {name!r} missing")
+            t = params[name]
+            if tuple(t.shape) != shape:
+                raise ValueError(f"{name}: shape {tuple(t.shape)} != expected {shape}")
+            tensors.append(t)
+        dev = [t.detach().to(device=device, dtype=torch.float32).contiguous() for t in tensors]
+        packed = torch.empty(self.packed_bytes, dtype=torch.uint8, device=device)
+        arr = (c_void_p * len(dev))(*[t.data_ptr() for t in dev])
+        check(lib().mt_vocoder_pack(self.h, arr, packed.data_ptr(), stream_handle(device)), "vocoder_pack")
+        torch.cuda.current_stream(device).synchronize()
+        self._packed, self._fp = packed, fp
+        return packed
+
+    def forward(self, packed, mel, out=None):
+        B, C, T = mel.shape
+        out = torch.empty((B, 1, T * self.hop), dtype=torch.float32, device=mel.device) if out is None else out
+        L = lib()
+        ws = _Workspace.get(L.mt_vocoder_workspace_bytes(self.h, B, T), mel.device)
+        check(L.mt_vocoder_forward(self.h, packed.data_ptr(), ptr(mel), B, T, ptr(out), ws.data_ptr(),
+                                   ws.numel(), stream_handle(mel.device)), "vocoder_forward")
+        return out
+
+
+# ---- index path / small ops ---------------------------------------------------------------
+
+def durations(logw: torch.Tensor, x_mask: torch.Tensor, length_scale: float):
+    """model.py:1273-1275 -> (w_ceil [B,1,Tx], cum [B,Tx], y_lengths int64 [B])."""
+    require_gpu(logw, x_mask, what="durations")
+    logw, x_mask = f32c(logw), f32c(x_mask)
+    B, _, Tx = logw.shape
+    w_ceil = torch.empty((B, 1, Tx), dtype=torch.float32, device=logw.device)
+    cum = torch.empty((B, Tx), dtype=torch.float32, device=logw.device)
+    yl = torch.empty((B,), dtype=torch.int64, device=logw.device)
+    check(lib().mt_durations(ptr(logw), ptr(x_mask), float(length_scale), B, Tx, ptr(w_ceil), ptr(cum),
+                             ptr(yl), stream_handle(logw.device)), "durations")
+    return w_ceil, cum, yl
+
+
+def alignment(cum: torch.Tensor, y_lengths: torch.Tensor, t_pad: int, mu: Optional[torch.Tensor],
+              want_attn: bool = True):
+    """model.py:1283-1289 -> (attn [B,1,Tx,T] | None, mu_y [B,C,T] | None, y_mask [B,1,T])."""
+    B, Tx = cum.shape
+    dev = cum.device
+    attn = torch.empty((B, 1, Tx, t_pad), dtype=torch.float32, device=dev) if want_attn else None
+    C = 0 if mu is None else mu.shape[1]
+    mu = f32c(mu)
+    mu_y = torch.empty((B, C, t_pad), dtype=torch.float32, device=dev) if mu is not None else None
+    y_mask = torch.empty((B, 1, t_pad), dtype=torch.float32, device=dev)
+    check(lib().mt_alignment(ptr(cum), ptr(y_lengths), B, Tx, t_pad, ptr(mu), C, ptr(attn), ptr(mu_y),
+                             ptr(y_mask), stream_handle(dev)), "alignment")
+    return attn, mu_y, y_mask
+
+
+def denorm_crop(z: torch.Tensor, mean: torch.Tensor, std: torch.Tensor, t_y: int) -> torch.Tensor:
+    B, C, T = z.shape
+    mean = f32c(mean.to(z.device)).reshape(-1).expand(C).contiguous()
+    std = f32c(std.to(z.device)).reshape(-1).expand(C).contiguous()
+    out = torch.empty((B, C, t_y), dtype=torch.float32, device=z.device)
+    check(lib().mt_denorm_crop(ptr(z), ptr(mean), ptr(std), B, C, T, t_y, ptr(out), stream_handle(z.device)),
+          "denorm_crop")
+    return out
+
+
+def stft_magnitude(audio: torch.Tensor) -> torch.Tensor:
+    require_gpu(audio, what="stft_magnitude")
+    audio = f32c(audio)
+    B, L = audio.shape
+    nfr = 1 + L // 256
+    mag = torch.empty((B, nfr, 513), dtype=torch.float32, device=audio.device)
+    check(lib().mt_stft_magnitude(ptr(audio), B, L, ptr(mag), stream_handle(audio.device)), "stft_magnitude")
+    return mag
+
+
+def denoise(audio: torch.Tensor, bias_spec: torch.Tensor, strength: float) -> torch.Tensor:
+    require_gpu(audio, what="denoise")
+    audio = f32c(audio)
+    B, L = audio.shape
+    out = torch.empty((B, 256 * (L // 256)), dtype=torch.float32, device=audio.device)
+    bias = f32c(bias_spec.reshape(-1).to(audio.device))
+    L_ = lib()
+    ws = _Workspace.get(L_.mt_denoise_workspace_bytes(B, L), audio.device)
+    check(L_.mt_denoise(ptr(audio), B, L, ptr(bias), float(strength), ptr(out), ws.data_ptr(), ws.numel(),
+                        stream_handle(audio.device)), "denoise")
+    return out
+
+
+def op_conv1d(x_btc: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], stride=1, pad=0, dil=1,
+              transposed=False, slope: Optional[float] = None, precision="fp32") -> torch.Tensor:
+    """Op-level test entry: y = conv(lrelu(x)) on [B,T,C] activations (dtype by precision)."""
+    require_gpu(x_btc, what="op_conv1d")
+    dt = dtype_code(precision)
+    et = torch.bfloat16 if dt == DTYPE_BF16 else torch.float32
+    x = x_btc.to(et).contiguous()
+    B, Tin, cin = x.shape
+    if transposed:
+        cout, k = W.shape[1], W.shape[2]
+        tout = (Tin - 1) * stride - 2 * pad + k
+    else:
+        cout, k = W.shape[0], W.shape[2]
+        tout = (Tin + 2 * pad - dil * (k - 1) - 1) // stride + 1
+    y = torch.empty((B, tout, cout), dtype=et, device=x.device)
+    L = lib()
+    nb = L.mt_op_conv1d_workspace_bytes(dt, cin, cout, k, stride, int(transposed))
+    ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
+    W, bias = f32c(W), f32c(bias)
+    check(L.mt_op_conv1d(dt, ptr(x), B, Tin, cin, ptr(W), ptr(bias), cout, k, stride, pad, dil, int(transposed),
+                         -1.0 if slope is None else float(slope), ptr(y), tout, ws.data_ptr(), ws.numel(),
+                         stream_handle(x.device)), "op_conv1d")
+    return y
+
+
+def op_attention(qkv: torch.Tensor, mask: torch.Tensor, heads: int, precision="fp32") -> torch.Tensor:
+    require_gpu(qkv, mask, what="op_attention")
+    dt = dtype_code(precision)
+    et = torch.bfloat16 if dt == DTYPE_BF16 else torch.float32
+    qkv = qkv.to(et).contiguous()
+    B, T, _ = qkv.shape
+    out = torch.empty((B, T, heads * 64), dtype=et, device=qkv.device)
+    mask = f32c(mask.reshape(B, T))
+    check(lib().mt_op_attention(dt, ptr(qkv), ptr(mask), ptr(out), B, T, heads, stream_handle(qkv.device)),
+          "op_attention")
+    return out

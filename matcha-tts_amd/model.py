@@ -1,0 +1,539 @@
+"""Drop-in ``model`` module: ``from model import MatchaTTS`` (main.py:8) on MI355X.
+
+Call surface and state_dict keys are those of the reference ``model.py``
+(Lounes78/matcha-tts): ``MatchaTTS(n_vocab, n_spks, spk_emb_dim, encoder_params,
+decoder_params, cfm_params, duration_predictor_params)``, ``.synthesize(...) ->
+(mel, y_lengths, attn)`` (model.py:1264-1300), plus the upstream-style
+``synthesise(...) -> dict`` used by the notebooks.
+
+What runs where:
+  * text encoder + duration predictor (model.py:148-535): host PyTorch (ROCm), as the
+    north star keeps it (SURVEY.md §2, §8f row 1 = next);
+  * duration -> alignment index path, CFM Euler/midpoint solver over the U-Net
+    estimator, denormalize/crop: hand-written HIP kernels behind the C ABI
+    (include/matcha_hip.h) — ``matcha_hip.runtime``.
+The estimator modules below only hold parameters (reference names/shapes); their
+forward is the HIP kernels. There is no CPU fallback for the HIP parts.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from matcha_hip import runtime as rt
+
+
+# ======================================================================================
+# utilities (model.py:42-125)
+# ======================================================================================
+
+def sequence_mask(length: torch.Tensor, max_length: Optional[int] = None) -> torch.Tensor:
+    if max_length is None:
+        max_length = int(length.max())
+    ar = torch.arange(int(max_length), dtype=length.dtype, device=length.device)
+    return ar[None, :] < length[:, None]
+
+
+def fix_len_compatibility(length, num_downsamplings_in_unet: int = 2) -> int:
+    """Round up to a multiple of 2**n (host int; model.py:49-55 ends in .item())."""
+    f = 2 ** num_downsamplings_in_unet
+    return int(math.ceil(int(length) / f) * f)
+
+
+def denormalize(data, mu, std):
+    mu = torch.as_tensor(mu, dtype=data.dtype, device=data.device)
+    std = torch.as_tensor(std, dtype=data.dtype, device=data.device)
+    return data * std.reshape(-1, 1) + mu.reshape(-1, 1)
+
+
+def normalize(data, mu, std):
+    mu = torch.as_tensor(mu, dtype=data.dtype, device=data.device)
+    std = torch.as_tensor(std, dtype=data.dtype, device=data.device)
+    return (data - mu.reshape(-1, 1)) / std.reshape(-1, 1)
+
+
+def _get(p, k, default=None):
+    if isinstance(p, dict):
+        return p.get(k, default)
+    return getattr(p, k, default)
+
+
+# ======================================================================================
+# text encoder (host PyTorch)  model.py:148-535
+# ======================================================================================
+
+class LayerNorm(nn.Module):
+    """Channel LayerNorm over dim 1 of [B,C,T] (model.py:148-166)."""
+
+    def __init__(self, channels: int, eps: float = 1e-4):
+        super().__init__()
+        self.channels, self.eps = channels, eps
+        self.gamma = nn.Parameter(torch.ones(channels))
+        self.beta = nn.Parameter(torch.zeros(channels))
+
+    def forward(self, x):
+        mean = x.mean(1, keepdim=True)
+        var = ((x - mean) ** 2).mean(1, keepdim=True)
+        y = (x - mean) * torch.rsqrt(var + self.eps)
+        return y * self.gamma[None, :, None] + self.beta[None, :, None]
+
+
+class ConvReluNorm(nn.Module):
+    """Prenet (model.py:171-208): n x (conv(x*mask) -> LayerNorm -> ReLU), zero-init 1x1 proj, residual."""
+
+    def __init__(self, in_channels, hidden_channels, out_channels, kernel_size, n_layers, p_dropout):
+        super().__init__()
+        self.n_layers = n_layers
+        self.conv_layers = nn.ModuleList(
+            [nn.Conv1d(in_channels if i == 0 else hidden_channels, hidden_channels, kernel_size,
+                       padding=kernel_size // 2) for i in range(n_layers)])
+        self.norm_layers = nn.ModuleList([LayerNorm(hidden_channels) for _ in range(n_layers)])
+        self.relu_drop = nn.Sequential(nn.ReLU(), nn.Dropout(p_dropout))
+        self.proj = nn.Conv1d(hidden_channels, out_channels, 1)
+        nn.init.zeros_(self.proj.weight)
+        nn.init.zeros_(self.proj.bias)
+
+    def forward(self, x, x_mask):
+        h = x
+        for conv, norm in zip(self.conv_layers, self.norm_layers):
+            h = self.relu_drop(norm(conv(h * x_mask)))
+        return (x + self.proj(h)) * x_mask
+
+
+class DurationPredictor(nn.Module):
+    """model.py:210-235: conv -> relu -> LayerNorm (x2) -> 1x1 -> log-durations."""
+
+    def __init__(self, in_channels, filter_channels, kernel_size, p_dropout):
+        super().__init__()
+        self.drop = nn.Dropout(p_dropout)
+        self.conv_1 = nn.Conv1d(in_channels, filter_channels, kernel_size, padding=kernel_size // 2)
+        self.norm_1 = LayerNorm(filter_channels)
+        self.conv_2 = nn.Conv1d(filter_channels, filter_channels, kernel_size, padding=kernel_size // 2)
+        self.norm_2 = LayerNorm(filter_channels)
+        self.proj = nn.Conv1d(filter_channels, 1, 1)
+
+    def forward(self, x, x_mask):
+        h = self.drop(self.norm_1(torch.relu(self.conv_1(x * x_mask))))
+        h = self.drop(self.norm_2(torch.relu(self.conv_2(h * x_mask))))
+        return self.proj(h * x_mask) * x_mask
+
+
+class RotaryPositionalEmebeddings(nn.Module):
+    """RoPE on the first d features of [B,H,T,C] (model.py:244-292; name kept for compatibility)."""
+
+    def __init__(self, d, base: int = 10_000):
+        super().__init__()
+        self.d, self.base = int(d), base
+
+    def forward(self, x):
+        t = x.shape[2]
+        theta = 1.0 / (self.base ** (torch.arange(0, self.d, 2, device=x.device).float() / self.d))
+        ang = torch.outer(torch.arange(t, device=x.device).float(), theta)
+        ang = torch.cat([ang, ang], dim=1)
+        cos, sin = ang.cos()[None, None], ang.sin()[None, None]
+        xr, xp = x[..., : self.d], x[..., self.d:]
+        h = self.d // 2
+        rot = torch.cat([-xr[..., h:], xr[..., :h]], dim=-1)
+        return torch.cat([xr * cos + rot * sin, xp], dim=-1)
+
+
+class MultiHeadAttention(nn.Module):
+    """RoPE multi-head attention with 1x1-conv projections (model.py:294-372)."""
+
+    def __init__(self, channels, out_channels, n_heads, heads_share=True, p_dropout=0.0,
+                 proximal_bias=False, proximal_init=False):
+        super().__init__()
+        assert channels % n_heads == 0, "channels must be divisible by n_heads"
+        self.channels, self.n_heads = channels, n_heads
+        self.k_channels = channels // n_heads
+        self.proximal_bias = proximal_bias
+        self.attn = None
+        self.conv_q = nn.Conv1d(channels, channels, 1)
+        self.conv_k = nn.Conv1d(channels, channels, 1)
+        self.conv_v = nn.Conv1d(channels, channels, 1)
+        self.query_rotary_pe = RotaryPositionalEmebeddings(self.k_channels * 0.5)
+        self.key_rotary_pe = RotaryPositionalEmebeddings(self.k_channels * 0.5)
+        self.conv_o = nn.Conv1d(channels, out_channels, 1)
+        self.drop = nn.Dropout(p_dropout)
+        nn.init.xavier_uniform_(self.conv_q.weight)
+        nn.init.xavier_uniform_(self.conv_k.weight)
+        if proximal_init:
+            with torch.no_grad():
+                self.conv_k.weight.copy_(self.conv_q.weight)
+                self.conv_k.bias.copy_(self.conv_q.bias)
+        nn.init.xavier_uniform_(self.conv_v.weight)
+
+    def forward(self, x, c, attn_mask=None):
+        q, k, v = self.conv_q(x), self.conv_k(c), self.conv_v(c)
+        b, d, t = k.shape
+        tq = q.shape[2]
+
+        def heads(z, n):
+            return z.view(b, self.n_heads, self.k_channels, n).transpose(2, 3)
+
+        q, k, v = heads(q, tq), heads(k, t), heads(v, t)
+        q, k = self.query_rotary_pe(q), self.key_rotary_pe(k)
+        s = torch.matmul(q, k.transpose(-2, -1)) / math.sqrt(self.k_channels)
+        if self.proximal_bias:
+            r = torch.arange(t, dtype=torch.float32, device=s.device)
+            s = s + (-torch.log1p(torch.abs(r[None] - r[:, None])))[None, None].to(s.dtype)
+        if attn_mask is not None:
+            s = s.masked_fill(attn_mask == 0, -1e4)
+        p = self.drop(torch.softmax(s, dim=-1))
+        self.attn = p
+        o = torch.matmul(p, v).transpose(2, 3).contiguous().view(b, d, tq)
+        return self.conv_o(o)
+
+
+class FFN(nn.Module):
+    def __init__(self, in_channels, out_channels, filter_channels, kernel_size, p_dropout=0.0):
+        super().__init__()
+        self.conv_1 = nn.Conv1d(in_channels, filter_channels, kernel_size, padding=kernel_size // 2)
+        self.conv_2 = nn.Conv1d(filter_channels, out_channels, kernel_size, padding=kernel_size // 2)
+        self.drop = nn.Dropout(p_dropout)
+
+    def forward(self, x, x_mask):
+        h = self.drop(torch.relu(self.conv_1(x * x_mask)))
+        return self.conv_2(h * x_mask) * x_mask
+
+
+class Encoder(nn.Module):
+    def __init__(self, hidden_channels, filter_channels, n_heads, n_layers, kernel_size=1, p_dropout=0.0):
+        super().__init__()
+        self.n_layers = n_layers
+        self.drop = nn.Dropout(p_dropout)
+        self.attn_layers = nn.ModuleList(
+            [MultiHeadAttention(hidden_channels, hidden_channels, n_heads, p_dropout=p_dropout)
+             for _ in range(n_layers)])
+        self.norm_layers_1 = nn.ModuleList([LayerNorm(hidden_channels) for _ in range(n_layers)])
+        self.ffn_layers = nn.ModuleList(
+            [FFN(hidden_channels, hidden_channels, filter_channels, kernel_size, p_dropout=p_dropout)
+             for _ in range(n_layers)])
+        self.norm_layers_2 = nn.ModuleList([LayerNorm(hidden_channels) for _ in range(n_layers)])
+
+    def forward(self, x, x_mask):
+        amask = x_mask.unsqueeze(2) * x_mask.unsqueeze(-1)
+        for attn, n1, ffn, n2 in zip(self.attn_layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2):
+            x = x * x_mask
+            x = n1(x + self.drop(attn(x, x, amask)))
+            x = n2(x + self.drop(ffn(x, x_mask)))
+        return x * x_mask
+
+
+class TextEncoder(nn.Module):
+    """model.py:452-535 -> (mu [B,n_feats,Tx], logw [B,1,Tx], x_mask [B,1,Tx])."""
+
+    def __init__(self, encoder_type, encoder_params, duration_predictor_params, n_vocab, n_spks=1,
+                 spk_emb_dim=128):
+        super().__init__()
+        self.encoder_type = encoder_type
+        self.n_vocab = n_vocab
+        self.n_feats = _get(encoder_params, "n_feats")
+        self.n_channels = _get(encoder_params, "n_channels")
+        self.spk_emb_dim, self.n_spks = spk_emb_dim, n_spks
+        self.emb = nn.Embedding(n_vocab, self.n_channels)
+        nn.init.normal_(self.emb.weight, 0.0, self.n_channels ** -0.5)
+        if _get(encoder_params, "prenet"):
+            self.prenet = ConvReluNorm(self.n_channels, self.n_channels, self.n_channels, kernel_size=5,
+                                       n_layers=3, p_dropout=0.5)
+        else:
+            self.prenet = lambda x, x_mask: x
+        width = self.n_channels + (spk_emb_dim if n_spks > 1 else 0)
+        self.encoder = Encoder(width, _get(encoder_params, "filter_channels"), _get(encoder_params, "n_heads"),
+                               _get(encoder_params, "n_layers"), _get(encoder_params, "kernel_size"),
+                               _get(encoder_params, "p_dropout"))
+        self.proj_m = nn.Conv1d(width, self.n_feats, 1)
+        self.proj_w = DurationPredictor(width, _get(duration_predictor_params, "filter_channels_dp"),
+                                        _get(duration_predictor_params, "kernel_size"),
+                                        _get(duration_predictor_params, "p_dropout"))
+
+    def forward(self, x, x_lengths, spks=None):
+        h = (self.emb(x) * math.sqrt(self.n_channels)).transpose(1, -1)
+        x_mask = sequence_mask(x_lengths, h.size(2)).unsqueeze(1).to(h.dtype)
+        h = self.prenet(h, x_mask)
+        if self.n_spks > 1:
+            h = torch.cat([h, spks.unsqueeze(-1).expand(-1, -1, h.shape[-1])], dim=1)
+        h = self.encoder(h, x_mask)
+        mu = self.proj_m(h) * x_mask
+        logw = self.proj_w(h.detach(), x_mask)
+        return mu, logw, x_mask
+
+
+# ======================================================================================
+# U-Net estimator parameter containers (state_dict keys of model.py:576-962).
+# Their arithmetic is the HIP estimator; they have no torch forward of their own.
+# ======================================================================================
+
+class _Params(nn.Module):
+    def forward(self, *a, **k):
+        raise RuntimeError(f"{type(self).__name__} is evaluated by the HIP estimator (Decoder.forward)")
+
+
+class LoRACompatibleLinear(nn.Linear):
+    pass
+
+
+class SnakeBeta(_Params):
+    def __init__(self, in_features, out_features, alpha=1.0, alpha_trainable=True, alpha_logscale=True):
+        super().__init__()
+        n = out_features if isinstance(out_features, int) else out_features[0]
+        self.proj = nn.Linear(in_features, n)
+        self.alpha_logscale = alpha_logscale
+        init = torch.zeros(n) if alpha_logscale else torch.ones(n) * alpha
+        self.alpha = nn.Parameter(init.clone(), requires_grad=alpha_trainable)
+        self.beta = nn.Parameter(init.clone(), requires_grad=alpha_trainable)
+        self.no_div_by_zero = 1e-9
+
+
+class FeedForward(_Params):
+    def __init__(self, dim, dim_out=None, mult=4, dropout=0.0, activation_fn="snakebeta", final_dropout=False):
+        super().__init__()
+        if activation_fn != "snakebeta":
+            raise NotImplementedError("the HIP estimator implements the SnakeBeta feed-forward (main.py:74)")
+        inner = int(dim * mult)
+        self.net = nn.ModuleList([SnakeBeta(dim, inner), nn.Dropout(dropout), nn.Linear(inner, dim_out or dim)])
+        if final_dropout:
+            self.net.append(nn.Dropout(dropout))
+
+
+class Attention(_Params):
+    def __init__(self, query_dim, heads=8, dim_head=64, dropout=0.0, bias=False, cross_attention_dim=None,
+                 upcast_attention=False):
+        super().__init__()
+        if cross_attention_dim is not None:
+            raise NotImplementedError("the reference decoder uses self-attention only (model.py:721-736)")
+        if dim_head != 64:
+            raise NotImplementedError("the HIP attention kernel is built for head dim 64")
+        inner = heads * dim_head
+        self.heads, self.scale = heads, dim_head ** -0.5
+        self.to_q = nn.Linear(query_dim, inner, bias=bias)
+        self.to_k = nn.Linear(query_dim, inner, bias=bias)
+        self.to_v = nn.Linear(query_dim, inner, bias=bias)
+        self.to_out = nn.ModuleList([nn.Linear(inner, query_dim), nn.Dropout(dropout)])
+
+
+class BasicTransformerBlock(_Params):
+    def __init__(self, dim, num_attention_heads, attention_head_dim, dropout=0.0, activation_fn="snakebeta",
+                 attention_bias=False):
+        super().__init__()
+        if attention_bias:
+            raise NotImplementedError("attention_bias=True is not used by the reference decoder")
+        self.norm1 = nn.LayerNorm(dim)
+        self.attn1 = Attention(dim, num_attention_heads, attention_head_dim, dropout, attention_bias)
+        self.norm3 = nn.LayerNorm(dim)
+        self.ff = FeedForward(dim, dropout=dropout, activation_fn=activation_fn)
+
+
+class SinusoidalPosEmb(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        assert dim % 2 == 0, "SinusoidalPosEmb requires dim to be even"
+        self.dim = dim
+
+    def forward(self, x, scale=1000):   # host helper (model.py:753-762); the HIP path has its own
+        x = x.reshape(-1)
+        emb = scale * x.unsqueeze(1) * rt.sinus_freq(self.dim).to(x.device).unsqueeze(0)
+        return torch.cat((emb.sin(), emb.cos()), dim=-1)
+
+
+class Block1D(_Params):
+    def __init__(self, dim, dim_out, groups=8):
+        super().__init__()
+        self.block = nn.Sequential(nn.Conv1d(dim, dim_out, 3, padding=1), nn.GroupNorm(groups, dim_out), nn.Mish())
+
+
+class ResnetBlock1D(_Params):
+    def __init__(self, dim, dim_out, time_emb_dim, groups=8):
+        super().__init__()
+        self.mlp = nn.Sequential(nn.Mish(), nn.Linear(time_emb_dim, dim_out))
+        self.block1 = Block1D(dim, dim_out, groups=groups)
+        self.block2 = Block1D(dim_out, dim_out, groups=groups)
+        self.res_conv = nn.Conv1d(dim, dim_out, 1)
+
+
+class Downsample1D(_Params):
+    def __init__(self, dim):
+        super().__init__()
+        self.conv = nn.Conv1d(dim, dim, 3, 2, 1)
+
+
+class Upsample1D(_Params):
+    def __init__(self, channels, use_conv_transpose=True, out_channels=None):
+        super().__init__()
+        if not use_conv_transpose:
+            raise NotImplementedError("the reference decoder uses the ConvTranspose1d upsampler")
+        self.conv = nn.ConvTranspose1d(channels, out_channels or channels, 4, 2, 1)
+
+
+class TimestepEmbedding(_Params):
+    def __init__(self, in_channels, time_embed_dim, act_fn="silu", out_dim=None):
+        super().__init__()
+        self.linear_1 = nn.Linear(in_channels, time_embed_dim)
+        self.act = nn.SiLU() if act_fn == "silu" else nn.Mish()
+        self.linear_2 = nn.Linear(time_embed_dim, out_dim or time_embed_dim)
+
+
+class Decoder(nn.Module):
+    """U-Net velocity estimator (model.py:834-1048). ``forward`` = one HIP estimator evaluation."""
+
+    def __init__(self, in_channels, out_channels, channels=(256, 256), dropout=0.05, attention_head_dim=64,
+                 n_blocks=1, num_mid_blocks=2, num_heads=4, time_emb_dim=None, time_mlp_dim=None, ffn_mult=4,
+                 precision: str = "fp32", **kwargs):
+        super().__init__()
+        channels = tuple(channels)
+        if channels != (256, 256) or out_channels != 80:
+            raise NotImplementedError("the HIP estimator is built for channels=(256,256), n_feats=80 (main.py:68)")
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.n_blocks, self.num_mid_blocks, self.num_heads = n_blocks, num_mid_blocks, num_heads
+        self.time_embeddings = SinusoidalPosEmb(in_channels)
+        tdim = channels[0] * 4
+        self.time_mlp = TimestepEmbedding(in_channels, tdim, act_fn="silu")
+
+        def tblocks(dim):
+            return nn.ModuleList([BasicTransformerBlock(dim, num_heads, attention_head_dim, dropout, "snakebeta")
+                                  for _ in range(n_blocks)])
+
+        self.down_blocks = nn.ModuleList([
+            nn.ModuleList([ResnetBlock1D(in_channels, 256, tdim), tblocks(256), Downsample1D(256)]),
+            nn.ModuleList([ResnetBlock1D(256, 256, tdim), tblocks(256), nn.Conv1d(256, 256, 3, padding=1)]),
+        ])
+        self.mid_blocks = nn.ModuleList([nn.ModuleList([ResnetBlock1D(256, 256, tdim), tblocks(256)])
+                                         for _ in range(num_mid_blocks)])
+        self.up_blocks = nn.ModuleList([
+            nn.ModuleList([ResnetBlock1D(512, 256, tdim), tblocks(256), Upsample1D(256, use_conv_transpose=True)]),
+            nn.ModuleList([ResnetBlock1D(512, 256, tdim), tblocks(256), nn.Conv1d(256, 256, 3, padding=1)]),
+        ])
+        self.final_block = Block1D(256, 256)
+        self.final_proj = nn.Conv1d(256, out_channels, 1)
+        self.precision = precision
+        self._engines = {}
+
+    # ---- HIP plumbing ----
+    def set_precision(self, precision: str):
+        rt.dtype_code(precision)
+        self.precision = precision
+        return self
+
+    def engine(self) -> rt.DecoderEngine:
+        key = self.precision
+        if key not in self._engines:
+            self._engines[key] = rt.DecoderEngine(self.in_channels, self.num_mid_blocks, self.n_blocks,
+                                                  self.num_heads, self.precision)
+        return self._engines[key]
+
+    def packed(self, device):
+        sd = {k: v for k, v in self.state_dict(keep_vars=True).items()}
+        return self.engine().pack(sd, device)
+
+    def forward(self, x, mask, mu, t, spks=None, cond=None):
+        """model.py:964-1048 — x, mu [B,80,T], mask [B,1,T], t [B] (or scalar) -> [B,80,T]."""
+        rt.require_gpu(x, mask, mu, spks, what="Decoder.forward")
+        x, mu, mask, spks = rt.f32c(x), rt.f32c(mu), rt.f32c(mask), rt.f32c(spks)
+        t = torch.as_tensor(t, dtype=torch.float32).reshape(-1)
+        eng, packed = self.engine(), self.packed(x.device)
+        tv = t.detach().cpu()
+        if tv.numel() == 1 or bool((tv == tv[0]).all()):
+            return eng.step(packed, x, mu, mask, spks, float(tv[0]))
+        # per-utterance times: rows are independent (per-sample GroupNorm / attention / masks)
+        outs = [eng.step(packed, x[i:i + 1], mu[i:i + 1], mask[i:i + 1], None if spks is None else spks[i:i + 1],
+                         float(tv[i])) for i in range(x.shape[0])]
+        return torch.cat(outs, 0)
+
+
+# ======================================================================================
+# Conditional flow matching (model.py:1063-1162)
+# ======================================================================================
+
+class BASECFM(nn.Module):
+    def __init__(self, n_feats, cfm_params, n_spks=1, spk_emb_dim=64):
+        super().__init__()
+        self.n_feats, self.n_spks, self.spk_emb_dim = n_feats, n_spks, spk_emb_dim
+        self.solver = _get(cfm_params, "solver", "euler")
+        self.sigma_min = _get(cfm_params, "sigma_min", 1e-4)
+        self.estimator = None
+
+    @torch.inference_mode()
+    def forward(self, mu, mask, n_timesteps, temperature=1.0, spks=None, cond=None):
+        """z = randn_like(mu)*temperature, then the Euler/midpoint loop — one HIP call."""
+        rt.require_gpu(mu, mask, spks, what="CFM.forward")
+        mu, mask, spks = rt.f32c(mu), rt.f32c(mask), rt.f32c(spks)
+        z = torch.randn_like(mu)
+        est = self.estimator
+        return est.engine().solve(est.packed(mu.device), z, temperature, mu, mask, spks, int(n_timesteps),
+                                  self.solver, out=z)
+
+    def compute_loss(self, x1, mask, mu, spks=None, cond=None):
+        raise NotImplementedError("CFM training (model.py:1147-1162) is outside this round's hot path "
+                                  "(SURVEY.md §8f row 3)")
+
+
+class CFM(BASECFM):
+    def __init__(self, n_feats, cfm_params, n_spks=1, spk_emb_dim=64, estimator=None):
+        super().__init__(n_feats, cfm_params, n_spks=n_spks, spk_emb_dim=spk_emb_dim)
+        if estimator is None:
+            raise ValueError("estimator must be provided")
+        self.estimator = estimator
+
+
+# ======================================================================================
+# MatchaTTS (model.py:1173-1300)
+# ======================================================================================
+
+class MatchaTTS(nn.Module):
+    def __init__(self, n_vocab, n_spks, spk_emb_dim, encoder_params, decoder_params, cfm_params,
+                 duration_predictor_params, precision: str = "fp32"):
+        super().__init__()
+        self.n_vocab, self.n_spks, self.spk_emb_dim = n_vocab, n_spks, spk_emb_dim
+        if n_spks > 1:
+            self.spk_emb = nn.Embedding(n_spks, spk_emb_dim)
+        self.register_buffer("mel_mean", torch.tensor(0.0))
+        self.register_buffer("mel_std", torch.tensor(1.0))
+        self.encoder = TextEncoder(_get(encoder_params, "encoder_type"), encoder_params, duration_predictor_params,
+                                   n_vocab, n_spks, spk_emb_dim)
+        n_feats = _get(encoder_params, "n_feats")
+        dec_in = 2 * n_feats + (spk_emb_dim if n_spks > 1 else 0)
+        est = Decoder(in_channels=dec_in, out_channels=n_feats, channels=_get(decoder_params, "channels"),
+                      dropout=_get(decoder_params, "dropout"),
+                      attention_head_dim=_get(decoder_params, "attention_head_dim"),
+                      n_blocks=_get(decoder_params, "n_blocks"), num_mid_blocks=_get(decoder_params, "num_mid_blocks"),
+                      num_heads=_get(decoder_params, "num_heads"), act_fn=_get(decoder_params, "act_fn"),
+                      precision=precision)
+        self.decoder = CFM(n_feats=n_feats, cfm_params=cfm_params, n_spks=n_spks, spk_emb_dim=spk_emb_dim,
+                           estimator=est)
+
+    def set_precision(self, precision: str):
+        """'fp32' (parity mode, default) or 'bf16' (bf16 MFMA, fp32 accumulate)."""
+        self.decoder.estimator.set_precision(precision)
+        return self
+
+    def forward(self, x, x_lengths, y, y_lengths, spks=None):
+        raise NotImplementedError("the training forward (model.py:1234-1262) is outside this round's hot path")
+
+    @torch.inference_mode()
+    def synthesize(self, x, x_lengths, n_timesteps, temperature=1.0, spks=None, length_scale=1.0):
+        """model.py:1264-1300 -> (mel [B,80,y_max], y_lengths int64 [B], attn [B,1,Tx,T_pad])."""
+        rt.require_gpu(x, x_lengths, spks, what="MatchaTTS.synthesize")
+        mu, logw, x_mask = self.encoder(x, x_lengths, spks)
+        w_ceil, cum, y_lengths = rt.durations(logw, x_mask, length_scale)
+        y_max = int(y_lengths.max())                 # the reference's host sync (model.py:1278-1281)
+        t_pad = fix_len_compatibility(y_max)
+        attn, mu_y, y_mask = rt.alignment(cum, y_lengths, t_pad, mu)
+        z = self.decoder(mu_y, y_mask, n_timesteps, temperature, spks, cond=None)
+        mel = rt.denorm_crop(z, self.mel_mean, self.mel_std, y_max)
+        return mel, y_lengths, attn
+
+    @torch.inference_mode()
+    def synthesise(self, x, x_lengths, n_timesteps, temperature=1.0, spks=None, length_scale=1.0):
+        """Upstream-Matcha-style alias (notebooks: MOS_audiou_generator.ipynb:294) -> dict."""
+        import time
+        t0 = time.perf_counter()
+        mel, y_lengths, attn = self.synthesize(x, x_lengths, n_timesteps, temperature, spks, length_scale)
+        y_max = mel.shape[-1]
+        dt = time.perf_counter() - t0
+        return {"mel": mel, "mel_lengths": y_lengths, "attn": attn[:, :, :, :y_max],
+                "decoder_outputs": normalize(mel, self.mel_mean, self.mel_std),
+                "rtf": dt * 22050 / (y_max * 256)}
