@@ -30,11 +30,35 @@ __device__ __forceinline__ float mish_e(float x) {
   }
 }
 
+// Tile configuration (compile time): BM x BN output tile, WAVES_M x WAVES_N waves, TG taps
+// per K-stage, SMAX = largest stride served. Static LDS: two stage buffers + tables.
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int TG_, int SMAX_>
+struct Tile {
+  static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, TG = TG_, SMAX = SMAX_;
+  static constexpr int NT = 64 * WAVES_M * WAVES_N;
+  static constexpr int DMAX = 5;  // largest dilation served (HiFi-GAN v1: 1, 3, 5)
+  static constexpr int RBMAX = (BN - 1) * SMAX + (TG - 1) * DMAX + 1;
+  static constexpr int WS_BYTES = TG * BM * ROWB;
+  static constexpr int XS_BYTES = RBMAX * ROWB;
+  static constexpr int BUF_BYTES = WS_BYTES + XS_BYTES;
+  static constexpr int TAB_BYTES = (512 + 2 * BN) * 4;
+  static constexpr int LDS_BYTES = 2 * BUF_BYTES + TAB_BYTES;
+  static constexpr int NWV = (TG * BM * 4 + NT - 1) / NT;  // 16-B weight vectors per thread per stage
+  static constexpr int NXV = (RBMAX * 4 + NT - 1) / NT;    // 16-B input vectors per thread per stage
+};
+
 // TAG only renames the symbol: TAG=1 is the op-level entry (mt_op_conv1d) used by bench.py's
 // roofline leg, so its launches get their own rocprof row; the code is identical.
-template <class E, int BM, int BN, int WAVES_M, int PF, int EF, int TAG = 0>
-__global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int tg_max) {
-  constexpr int WAVES_N = 4 / WAVES_M;
+//
+// Pipeline per K-stage s (tap group x 64-byte channel chunk), one barrier per stage:
+//   issue(s+1): global loads of stage s+1 into registers (addresses clamped, no branches)
+//   MFMAs of stage s from LDS buffer s&1
+//   commit(s+1): prologue transform + zero padding, ds_write into buffer (s+1)&1
+//   __syncthreads()
+template <class E, class TL, int PF, int EF, int TAG = 0>
+__global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
+  constexpr int BM = TL::BM, BN = TL::BN, WAVES_M = TL::WAVES_M, WAVES_N = TL::WAVES_N;
+  constexpr int NT = TL::NT, NWAVES = WAVES_M * WAVES_N, TG = TL::TG;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int FM = WM / 16, FN = WN / 16;
   constexpr int CH = Chunk<E>::CH;
@@ -42,20 +66,17 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int tg_max) {
   static_assert(CH / VN == 4, "64-byte chunk = 4 x 16-byte vectors");
   constexpr bool NEED_GN = (PF & PF_GN) || (EF & EF_GNADD);
 
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ __attribute__((aligned(16))) char smem[TL::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WAVES_M, wn = wave / WAVES_M;
   const int ntiles = (a.Ncols + BN - 1) / BN;
   const int b = blockIdx.x / ntiles, nt = blockIdx.x - b * ntiles;
   const int n0 = nt * BN, m0 = blockIdx.y * BM;
 
-  const int RBmax = (BN - 1) * a.stride + (tg_max - 1) * a.dil + 1;
-  char* Ws = smem;
-  char* Xs = smem + tg_max * BM * ROWB;
-  float* ga = reinterpret_cast<float*>(Xs + RBmax * ROWB);  // [256]
-  float* gsh = ga + 256;                                     // [256]
-  float* lnm = gsh + 256;                                    // [BN]
-  float* lnr = lnm + BN;                                     // [BN]
+  float* ga = reinterpret_cast<float*>(smem + 2 * TL::BUF_BYTES);  // [256]
+  float* gsh = ga + 256;                                           // [256]
+  float* lnm = gsh + 256;                                          // [BN]
+  float* lnr = lnm + BN;                                           // [BN]
 
   // ---- pre-phase: GroupNorm coefficients for utterance b (merged tile partials) ----
   if constexpr (NEED_GN) {
@@ -76,7 +97,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int tg_max) {
       lnr[tid] = (float)(1.0 / sqrt(var + (double)a.gn_eps));
     }
     __syncthreads();
-    for (int c = tid; c < C; c += 256) {
+    for (int c = tid; c < C; c += NT) {
       const int g = c >> 5;
       const float sc = lnr[g] * a.gn_g[c];
       ga[c] = sc;
@@ -88,7 +109,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int tg_max) {
   // ---- pre-phase: LayerNorm row statistics (k=1 GEMMs only: rows n0..n0+BN-1) ----
   if constexpr (PF & PF_LN) {
     const E* x0 = reinterpret_cast<const E*>(a.x0);
-    for (int r = wave; r < BN; r += 4) {
+    for (int r = wave; r < BN; r += NWAVES) {
       const int f = n0 + r;
       float mean = 0.f, rstd = 0.f;
       if (f < a.Tin) {
@@ -131,75 +152,130 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int tg_max) {
   const E* wp = reinterpret_cast<const E*>(a.w);
   const int c1 = a.cin - a.c0;
   const int nchunks = a.cin_pad / CH;
+  const int ngroups = (a.taps + TG - 1) / TG;
+  const int S = ngroups * nchunks;
 
-  for (int tg0 = 0; tg0 < a.taps; tg0 += tg_max) {
-    const int ntg = min(tg_max, a.taps - tg0);
+  Vec16<E> xr[TL::NXV], wr[TL::NWV];
+
+  // global -> registers for stage s (every load issued, invalid ones from a clamped address)
+  auto issue = [&](int s) {
+    const int gi = s / nchunks, c = s - gi * nchunks;
+    const int tg0 = gi * TG, ntg = min(TG, a.taps - tg0);
     const int RB = (BN - 1) * a.stride + (ntg - 1) * a.dil + 1;
     const int fbase = n0 * a.stride - a.pad + tg0 * a.dil;
-    for (int c = 0; c < nchunks; ++c) {
-      const int cbase = c * CH;
-      // ---- stage input rows (+prologue) ----
-      for (int v = tid; v < RB * 4; v += 256) {
-        const int r = v >> 2, s = v & 3;
-        const int f = fbase + r;
-        const int ch = cbase + s * VN;
-        Vec16<E> val = zero16<E>();
-        if (f >= 0 && f < a.Tin && ch < a.cin) {
-          const size_t row = (size_t)b * a.Tin + f;
-          const E* src = (ch < a.c0) ? x0p + row * a.c0 + ch : x1p + row * c1 + (ch - a.c0);
-          val = load16(src);
-          if constexpr (PF != 0) {
-            float mk = 1.f, lm = 0.f, lr = 1.f;
-            if constexpr ((PF & PF_MASK) != 0) mk = a.pmask[row];
-            if constexpr ((PF & PF_LN) != 0) {
-              lm = lnm[f - n0];
-              lr = lnr[f - n0];
-            }
+    const int cbase = c * CH;
 #pragma unroll
-            for (int i = 0; i < VN; ++i) {
-              float x = val.get(i);
-              const int cc = ch + i;
-              if constexpr ((PF & PF_LN) != 0) x = (x - lm) * lr * a.ln_g[cc] + a.ln_b[cc];
-              if constexpr ((PF & PF_GN) != 0) x = mish_e<E>(x * ga[cc] + gsh[cc]);
-              if constexpr ((PF & PF_TB) != 0) x = x + a.tb[cc];
-              if constexpr ((PF & PF_LRELU) != 0) x = lrelu_f(x, a.slope);
-              if constexpr ((PF & PF_MASK) != 0) x = x * mk;
-              val.set(i, x);
-            }
-          }
-        }
-        store16(reinterpret_cast<E*>(Xs + r * ROWB + s * 16), val);
-      }
-      // ---- stage weight rows for the taps of this group ----
-      for (int v = tid; v < ntg * BM * 4; v += 256) {
-        const int rr = v >> 2, s = v & 3;
-        const int t = rr / BM, m = rr - t * BM;
-        Vec16<E> val = zero16<E>();
-        if (m0 + m < a.Mpad)
-          val = load16(wp + ((size_t)(m0 + m) * a.taps + (tg0 + t)) * a.cin_pad + cbase + s * VN);
-        store16(reinterpret_cast<E*>(Ws + rr * ROWB + s * 16), val);
-      }
-      __syncthreads();
-      // ---- MFMA over the taps of this group ----
-      for (int t = 0; t < ntg; ++t) {
-        Vec16<E> af[FM], bfg[FN];
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm)
-          af[fm] = load16(reinterpret_cast<const E*>(
-              Ws + (t * BM + wm * WM + fm * 16 + (lane & 15)) * ROWB + (lane >> 4) * 16));
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int col = wn * WN + fn * 16 + (lane & 15);
-          bfg[fn] = load16(reinterpret_cast<const E*>(
-              Xs + (col * a.stride + t * a.dil) * ROWB + (lane >> 4) * 16));
-        }
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-          for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(af[fm].v, bfg[fn].v, acc[fm][fn]);
-      }
-      __syncthreads();
+    for (int i = 0; i < TL::NXV; ++i) {
+      const int v = tid + i * NT;
+      const int r = v >> 2, sl = v & 3;
+      int f = fbase + r;
+      int ch = cbase + sl * VN;
+      const bool ok = (v < RB * 4) && f >= 0 && f < a.Tin && ch < a.cin;
+      f = ok ? f : 0;
+      ch = ok ? ch : 0;
+      const size_t row = (size_t)b * a.Tin + f;
+      const E* src = (ch < a.c0) ? x0p + row * a.c0 + ch : x1p + row * c1 + (ch - a.c0);
+      xr[i] = load16(src);
     }
+#pragma unroll
+    for (int i = 0; i < TL::NWV; ++i) {
+      const int v = tid + i * NT;
+      const int rr = v >> 2, sl = v & 3;
+      const int t = rr / BM, m = rr - t * BM;
+      const bool ok = (t < ntg) && (m0 + m < a.Mpad);
+      const size_t off = ok ? ((size_t)(m0 + m) * a.taps + (tg0 + t)) * a.cin_pad + cbase + sl * VN : 0;
+      wr[i] = load16(wp + off);
+    }
+  };
+
+  // registers -> LDS buffer `buf` for stage s (prologue transform, zero padding)
+  auto commit = [&](int s, int buf) {
+    char* Ws = smem + buf * TL::BUF_BYTES;
+    char* Xs = Ws + TL::WS_BYTES;
+    const int gi = s / nchunks, c = s - gi * nchunks;
+    const int tg0 = gi * TG, ntg = min(TG, a.taps - tg0);
+    const int RB = (BN - 1) * a.stride + (ntg - 1) * a.dil + 1;
+    const int fbase = n0 * a.stride - a.pad + tg0 * a.dil;
+    const int cbase = c * CH;
+#pragma unroll
+    for (int i = 0; i < TL::NXV; ++i) {
+      const int v = tid + i * NT;
+      if (v >= RB * 4) continue;
+      const int r = v >> 2, sl = v & 3;
+      const int f = fbase + r;
+      const int ch = cbase + sl * VN;
+      Vec16<E> val = xr[i];
+      if (f < 0 || f >= a.Tin || ch >= a.cin) {
+        val = zero16<E>();
+      } else if constexpr (PF != 0) {
+        const size_t row = (size_t)b * a.Tin + f;
+        float mk = 1.f, lm = 0.f, lr = 1.f;
+        if constexpr ((PF & PF_MASK) != 0) mk = a.pmask[row];
+        if constexpr ((PF & PF_LN) != 0) {
+          lm = lnm[f - n0];
+          lr = lnr[f - n0];
+        }
+#pragma unroll
+        for (int k = 0; k < VN; ++k) {
+          float x = val.get(k);
+          const int cc = ch + k;
+          if constexpr ((PF & PF_LN) != 0) x = (x - lm) * lr * a.ln_g[cc] + a.ln_b[cc];
+          if constexpr ((PF & PF_GN) != 0) x = mish_e<E>(x * ga[cc] + gsh[cc]);
+          if constexpr ((PF & PF_TB) != 0) x = x + a.tb[cc];
+          if constexpr ((PF & PF_LRELU) != 0) x = lrelu_f(x, a.slope);
+          if constexpr ((PF & PF_MASK) != 0) x = x * mk;
+          val.set(k, x);
+        }
+      }
+      store16(reinterpret_cast<E*>(Xs + r * ROWB + sl * 16), val);
+    }
+#pragma unroll
+    for (int i = 0; i < TL::NWV; ++i) {
+      const int v = tid + i * NT;
+      const int rr = v >> 2, sl = v & 3;
+      const int t = rr / BM, m = rr - t * BM;
+      if (t >= TG) continue;
+      Vec16<E> val = wr[i];
+      if (t >= ntg || m0 + m >= a.Mpad) val = zero16<E>();
+      store16(reinterpret_cast<E*>(Ws + rr * ROWB + sl * 16), val);
+    }
+  };
+
+  auto compute = [&](int s, int buf) {
+    const char* Ws = smem + buf * TL::BUF_BYTES;
+    const char* Xs = Ws + TL::WS_BYTES;
+    const int gi = s / nchunks;
+    const int ntg = min(TG, a.taps - gi * TG);
+#pragma unroll
+    for (int t = 0; t < TG; ++t) {
+      if (t >= ntg) break;
+      Vec16<E> af[FM], bfg[FN];
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+        af[fm] = load16(reinterpret_cast<const E*>(
+            Ws + (t * BM + wm * WM + fm * 16 + (lane & 15)) * ROWB + (lane >> 4) * 16));
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int col = wn * WN + fn * 16 + (lane & 15);
+        bfg[fn] = load16(reinterpret_cast<const E*>(
+            Xs + (col * a.stride + t * a.dil) * ROWB + (lane >> 4) * 16));
+      }
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(af[fm].v, bfg[fn].v, acc[fm][fn]);
+    }
+  };
+
+  issue(0);
+  commit(0, 0);
+  __syncthreads();
+  for (int s = 0; s < S; ++s) {
+    const bool more = s + 1 < S;
+    if (more) issue(s + 1);
+    compute(s, s & 1);
+    if (more) commit(s + 1, (s + 1) & 1);
+    __syncthreads();
   }
 
   // ---- epilogue ----
@@ -327,7 +403,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int tg_max) {
   if constexpr ((EF & EF_GNSTATS) != 0) {
     static_assert(WM >= 32, "GN stats need >= 32 rows per wave");
     __syncthreads();
-    double* red = reinterpret_cast<double*>(smem);  // [4][FM][2]
+    double* red = reinterpret_cast<double*>(smem);  // [NWAVES][FM][2]
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
       const double s1 = wave_sum_d(g1[fm]);
@@ -364,20 +440,24 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvArgs a, int tg_max) {
 // ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
-enum : int { CFG_128x128 = 1, CFG_128x64 = 2, CFG_64x128 = 4, CFG_32x256 = 8, CFG_16x256 = 16 };
+enum : int { CFG_128x256 = 1, CFG_128x128 = 2, CFG_64x256 = 4, CFG_32x256 = 8, CFG_16x256 = 16 };
 
-template <class E, int BM, int BN, int WAVES_M, int PF, int EF, int TAG = 0>
+// every tile is 8 waves (512 threads): 2 waves per SIMD at one workgroup per CU
+using T128x256 = Tile<128, 256, 2, 4, 2, 1>;  // big layers, wave tile 64x64
+using T128x128 = Tile<128, 128, 2, 4, 2, 2>;  // small N or stride 2, wave tile 64x32
+using T64x256 = Tile<64, 256, 1, 8, 4, 1>;    // wave tile 64x32
+using T32x256 = Tile<32, 256, 1, 8, 4, 1>;    // wave tile 32x32
+using T16x256 = Tile<16, 256, 1, 8, 4, 1>;    // wave tile 16x32
+
+template <class E, class TL, int PF, int EF, int TAG = 0>
 static int launch_tile(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
-  const int tgmax = BM >= 256 ? 2 : 4;
-  const int tg = std::min(a.taps, tgmax);
-  const int RBmax = (BN - 1) * a.stride + (tg - 1) * a.dil + 1;
-  size_t lds = (size_t)tg * BM * ROWB + (size_t)RBmax * ROWB + (512 + 2 * BN) * sizeof(float);
-  lds = std::max(lds, (size_t)4 * 8 * 2 * sizeof(double));
-  MT_REQUIRE(lds <= 65536, "conv: LDS request %zu too large (taps %d dil %d stride %d)", lds, a.taps,
-             a.dil, a.stride);
-  const int ntiles = (a.Ncols + BN - 1) / BN;
-  dim3 grid((unsigned)(ntiles * a.B), (unsigned)((a.M + BM - 1) / BM));
-  hipLaunchKernelGGL((conv_kernel<E, BM, BN, WAVES_M, PF, EF, TAG>), grid, dim3(256), lds, stream, a, tg);
+  const int ntg = std::min(a.taps, TL::TG);
+  const int RB = (TL::BN - 1) * a.stride + (ntg - 1) * a.dil + 1;
+  MT_REQUIRE(a.stride <= TL::SMAX && RB <= TL::RBMAX,
+             "conv: stride %d / dilation %d exceed the tile's static bounds", a.stride, a.dil);
+  const int ntiles = (a.Ncols + TL::BN - 1) / TL::BN;
+  dim3 grid((unsigned)(ntiles * a.B), (unsigned)((a.M + TL::BM - 1) / TL::BM));
+  hipLaunchKernelGGL((conv_kernel<E, TL, PF, EF, TAG>), grid, dim3(TL::NT), 0, stream, a);
   MT_CHECK_HIP(hipGetLastError());
   if (ntiles_out) *ntiles_out = ntiles;
   return 0;
@@ -416,40 +496,36 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
     return (long)a.B * ((a.Ncols + bn - 1) / bn) * ((M + bm - 1) / bm);
   };
   if constexpr ((CFGS & CFG_16x256) != 0)
-    if (M <= 16) return launch_tile<E, 16, 256, 1, PF, EF, TAG>(a, stream, ntiles_out);
+    if (M <= 16) return launch_tile<E, T16x256, PF, EF, TAG>(a, stream, ntiles_out);
   if constexpr ((CFGS & CFG_32x256) != 0)
-    if (M <= 32) return launch_tile<E, 32, 256, 1, PF, EF, TAG>(a, stream, ntiles_out);
-  if constexpr ((CFGS & CFG_64x128) != 0)
-    if (M <= 64) return launch_tile<E, 64, 128, 1, PF, EF, TAG>(a, stream, ntiles_out);
-  if constexpr ((CFGS & CFG_128x128) != 0 && (CFGS & CFG_128x64) != 0) {
-    if (wgs(128, 128) >= 1024) return launch_tile<E, 128, 128, 2, PF, EF, TAG>(a, stream, ntiles_out);
-    return launch_tile<E, 128, 64, 2, PF, EF, TAG>(a, stream, ntiles_out);
-  } else if constexpr ((CFGS & CFG_128x128) != 0) {
-    return launch_tile<E, 128, 128, 2, PF, EF, TAG>(a, stream, ntiles_out);
-  } else if constexpr ((CFGS & CFG_128x64) != 0) {
-    return launch_tile<E, 128, 64, 2, PF, EF, TAG>(a, stream, ntiles_out);
-  }
+    if (M <= 32) return launch_tile<E, T32x256, PF, EF, TAG>(a, stream, ntiles_out);
+  if constexpr ((CFGS & CFG_64x256) != 0)
+    if (M <= 64) return launch_tile<E, T64x256, PF, EF, TAG>(a, stream, ntiles_out);
+  if constexpr ((CFGS & CFG_128x256) != 0)
+    if (a.stride == 1 && (wgs(128, 256) >= 512 || (CFGS & CFG_128x128) == 0))
+      return launch_tile<E, T128x256, PF, EF, TAG>(a, stream, ntiles_out);
+  if constexpr ((CFGS & CFG_128x128) != 0) return launch_tile<E, T128x128, PF, EF, TAG>(a, stream, ntiles_out);
   set_error("conv: no tile configuration for M=%d (pf %d ef %d)", M, PF, EF);
   return -1;
 }
 
 // (PF, EF, tile configs) combinations used by the decoder and the vocoder.
 #define MT_CONV_COMBOS(X)                                                              \
-  X(PF_MASK, EF_GNSTATS, CFG_128x128 | CFG_128x64)                                     \
-  X(PF_GN | PF_TB | PF_MASK, EF_GNSTATS, CFG_128x128 | CFG_128x64)                     \
-  X(PF_MASK, EF_GNADD, CFG_128x128 | CFG_128x64)                                       \
-  X(PF_LN, 0, CFG_128x128 | CFG_128x64)                                                \
-  X(0, EF_RESID, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256)                   \
-  X(PF_LN, EF_SNAKE, CFG_128x128 | CFG_128x64)                                         \
-  X(PF_MASK, 0, CFG_128x128 | CFG_128x64)                                              \
-  X(PF_GN | PF_MASK, EF_MASK | EF_EULER, CFG_128x128 | CFG_128x64)                     \
-  X(0, 0, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256 | CFG_16x256)             \
-  X(PF_LRELU, 0, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256 | CFG_16x256)      \
-  X(PF_LRELU, EF_RESID, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256)            \
-  X(PF_LRELU, EF_RESID | EF_ACCUM, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256) \
+  X(PF_MASK, EF_GNSTATS, CFG_128x256 | CFG_128x128)                                     \
+  X(PF_GN | PF_TB | PF_MASK, EF_GNSTATS, CFG_128x256 | CFG_128x128)                     \
+  X(PF_MASK, EF_GNADD, CFG_128x256 | CFG_128x128)                                       \
+  X(PF_LN, 0, CFG_128x256 | CFG_128x128)                                                \
+  X(0, EF_RESID, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256)                   \
+  X(PF_LN, EF_SNAKE, CFG_128x256 | CFG_128x128)                                         \
+  X(PF_MASK, 0, CFG_128x256 | CFG_128x128)                                              \
+  X(PF_GN | PF_MASK, EF_MASK | EF_EULER, CFG_128x256 | CFG_128x128)                     \
+  X(0, 0, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256 | CFG_16x256)             \
+  X(PF_LRELU, 0, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256 | CFG_16x256)      \
+  X(PF_LRELU, EF_RESID, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256)            \
+  X(PF_LRELU, EF_RESID | EF_ACCUM, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256) \
   X(PF_LRELU, EF_RESID | EF_ACCUM | EF_DIV,                                            \
-    CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256)                                \
-  X(PF_LRELU, EF_RESID | EF_DIV, CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256)   \
+    CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256)                                \
+  X(PF_LRELU, EF_RESID | EF_DIV, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256)   \
   X(PF_LRELU, EF_TANH | EF_OUTF32, CFG_16x256 | CFG_32x256)
 
 #define MT_DEFINE_LAUNCH(PFV, EFV, CFGV)                                                    \
@@ -464,7 +540,7 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
 MT_CONV_COMBOS(MT_DEFINE_LAUNCH)
 
 int launch_conv_op(int dtype, int pf, const ConvArgs& a, hipStream_t stream) {
-  constexpr int ALL = CFG_128x128 | CFG_128x64 | CFG_64x128 | CFG_32x256 | CFG_16x256;
+  constexpr int ALL = CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256 | CFG_16x256;
   if (pf == PF_LRELU)
     return dtype == BF16 ? launch_sel<bf16, PF_LRELU, 0, ALL, 1>(a, stream, nullptr)
                          : launch_sel<float, PF_LRELU, 0, ALL, 1>(a, stream, nullptr);
