@@ -131,6 +131,10 @@ size_t mt_op_conv1d_workspace_bytes(int dtype, int cin, int cout, int k, int str
 int mt_op_conv1d(int dtype, const void* x, int B, int Tin, int cin, const float* W, const float* bias,
                  int cout, int k, int stride, int pad, int dil, int transposed, float slope, void* y,
                  int Tout, void* ws, size_t ws_bytes, void* stream);
+/* same with a fixed tile variant (in-process A/B timing; lrelu prologue only; -1 = automatic) */
+int mt_op_conv1d_tile(int variant, int dtype, const void* x, int B, int Tin, int cin, const float* W,
+                      const float* bias, int cout, int k, int stride, int pad, int dil, int transposed,
+                      float slope, void* y, int Tout, void* ws, size_t ws_bytes, void* stream);
 /* qkv [B][T][3*heads*64], mask [B][T] -> out [B][T][heads*64], reference mask semantics */
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                     void* stream);

@@ -178,7 +178,7 @@ size_t mt_op_conv1d_workspace_bytes(int dtype, int cin, int cout, int k, int str
     mt::make_conv(cout, cin, k, stride, 0, 1, {0}, 1, es, pk);
   return pk.off;
 }
-int mt_op_conv1d(int dtype, const void* x, int B, int Tin, int cin, const float* W, const float* bias,
+int mt_op_conv1d_tile(int variant, int dtype, const void* x, int B, int Tin, int cin, const float* W, const float* bias,
                  int cout, int k, int stride, int pad, int dil, int transposed, float slope, void* y, int Tout,
                  void* ws, size_t ws_bytes, void* stream) {
   MT_REQUIRE(x && W && y && ws, "op_conv1d: null argument");
@@ -196,7 +196,13 @@ int mt_op_conv1d(int dtype, const void* x, int B, int Tin, int cin, const float*
   a.x0 = x;
   a.y = y;
   a.slope = slope;
-  return mt::launch_conv_op(dtype, slope >= 0.f ? mt::PF_LRELU : 0, a, st);
+  return mt::launch_conv_op(dtype, slope >= 0.f ? mt::PF_LRELU : 0, a, st, variant);
+}
+int mt_op_conv1d(int dtype, const void* x, int B, int Tin, int cin, const float* W, const float* bias,
+                 int cout, int k, int stride, int pad, int dil, int transposed, float slope, void* y, int Tout,
+                 void* ws, size_t ws_bytes, void* stream) {
+  return mt_op_conv1d_tile(-1, dtype, x, B, Tin, cin, W, bias, cout, k, stride, pad, dil, transposed, slope, y,
+                           Tout, ws, ws_bytes, stream);
 }
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                     void* stream) {

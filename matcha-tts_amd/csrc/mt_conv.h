@@ -14,7 +14,7 @@ namespace mt {
 
 // prologue flags (applied to every staged input element, in this order)
 enum : int {
-  PF_LN = 1,      // (x - mean[f]) * rstd[f] * ln_g[c] + ln_b[c]   (stats computed in-kernel)
+  PF_LN = 1,      // (x - mean[f]) * rstd[f]  (stats from rowstats(); gamma/beta folded into W)
   PF_GN = 2,      // mish(x * ga[b,c] + gs[b,c])                     (GroupNorm8 + Mish)
   PF_TB = 4,      // + tb[c]                                          (time-embedding bias)
   PF_LRELU = 8,   // leaky_relu(x, slope)
@@ -50,9 +50,10 @@ struct ConvArgs {
   // prologue params
   const float* pmask;   // [B][Tin]
   float slope;
-  const float* ln_g;
+  const float* ln_g;       // unused: LayerNorm gamma/beta are folded into the packed weights
   const float* ln_b;
   float ln_eps;
+  const float* ln_stats;   // [B*Tin][2] per-frame (mean, rstd) from rowstats()
   const double* gn_in;  // [B][G][gn_ntiles][2] partial (sum, sumsq) of the GN'd tensor
   int gn_ntiles, gn_T;  // partial count per (b, group); frames of the GN'd tensor
   const float* gn_g;
@@ -87,6 +88,6 @@ int launch_conv(const ConvArgs& a, hipStream_t stream, int* ntiles_out = nullptr
 int launch_conv_dyn(int dtype, int pf, int ef, const ConvArgs& a, hipStream_t stream,
                     int* ntiles_out = nullptr);
 // op-level entry (mt_op_conv1d): same kernels, separate symbols (TAG=1) for profiling
-int launch_conv_op(int dtype, int pf, const ConvArgs& a, hipStream_t stream);
+int launch_conv_op(int dtype, int pf, const ConvArgs& a, hipStream_t stream, int variant = -1);
 
 }  // namespace mt

@@ -16,8 +16,6 @@
 
 namespace mt {
 
-static constexpr int ROWB = 80;
-
 template <class E>
 __device__ __forceinline__ float mish_e(float x) {
   if constexpr (std::is_same<E, float>::value) {
@@ -30,21 +28,24 @@ __device__ __forceinline__ float mish_e(float x) {
   }
 }
 
-// Tile configuration (compile time): BM x BN output tile, WAVES_M x WAVES_N waves, TG taps
-// per K-stage, SMAX = largest stride served. Static LDS: two stage buffers + tables.
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int TG_, int SMAX_>
+// Tile configuration (compile time): BM x BN output tile, WAVES_M x WAVES_N waves, TG taps and
+// CK bytes of input channels per K-stage (LDS rows of CK+16 bytes: conflict-free ds_read_b128
+// for CK in {64,128,256}), SMAX = largest stride served. Static LDS: two stage buffers + tables.
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int TG_, int CK_, int SMAX_>
 struct Tile {
   static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, TG = TG_, SMAX = SMAX_;
+  static constexpr int CK = CK_, ROW = CK_ + 16, VPR = CK_ / 16, KS = CK_ / 64;
   static constexpr int NT = 64 * WAVES_M * WAVES_N;
   static constexpr int DMAX = 5;  // largest dilation served (HiFi-GAN v1: 1, 3, 5)
   static constexpr int RBMAX = (BN - 1) * SMAX + (TG - 1) * DMAX + 1;
-  static constexpr int WS_BYTES = TG * BM * ROWB;
-  static constexpr int XS_BYTES = RBMAX * ROWB;
+  static constexpr int WS_BYTES = TG * BM * ROW;
+  static constexpr int XS_BYTES = RBMAX * ROW;
   static constexpr int BUF_BYTES = WS_BYTES + XS_BYTES;
-  static constexpr int TAB_BYTES = (512 + 2 * BN) * 4;
+  static constexpr int TAB_BYTES = (768 + 2 * BN) * 4;
   static constexpr int LDS_BYTES = 2 * BUF_BYTES + TAB_BYTES;
-  static constexpr int NWV = (TG * BM * 4 + NT - 1) / NT;  // 16-B weight vectors per thread per stage
-  static constexpr int NXV = (RBMAX * 4 + NT - 1) / NT;    // 16-B input vectors per thread per stage
+  static constexpr int NWV = (TG * BM * VPR + NT - 1) / NT;  // 16-B weight vectors per thread per stage
+  static constexpr int NXV = (RBMAX * VPR + NT - 1) / NT;    // 16-B input vectors per thread per stage
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
 // TAG only renames the symbol: TAG=1 is the op-level entry (mt_op_conv1d) used by bench.py's
@@ -61,9 +62,10 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
   constexpr int NT = TL::NT, NWAVES = WAVES_M * WAVES_N, TG = TL::TG;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int FM = WM / 16, FN = WN / 16;
-  constexpr int CH = Chunk<E>::CH;
-  constexpr int VN = Vec16<E>::N;
-  static_assert(CH / VN == 4, "64-byte chunk = 4 x 16-byte vectors");
+  constexpr int VN = Vec16<E>::N;                 // elements per 16 bytes
+  constexpr int VPR = TL::VPR;                       // 16-B vectors per LDS row
+  constexpr int CH = VPR * VN;                       // channels per K-stage
+  constexpr int ROWB = TL::ROW;
   constexpr bool NEED_GN = (PF & PF_GN) || (EF & EF_GNADD);
 
   __shared__ __attribute__((aligned(16))) char smem[TL::LDS_BYTES];
@@ -77,6 +79,12 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
   float* gsh = ga + 256;                                           // [256]
   float* lnm = gsh + 256;                                          // [BN]
   float* lnr = lnm + BN;                                           // [BN]
+  float* tbs = lnr + BN;                                           // [256] time-embedding bias
+
+  if constexpr ((PF & PF_TB) != 0) {
+    for (int c = tid; c < a.cin; c += NT) tbs[c] = a.tb[c];
+    __syncthreads();
+  }
 
   // ---- pre-phase: GroupNorm coefficients for utterance b (merged tile partials) ----
   if constexpr (NEED_GN) {
@@ -106,37 +114,18 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // ---- pre-phase: LayerNorm row statistics (k=1 GEMMs only: rows n0..n0+BN-1) ----
+  // ---- pre-phase: LayerNorm row statistics of the tile's frames (k=1 GEMMs only) ----
   if constexpr (PF & PF_LN) {
-    const E* x0 = reinterpret_cast<const E*>(a.x0);
-    for (int r = wave; r < BN; r += NWAVES) {
+    for (int r = tid; r < BN; r += NT) {
       const int f = n0 + r;
       float mean = 0.f, rstd = 0.f;
       if (f < a.Tin) {
-        const E* row = x0 + (size_t)(b * a.Tin + f) * a.cin;
-        float xv[8];
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int c = lane + i * 64;
-          xv[i] = (c < a.cin) ? to_f(row[c]) : 0.f;
-          s += xv[i];
-        }
-        mean = wave_sum(s) / (float)a.cin;
-        float q = 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int c = lane + i * 64;
-          const float d = xv[i] - mean;
-          q += (c < a.cin) ? d * d : 0.f;
-        }
-        const float var = wave_sum(q) / (float)a.cin;
-        rstd = 1.f / sqrtf(var + a.ln_eps);
+        const float* st = a.ln_stats + ((size_t)b * a.Tin + f) * 2;
+        mean = st[0];
+        rstd = st[1];
       }
-      if (lane == 0) {
-        lnm[r] = mean;
-        lnr[r] = rstd;
-      }
+      lnm[r] = mean;
+      lnr[r] = rstd;
     }
     __syncthreads();
   }
@@ -151,7 +140,7 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
   const E* x1p = reinterpret_cast<const E*>(a.x1);
   const E* wp = reinterpret_cast<const E*>(a.w);
   const int c1 = a.cin - a.c0;
-  const int nchunks = a.cin_pad / CH;
+  const int nchunks = (a.cin_pad + CH - 1) / CH;
   const int ngroups = (a.taps + TG - 1) / TG;
   const int S = ngroups * nchunks;
 
@@ -167,10 +156,10 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < TL::NXV; ++i) {
       const int v = tid + i * NT;
-      const int r = v >> 2, sl = v & 3;
+      const int r = v / VPR, sl = v % VPR;
       int f = fbase + r;
       int ch = cbase + sl * VN;
-      const bool ok = (v < RB * 4) && f >= 0 && f < a.Tin && ch < a.cin;
+      const bool ok = (v < RB * VPR) && f >= 0 && f < a.Tin && ch < a.cin;
       f = ok ? f : 0;
       ch = ok ? ch : 0;
       const size_t row = (size_t)b * a.Tin + f;
@@ -180,9 +169,9 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < TL::NWV; ++i) {
       const int v = tid + i * NT;
-      const int rr = v >> 2, sl = v & 3;
+      const int rr = v / VPR, sl = v % VPR;
       const int t = rr / BM, m = rr - t * BM;
-      const bool ok = (t < ntg) && (m0 + m < a.Mpad);
+      const bool ok = (t < ntg) && (m0 + m < a.Mpad) && (cbase + sl * VN < a.cin_pad);
       const size_t off = ok ? ((size_t)(m0 + m) * a.taps + (tg0 + t)) * a.cin_pad + cbase + sl * VN : 0;
       wr[i] = load16(wp + off);
     }
@@ -200,8 +189,8 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < TL::NXV; ++i) {
       const int v = tid + i * NT;
-      if (v >= RB * 4) continue;
-      const int r = v >> 2, sl = v & 3;
+      if (v >= RB * VPR) continue;
+      const int r = v / VPR, sl = v % VPR;
       const int f = fbase + r;
       const int ch = cbase + sl * VN;
       Vec16<E> val = xr[i];
@@ -219,9 +208,9 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
         for (int k = 0; k < VN; ++k) {
           float x = val.get(k);
           const int cc = ch + k;
-          if constexpr ((PF & PF_LN) != 0) x = (x - lm) * lr * a.ln_g[cc] + a.ln_b[cc];
+          if constexpr ((PF & PF_LN) != 0) x = (x - lm) * lr;  // gamma/beta folded into W, bias
           if constexpr ((PF & PF_GN) != 0) x = mish_e<E>(x * ga[cc] + gsh[cc]);
-          if constexpr ((PF & PF_TB) != 0) x = x + a.tb[cc];
+          if constexpr ((PF & PF_TB) != 0) x = x + tbs[cc];
           if constexpr ((PF & PF_LRELU) != 0) x = lrelu_f(x, a.slope);
           if constexpr ((PF & PF_MASK) != 0) x = x * mk;
           val.set(k, x);
@@ -232,38 +221,51 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < TL::NWV; ++i) {
       const int v = tid + i * NT;
-      const int rr = v >> 2, sl = v & 3;
+      const int rr = v / VPR, sl = v % VPR;
       const int t = rr / BM, m = rr - t * BM;
       if (t >= TG) continue;
       Vec16<E> val = wr[i];
-      if (t >= ntg || m0 + m >= a.Mpad) val = zero16<E>();
+      if (t >= ntg || m0 + m >= a.Mpad || cbase + sl * VN >= a.cin_pad) val = zero16<E>();
       store16(reinterpret_cast<E*>(Ws + rr * ROWB + sl * 16), val);
     }
   };
 
+  // MFMAs of one K-stage; the A/B fragments of step j+1 are read from LDS before the MFMAs of
+  // step j are issued (steps = taps x 64-byte K slices), so LDS latency hides under the MFMAs.
   auto compute = [&](int s, int buf) {
     const char* Ws = smem + buf * TL::BUF_BYTES;
     const char* Xs = Ws + TL::WS_BYTES;
     const int gi = s / nchunks;
     const int ntg = min(TG, a.taps - gi * TG);
+    const int nsteps = ntg * TL::KS;
+    const char* abase = Ws + (wm * WM + (lane & 15)) * ROWB + (lane >> 4) * 16;
+    const char* bbase = Xs + ((wn * WN + (lane & 15)) * a.stride) * ROWB + (lane >> 4) * 16;
+    auto load_frags = [&](int j, Vec16<E>(&af)[FM], Vec16<E>(&bf)[FN]) {
+      const int t = j / TL::KS, ks = j - t * TL::KS;
+      const char* ap = abase + t * BM * ROWB + ks * 64;
+      const char* bp = bbase + (t * a.dil) * ROWB + ks * 64;
 #pragma unroll
-    for (int t = 0; t < TG; ++t) {
-      if (t >= ntg) break;
-      Vec16<E> af[FM], bfg[FN];
+      for (int fm = 0; fm < FM; ++fm) af[fm] = load16(reinterpret_cast<const E*>(ap + fm * 16 * ROWB));
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn)
+        bf[fn] = load16(reinterpret_cast<const E*>(bp + fn * 16 * a.stride * ROWB));
+    };
+    auto mma = [&](const Vec16<E>(&af)[FM], const Vec16<E>(&bf)[FN]) {
 #pragma unroll
       for (int fm = 0; fm < FM; ++fm)
-        af[fm] = load16(reinterpret_cast<const E*>(
-            Ws + (t * BM + wm * WM + fm * 16 + (lane & 15)) * ROWB + (lane >> 4) * 16));
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        const int col = wn * WN + fn * 16 + (lane & 15);
-        bfg[fn] = load16(reinterpret_cast<const E*>(
-            Xs + (col * a.stride + t * a.dil) * ROWB + (lane >> 4) * 16));
-      }
+        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(af[fm].v, bf[fn].v, acc[fm][fn]);
+    };
+    Vec16<E> a0[FM], b0[FN], a1[FM], b1[FN];
+    load_frags(0, a0, b0);
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(af[fm].v, bfg[fn].v, acc[fm][fn]);
+    for (int j = 0; j < TG * TL::KS; j += 2) {
+      if (j >= nsteps) break;
+      if (j + 1 < nsteps) load_frags(j + 1, a1, b1);
+      mma(a0, b0);
+      if (j + 1 >= nsteps) break;
+      if (j + 2 < nsteps) load_frags(j + 2, a0, b0);
+      mma(a1, b1);
     }
   };
 
@@ -285,31 +287,40 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
 
 #pragma unroll
   for (int fm = 0; fm < FM; ++fm) {
+    const int mr = m0 + wm * WM + fm * 16 + 4 * (lane >> 4);
+    if (mr >= a.M) continue;
+    const int ph = mr / a.cout;
+    const int ch = mr - ph * a.cout;
+    bool ok[4];
+    float bias4[4], alpha4[4], ibeta4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ok[r] = (mr + r) < a.M;
+      bias4[r] = ok[r] ? a.bias[mr + r] : 0.f;
+      if constexpr ((EF & EF_SNAKE) != 0) {
+        alpha4[r] = ok[r] ? a.snake_alpha[ch + r] : 0.f;
+        ibeta4[r] = ok[r] ? a.snake_ibeta[ch + r] : 0.f;
+      }
+    }
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
-      const int mr = m0 + wm * WM + fm * 16 + 4 * (lane >> 4);
       const int n = n0 + wn * WN + fn * 16 + (lane & 15);
-      if (n >= a.Ncols || mr >= a.M) continue;
-      const int ph = mr / a.cout;
-      const int ch = mr - ph * a.cout;
+      if (n >= a.Ncols) continue;
       const int fr = n * a.ups + ph - a.opad;
       if (fr < 0 || fr >= a.Tout) continue;
       const size_t orow = (size_t)b * a.Tout + fr;
       float em = 1.f;
       if constexpr ((EF & (EF_MASK | EF_GNADD)) != 0) em = a.emask[orow];
-      bool ok[4];
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        ok[r] = (mr + r) < a.M;
-        v[r] = acc[fm][fn][r] + (ok[r] ? a.bias[mr + r] : 0.f);
-      }
+      for (int r = 0; r < 4; ++r) v[r] = acc[fm][fn][r] + bias4[r];
       if constexpr ((EF & EF_SNAKE) != 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          if (!ok[r]) continue;
-          const float sn = sinf(v[r] * a.snake_alpha[ch + r]);
-          v[r] = v[r] + a.snake_ibeta[ch + r] * (sn * sn);
+          float sn;
+          if constexpr (std::is_same<E, float>::value) sn = sinf(v[r] * alpha4[r]);
+          else sn = __sinf(v[r] * alpha4[r]);
+          v[r] = v[r] + ibeta4[r] * (sn * sn);
         }
       }
       if constexpr ((EF & EF_GNSTATS) != 0) {
@@ -440,14 +451,24 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
 // ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
-enum : int { CFG_128x256 = 1, CFG_128x128 = 2, CFG_64x256 = 4, CFG_32x256 = 8, CFG_16x256 = 16 };
+enum : int { CFG_BIG = 1, CFG_SMALLN = 2, CFG_64 = 4, CFG_32 = 8, CFG_16 = 16 };
 
 // every tile is 8 waves (512 threads): 2 waves per SIMD at one workgroup per CU
-using T128x256 = Tile<128, 256, 2, 4, 2, 1>;  // big layers, wave tile 64x64
-using T128x128 = Tile<128, 128, 2, 4, 2, 2>;  // small N or stride 2, wave tile 64x32
-using T64x256 = Tile<64, 256, 1, 8, 4, 1>;    // wave tile 64x32
-using T32x256 = Tile<32, 256, 1, 8, 4, 1>;    // wave tile 32x32
-using T16x256 = Tile<16, 256, 1, 8, 4, 1>;    // wave tile 16x32
+using TConv = Tile<128, 256, 2, 4, 4, 64, 1>;    // k >= 3 convs: 4 taps x 32 bf16 channels per stage
+using TConvT = Tile<128, 256, 2, 4, 2, 64, 1>;   // 2-tap polyphase ConvTranspose
+using TGemm = Tile<128, 256, 2, 4, 1, 128, 1>;   // 1x1 (Linear) GEMMs: 64 bf16 channels per stage
+using TSmall = Tile<128, 128, 2, 4, 2, 64, 2>;   // stride-2 conv or too few column tiles
+using T64x256 = Tile<64, 512, 1, 8, 4, 64, 1>;   // wave tile 64x64 (HiFi-GAN 64-channel stage)
+using T32x256 = Tile<32, 512, 1, 8, 4, 64, 1>;   // wave tile 32x64 (32-channel stage)
+using T16x256 = Tile<16, 512, 1, 8, 4, 64, 1>;   // wave tile 16x64 (conv_post, M = 1)
+
+// tile variants for in-process A/B timing of the op-level entry (mt_op_conv1d_tile)
+using V1 = Tile<128, 256, 2, 4, 4, 64, 1>;
+using V2 = Tile<128, 256, 2, 4, 2, 128, 1>;
+using V3 = Tile<128, 512, 2, 4, 2, 64, 1>;
+using V4 = Tile<128, 256, 2, 4, 3, 64, 1>;
+using V5 = Tile<128, 128, 2, 4, 4, 64, 1>;
+using V6 = Tile<128, 128, 2, 4, 1, 256, 1>;
 
 template <class E, class TL, int PF, int EF, int TAG = 0>
 static int launch_tile(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
@@ -474,8 +495,8 @@ static int check_args(const ConvArgs& a, int esize, int pf, int ef) {
   MT_REQUIRE(a.taps >= 1 && a.dil >= 1 && a.stride >= 1 && a.ups >= 1, "conv: taps/dil/stride");
   MT_REQUIRE(a.x0 && a.w && a.bias && (a.y || (ef & EF_EULER)), "conv: null pointer");
   MT_REQUIRE(a.c0 == a.cin || a.x1, "conv: second source missing");
-  if (pf & PF_LN) MT_REQUIRE(a.taps == 1 && a.stride == 1 && a.pad == 0 && a.c0 == a.cin && a.cin <= 512,
-                             "conv: LN prologue needs a single-source 1x1 GEMM with cin<=512");
+  if (pf & PF_LN) MT_REQUIRE(a.taps == 1 && a.stride == 1 && a.pad == 0 && a.ln_stats,
+                             "conv: LN prologue needs a 1x1 GEMM and row statistics");
   if (pf & PF_GN) MT_REQUIRE(a.cin <= 256 && a.cin % 32 == 0 && a.gn_in, "conv: GN prologue");
   if (ef & EF_GNADD) MT_REQUIRE(a.cout <= 256 && a.cout % 32 == 0 && a.gn_in && a.gy, "conv: GN epilogue");
   if (ef & EF_GNSTATS) MT_REQUIRE(a.M % 32 == 0 && a.gn_out && a.ups == 1, "conv: GN stats");
@@ -492,41 +513,43 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
   int rc = check_args(a, (int)sizeof(E), PF, EF);
   if (rc) return rc;
   const int M = a.M;
-  auto wgs = [&](int bm, int bn) {
-    return (long)a.B * ((a.Ncols + bn - 1) / bn) * ((M + bm - 1) / bm);
-  };
-  if constexpr ((CFGS & CFG_16x256) != 0)
+  if constexpr ((CFGS & CFG_16) != 0)
     if (M <= 16) return launch_tile<E, T16x256, PF, EF, TAG>(a, stream, ntiles_out);
-  if constexpr ((CFGS & CFG_32x256) != 0)
+  if constexpr ((CFGS & CFG_32) != 0)
     if (M <= 32) return launch_tile<E, T32x256, PF, EF, TAG>(a, stream, ntiles_out);
-  if constexpr ((CFGS & CFG_64x256) != 0)
+  if constexpr ((CFGS & CFG_64) != 0)
     if (M <= 64) return launch_tile<E, T64x256, PF, EF, TAG>(a, stream, ntiles_out);
-  if constexpr ((CFGS & CFG_128x256) != 0)
-    if (a.stride == 1 && (wgs(128, 256) >= 512 || (CFGS & CFG_128x128) == 0))
-      return launch_tile<E, T128x256, PF, EF, TAG>(a, stream, ntiles_out);
-  if constexpr ((CFGS & CFG_128x128) != 0) return launch_tile<E, T128x128, PF, EF, TAG>(a, stream, ntiles_out);
+  if constexpr ((CFGS & CFG_BIG) != 0) {
+    const long wgs = (long)a.B * ((a.Ncols + 255) / 256) * ((M + 127) / 128);
+    if (a.stride == 1 && (wgs >= 192 || (CFGS & CFG_SMALLN) == 0)) {
+      if (a.taps == 1) return launch_tile<E, TGemm, PF, EF, TAG>(a, stream, ntiles_out);
+      if (a.taps == 2) return launch_tile<E, TConvT, PF, EF, TAG>(a, stream, ntiles_out);
+      return launch_tile<E, TConv, PF, EF, TAG>(a, stream, ntiles_out);
+    }
+  }
+  if constexpr ((CFGS & CFG_SMALLN) != 0) return launch_tile<E, TSmall, PF, EF, TAG>(a, stream, ntiles_out);
   set_error("conv: no tile configuration for M=%d (pf %d ef %d)", M, PF, EF);
   return -1;
 }
 
 // (PF, EF, tile configs) combinations used by the decoder and the vocoder.
 #define MT_CONV_COMBOS(X)                                                              \
-  X(PF_MASK, EF_GNSTATS, CFG_128x256 | CFG_128x128)                                     \
-  X(PF_GN | PF_TB | PF_MASK, EF_GNSTATS, CFG_128x256 | CFG_128x128)                     \
-  X(PF_MASK, EF_GNADD, CFG_128x256 | CFG_128x128)                                       \
-  X(PF_LN, 0, CFG_128x256 | CFG_128x128)                                                \
-  X(0, EF_RESID, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256)                   \
-  X(PF_LN, EF_SNAKE, CFG_128x256 | CFG_128x128)                                         \
-  X(PF_MASK, 0, CFG_128x256 | CFG_128x128)                                              \
-  X(PF_GN | PF_MASK, EF_MASK | EF_EULER, CFG_128x256 | CFG_128x128)                     \
-  X(0, 0, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256 | CFG_16x256)             \
-  X(PF_LRELU, 0, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256 | CFG_16x256)      \
-  X(PF_LRELU, EF_RESID, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256)            \
-  X(PF_LRELU, EF_RESID | EF_ACCUM, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256) \
+  X(PF_MASK, EF_GNSTATS, CFG_BIG | CFG_SMALLN)                                     \
+  X(PF_GN | PF_TB | PF_MASK, EF_GNSTATS, CFG_BIG | CFG_SMALLN)                     \
+  X(PF_MASK, EF_GNADD, CFG_BIG | CFG_SMALLN)                                       \
+  X(PF_LN, 0, CFG_BIG | CFG_SMALLN)                                                \
+  X(0, EF_RESID, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32)                   \
+  X(PF_LN, EF_SNAKE, CFG_BIG | CFG_SMALLN)                                         \
+  X(PF_MASK, 0, CFG_BIG | CFG_SMALLN)                                              \
+  X(PF_GN | PF_MASK, EF_MASK | EF_EULER, CFG_BIG | CFG_SMALLN)                     \
+  X(0, 0, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32 | CFG_16)             \
+  X(PF_LRELU, 0, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32 | CFG_16)      \
+  X(PF_LRELU, EF_RESID, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32)            \
+  X(PF_LRELU, EF_RESID | EF_ACCUM, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32) \
   X(PF_LRELU, EF_RESID | EF_ACCUM | EF_DIV,                                            \
-    CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256)                                \
-  X(PF_LRELU, EF_RESID | EF_DIV, CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256)   \
-  X(PF_LRELU, EF_TANH | EF_OUTF32, CFG_16x256 | CFG_32x256)
+    CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32)                                \
+  X(PF_LRELU, EF_RESID | EF_DIV, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32)   \
+  X(PF_LRELU, EF_TANH | EF_OUTF32, CFG_16 | CFG_32)
 
 #define MT_DEFINE_LAUNCH(PFV, EFV, CFGV)                                                    \
   template <>                                                                             \
@@ -539,8 +562,29 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
   }
 MT_CONV_COMBOS(MT_DEFINE_LAUNCH)
 
-int launch_conv_op(int dtype, int pf, const ConvArgs& a, hipStream_t stream) {
-  constexpr int ALL = CFG_128x256 | CFG_128x128 | CFG_64x256 | CFG_32x256 | CFG_16x256;
+template <class E, int PF>
+static int launch_variant(int variant, const ConvArgs& a, hipStream_t stream) {
+  int rc = check_args(a, (int)sizeof(E), PF, 0);
+  if (rc) return rc;
+  switch (variant) {
+    case 0: return launch_tile<E, TConvT, PF, 0, 1>(a, stream, nullptr);
+    case 1: return launch_tile<E, V1, PF, 0, 1>(a, stream, nullptr);
+    case 2: return launch_tile<E, V2, PF, 0, 1>(a, stream, nullptr);
+    case 3: return launch_tile<E, V3, PF, 0, 1>(a, stream, nullptr);
+    case 4: return launch_tile<E, V4, PF, 0, 1>(a, stream, nullptr);
+    case 5: return launch_tile<E, V5, PF, 0, 1>(a, stream, nullptr);
+    case 6: return launch_tile<E, V6, PF, 0, 1>(a, stream, nullptr);
+    default: set_error("conv: unknown tile variant %d", variant); return -1;
+  }
+}
+
+int launch_conv_op(int dtype, int pf, const ConvArgs& a, hipStream_t stream, int variant) {
+  if (variant >= 0) {
+    MT_REQUIRE(pf == PF_LRELU, "conv: tile variants are compiled for the lrelu prologue only");
+    return dtype == BF16 ? launch_variant<bf16, PF_LRELU>(variant, a, stream)
+                         : launch_variant<float, PF_LRELU>(variant, a, stream);
+  }
+  constexpr int ALL = CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32 | CFG_16;
   if (pf == PF_LRELU)
     return dtype == BF16 ? launch_sel<bf16, PF_LRELU, 0, ALL, 1>(a, stream, nullptr)
                          : launch_sel<float, PF_LRELU, 0, ALL, 1>(a, stream, nullptr);

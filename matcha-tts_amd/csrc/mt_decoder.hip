@@ -70,11 +70,12 @@ GemmW make_convT(int cin, int cout, int k, int s, int pad, int w, int b, int esi
 int pack_gemm(const GemmW& g, int dtype, const float* const* params, char* P, hipStream_t st) {
   int rc;
   void* wdst = P + g.w_off;
+  const float* colscale = g.ln_g >= 0 ? params[g.ln_g] : nullptr;
   if (g.kind == 0) {
     const int rows_per = g.cout / (int)g.wsrc.size();
     for (size_t i = 0; i < g.wsrc.size(); ++i) {
       rc = pack_conv(dtype, params[g.wsrc[i]], 0, rows_per, g.cin, g.k, 1, (int)i * rows_per, rows_per,
-                     g.Mpad, g.taps, g.cin_pad, wdst, st);
+                     g.Mpad, g.taps, g.cin_pad, wdst, st, colscale);
       if (rc) return rc;
     }
     const int rest = g.Mpad - g.cout;  // zero pad rows
@@ -87,7 +88,16 @@ int pack_gemm(const GemmW& g, int dtype, const float* const* params, char* P, hi
                    g.cin_pad, wdst, st);
     if (rc) return rc;
   }
-  return pack_vec(g.bsrc >= 0 ? params[g.bsrc] : nullptr, g.cout, g.M, 0, (float*)(P + g.b_off), st);
+  rc = pack_vec(g.bsrc >= 0 ? params[g.bsrc] : nullptr, g.cout, g.M, 0, (float*)(P + g.b_off), st);
+  if (rc) return rc;
+  if (g.ln_b >= 0) {  // LN(x) = x_hat*gamma + beta  ->  W(gamma) x_hat + (b + W beta)
+    const int rows_per = g.cout / (int)g.wsrc.size();
+    for (size_t i = 0; i < g.wsrc.size(); ++i) {
+      rc = fold_bias(params[g.wsrc[i]], params[g.ln_b], rows_per, g.cin, (float*)(P + g.b_off) + i * rows_per, st);
+      if (rc) return rc;
+    }
+  }
+  return 0;
 }
 
 void gemm_geom(const GemmW& g, int Tin, int* Tout, int* Ncols) {
@@ -203,8 +213,12 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
       int w2 = L.add(q + ".ff.net.2.weight", {C, TE});
       int b2 = L.add(q + ".ff.net.2.bias", {C});
       t.qkv = make_conv(3 * inner, C, 1, 1, 0, 1, {wq, wk, wv}, -1, esize, pk);
+      t.qkv.ln_g = t.ln1g;
+      t.qkv.ln_b = t.ln1b;
       t.out = make_conv(C, inner, 1, 1, 0, 1, {wo}, bo, esize, pk);
       t.ff1 = make_conv(TE, C, 1, 1, 0, 1, {w1}, b1, esize, pk);
+      t.ff1.ln_g = t.ln3g;
+      t.ff1.ln_b = t.ln3b;
       t.ff2 = make_conv(C, TE, 1, 1, 0, 1, {w2}, b2, esize, pk);
       t.ln1_off = pk.take(2 * C * 4);
       t.ln3_off = pk.take(2 * C * 4);
@@ -319,6 +333,7 @@ size_t Decoder::workspace_bytes(int B, int T, int S) const {
   n += align256(BT * inner * esize);                  // ob
   n += align256(BT * TE * esize);                     // ff
   n += align256(BT * NF * 4);                         // zm
+  n += align256(BT * 2 * 4);                          // lns (LayerNorm row stats)
   n += align256((size_t)B * ((T + 1) / 2) * 4);       // m1
   n += 2 * align256((size_t)B * 8 * ntl * 2 * 8);     // gn1 gn2
   n += align256((size_t)S * c_cond * 4);              // emb
@@ -351,6 +366,7 @@ Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
   w.ob = take(BT * inner * esize);
   w.ff = take(BT * TE * esize);
   w.zm = (float*)take(BT * NF * 4);
+  w.lns = (float*)take(BT * 2 * 4);
   w.m1 = (float*)take((size_t)B * ((T + 1) / 2) * 4);
   w.gn1 = (double*)take((size_t)B * 8 * ntl * 2 * 8);
   w.gn2 = (double*)take((size_t)B * 8 * ntl * 2 * 8);
@@ -428,11 +444,11 @@ template <class E>
 int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, int B, int Tl,
                     hipStream_t st) const {
   int rc;
+  if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
   ConvArgs q = gemm_args(t.qkv, P, B, Tl);
   q.x0 = x;
   q.y = w.qkv;
-  q.ln_g = (const float*)(P + t.ln1_off);
-  q.ln_b = (const float*)(P + t.ln1_off) + C;
+  q.ln_stats = w.lns;
   if ((rc = launch_conv<E, PF_LN, 0>(q, st))) return rc;
   if ((rc = launch_attention(dtype, w.qkv, mask, w.ob, B, Tl, heads, st))) return rc;
   ConvArgs o = gemm_args(t.out, P, B, Tl);
@@ -441,11 +457,11 @@ int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const fl
   o.resid = x;
   o.ldr = C;
   if ((rc = launch_conv<E, 0, EF_RESID>(o, st))) return rc;
+  if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
   ConvArgs f1 = gemm_args(t.ff1, P, B, Tl);
   f1.x0 = x;
   f1.y = w.ff;
-  f1.ln_g = (const float*)(P + t.ln3_off);
-  f1.ln_b = (const float*)(P + t.ln3_off) + C;
+  f1.ln_stats = w.lns;
   f1.snake_alpha = (const float*)(P + t.snake_off);
   f1.snake_ibeta = (const float*)(P + t.snake_off) + TE;
   if ((rc = launch_conv<E, PF_LN, EF_SNAKE>(f1, st))) return rc;

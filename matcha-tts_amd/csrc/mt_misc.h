@@ -10,7 +10,9 @@ struct TimeSched {
 };
 
 int pack_conv(int dtype, const float* W, int kind, int cout, int cin, int k, int s, int row0, int Mrows,
-              int Mpad, int taps, int cin_pad, void* out, hipStream_t st);
+              int Mpad, int taps, int cin_pad, void* out, hipStream_t st, const float* colscale = nullptr);
+int rowstats(int dtype, const void* x, int rows, int C, float eps, float* stats, hipStream_t st);
+int fold_bias(const float* W, const float* beta, int M, int K, float* out, hipStream_t st);
 int pack_vec(const float* src, int period, int n, int op, float* out, hipStream_t st);
 
 int bct_to_btc(int dtype, const float* src, int B, int C, int T, float scale, void* dst, int ld, int coff,

@@ -16,7 +16,7 @@ namespace mt {
 template <class E>
 __global__ void pack_conv_kernel(const float* __restrict__ W, int kind, int cout, int cin, int k,
                                  int s, int row0, int Mpad, int taps, int cin_pad, int Mrows,
-                                 E* __restrict__ out) {
+                                 const float* __restrict__ colscale, E* __restrict__ out) {
   const size_t total = (size_t)Mrows * taps * cin_pad;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
@@ -26,7 +26,7 @@ __global__ void pack_conv_kernel(const float* __restrict__ W, int kind, int cout
     float v = 0.f;
     if (ci < cin) {
       if (kind == 0) {
-        if (m < cout) v = W[((size_t)m * cin + ci) * k + t];
+        if (m < cout) v = W[((size_t)m * cin + ci) * k + t] * (colscale ? colscale[ci] : 1.f);
       } else {
         const int ph = m / cout, co = m % cout;
         if (ph < s) {
@@ -41,15 +41,15 @@ __global__ void pack_conv_kernel(const float* __restrict__ W, int kind, int cout
 }
 
 int pack_conv(int dtype, const float* W, int kind, int cout, int cin, int k, int s, int row0,
-              int Mrows, int Mpad, int taps, int cin_pad, void* out, hipStream_t st) {
+              int Mrows, int Mpad, int taps, int cin_pad, void* out, hipStream_t st, const float* colscale) {
   const size_t total = (size_t)Mrows * taps * cin_pad;
   const int blocks = (int)std::min<size_t>((total + 255) / 256, 65535);
   if (dtype == BF16)
     hipLaunchKernelGGL(pack_conv_kernel<bf16>, dim3(blocks), dim3(256), 0, st, W, kind, cout, cin, k, s,
-                       row0, Mpad, taps, cin_pad, Mrows, (bf16*)out);
+                       row0, Mpad, taps, cin_pad, Mrows, colscale, (bf16*)out);
   else
     hipLaunchKernelGGL(pack_conv_kernel<float>, dim3(blocks), dim3(256), 0, st, W, kind, cout, cin, k,
-                       s, row0, Mpad, taps, cin_pad, Mrows, (float*)out);
+                       s, row0, Mpad, taps, cin_pad, Mrows, colscale, (float*)out);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -67,6 +67,76 @@ __global__ void vec_kernel(const float* __restrict__ src, int period, int n, int
 
 int pack_vec(const float* src, int period, int n, int op, float* out, hipStream_t st) {
   hipLaunchKernelGGL(vec_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, period, n, op, out);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// LayerNorm folding (pack time): out[row0 + m] += sum_i W[m][i] * beta[i]  (W [M][K] fp32, Linear)
+__global__ void fold_bias_kernel(const float* __restrict__ W, const float* __restrict__ beta, int M, int K,
+                                 float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  double acc = 0.0;
+  for (int i = lane; i < K; i += 64) acc += (double)W[(size_t)m * K + i] * (double)beta[i];
+  acc = wave_sum_d(acc);
+  if (lane == 0) out[m] = (float)((double)out[m] + acc);
+}
+
+int fold_bias(const float* W, const float* beta, int M, int K, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(fold_bias_kernel, dim3((M + 3) / 4), dim3(256), 0, st, W, beta, M, K, out);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
+// LayerNorm row statistics (nn.LayerNorm over the channel axis of [rows][C], C = 256):
+// 16 lanes per row, two-pass in registers (mean, then mean of squared deviations).
+// ------------------------------------------------------------------------------------
+template <class E, int C>
+__global__ __launch_bounds__(256) void rowstats_kernel(const E* __restrict__ x, int rows, float eps,
+                                                       float* __restrict__ stats) {
+  constexpr int VN = Vec16<E>::N;
+  constexpr int NV = C / 16 / VN;  // 16-byte vectors per lane
+  const int lane = threadIdx.x & 63;
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+  const int sub = lane & 15;
+  const bool ok = row < rows;
+  const E* p = x + (size_t)(ok ? row : 0) * C;
+  Vec16<E> v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = load16(p + (i * 16 + sub) * VN);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int k = 0; k < VN; ++k) s += v[i].get(k);
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int k = 0; k < VN; ++k) {
+      const float d = v[i].get(k) - mean;
+      q += d * d;
+    }
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o, 64);
+  if (ok && sub == 0) {
+    stats[(size_t)row * 2] = mean;
+    stats[(size_t)row * 2 + 1] = 1.f / sqrtf(q / (float)C + eps);
+  }
+}
+
+int rowstats(int dtype, const void* x, int rows, int C, float eps, float* stats, hipStream_t st) {
+  MT_REQUIRE(C == 256, "rowstats: C=%d (built for 256)", C);
+  dim3 grid((rows * 16 + 255) / 256);
+  if (dtype == BF16)
+    hipLaunchKernelGGL((rowstats_kernel<bf16, 256>), grid, dim3(256), 0, st, (const bf16*)x, rows, eps, stats);
+  else
+    hipLaunchKernelGGL((rowstats_kernel<float, 256>), grid, dim3(256), 0, st, (const float*)x, rows, eps, stats);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -37,6 +37,7 @@ struct GemmW {
   int M = 0, Mpad = 0, taps = 1, cin_pad = 0, gpad = 0, ups = 1, opad = 0;
   std::vector<int> wsrc;  // weight params (several = rows stacked, e.g. Q|K|V)
   int bsrc = -1;          // bias param or -1 (zeros)
+  int ln_g = -1, ln_b = -1;  // LayerNorm (on the input channels) folded into W and bias
   size_t w_off = 0, b_off = 0;
 };
 
@@ -83,7 +84,7 @@ struct Decoder {
 
   struct Work {
     char *xin, *H0, *H1, *XA, *XB, *XC, *U, *XF, *y1, *y2, *qkv, *ob, *ff;
-    float *zm, *m1, *emb, *h1, *h2, *tb;
+    float *zm, *m1, *emb, *h1, *h2, *tb, *lns;
     double *gn1, *gn2;
     const float* m0;
   };

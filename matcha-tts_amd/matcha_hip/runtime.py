@@ -284,7 +284,8 @@ def denoise(audio: torch.Tensor, bias_spec: torch.Tensor, strength: float) -> to
 
 
 def op_conv1d(x_btc: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], stride=1, pad=0, dil=1,
-              transposed=False, slope: Optional[float] = None, precision="fp32") -> torch.Tensor:
+              transposed=False, slope: Optional[float] = None, precision="fp32", variant: int = -1,
+              out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Op-level test entry: y = conv(lrelu(x)) on [B,T,C] activations (dtype by precision)."""
     require_gpu(x_btc, what="op_conv1d")
     dt = dtype_code(precision)
@@ -297,14 +298,15 @@ def op_conv1d(x_btc: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor]
     else:
         cout, k = W.shape[0], W.shape[2]
         tout = (Tin + 2 * pad - dil * (k - 1) - 1) // stride + 1
-    y = torch.empty((B, tout, cout), dtype=et, device=x.device)
+    y = torch.empty((B, tout, cout), dtype=et, device=x.device) if out is None else out
     L = lib()
     nb = L.mt_op_conv1d_workspace_bytes(dt, cin, cout, k, stride, int(transposed))
-    ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
+    if ws is None or ws.numel() < nb:
+        ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
     W, bias = f32c(W), f32c(bias)
-    check(L.mt_op_conv1d(dt, ptr(x), B, Tin, cin, ptr(W), ptr(bias), cout, k, stride, pad, dil, int(transposed),
-                         -1.0 if slope is None else float(slope), ptr(y), tout, ws.data_ptr(), ws.numel(),
-                         stream_handle(x.device)), "op_conv1d")
+    check(L.mt_op_conv1d_tile(int(variant), dt, ptr(x), B, Tin, cin, ptr(W), ptr(bias), cout, k, stride, pad, dil,
+                              int(transposed), -1.0 if slope is None else float(slope), ptr(y), tout, ws.data_ptr(),
+                              ws.numel(), stream_handle(x.device)), "op_conv1d")
     return y
 
 
