@@ -91,6 +91,9 @@ int mt_vocoder_num_params(const mt_vocoder* v);
 int mt_vocoder_param_name(const mt_vocoder* v, int i, char* buf, int buflen);
 int mt_vocoder_param_shape(const mt_vocoder* v, int i, int64_t* shape, int maxdim);
 size_t mt_vocoder_packed_bytes(const mt_vocoder* v);
+/* fused ResBlock stages for the 32/64-channel stages in bf16 (default on; bit-identical to the
+ * per-layer path, which 0 selects) */
+int mt_vocoder_set_fusion(mt_vocoder* v, int enable);
 int mt_vocoder_pack(const mt_vocoder* v, const float* const* params, void* packed, void* stream);
 size_t mt_vocoder_workspace_bytes(const mt_vocoder* v, int B, int T);
 /* mel [B,80,T] fp32 -> wav [B,1,T*prod(up_rates)] fp32 */
@@ -138,6 +141,18 @@ int mt_op_conv1d_tile(int variant, int dtype, const void* x, int B, int Tin, int
 /* qkv [B][T][3*heads*64], mask [B][T] -> out [B][T][heads*64], reference mask semantics */
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                     void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Launch probe (measurement only; no reference counterpart). Arms HIP events around every
+ * launch of one kernel site, on the stream the kernel is launched on, so a benchmark can time
+ * that kernel inside its own timed region. Sites: 1 = fused 64-channel HiFi-GAN ResBlock stage,
+ * 2 = fused 32-channel stage. mt_probe_stop synchronizes the recorded events and returns the
+ * number of launches, their summed duration and the algorithmic FLOPs / bytes they did.
+ * ------------------------------------------------------------------------------------- */
+#define MT_PROBE_RBFUSE_C64 1
+#define MT_PROBE_RBFUSE_C32 2
+int mt_probe_start(int site, int max_launches);
+int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes);
 
 #ifdef __cplusplus
 }

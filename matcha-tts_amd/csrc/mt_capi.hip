@@ -5,6 +5,7 @@
 
 #include "../../include/matcha_hip.h"
 #include "mt_model.h"
+#include "mt_probe.h"
 
 namespace mt {
 const char* last_error();
@@ -122,6 +123,11 @@ int mt_vocoder_param_shape(const mt_vocoder* v, int i, int64_t* shape, int maxdi
   MT_REQUIRE(v, "null vocoder");
   return param_shape(v->v.params, i, shape, maxdim);
 }
+int mt_vocoder_set_fusion(mt_vocoder* v, int enable) {
+  MT_REQUIRE(v, "null vocoder");
+  v->v.fuse = enable ? 1 : 0;
+  return 0;
+}
 size_t mt_vocoder_packed_bytes(const mt_vocoder* v) { return v ? v->v.packed_bytes : 0; }
 int mt_vocoder_pack(const mt_vocoder* v, const float* const* params, void* packed, void* stream) {
   MT_REQUIRE(v && params && packed, "vocoder_pack: null argument");
@@ -208,6 +214,12 @@ int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, in
                     void* stream) {
   MT_REQUIRE(qkv && mask && out, "op_attention: null argument");
   return mt::launch_attention(dtype, qkv, mask, out, B, T, heads, (hipStream_t)stream);
+}
+
+int mt_probe_start(int site, int max_launches) { return mt::probe_start(site, max_launches); }
+
+int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes) {
+  return mt::probe_stop(launches, total_ms, flops, bytes);
 }
 
 }  // extern "C"

@@ -118,6 +118,7 @@ struct Decoder {
 // -------------------------------------------------------------------------------------
 struct Vocoder {
   int resblock = 1, dtype = BF16, esize = 2;
+  int fuse = 1;  // fused ResBlock stages (mt_rbfuse) where supported
   std::vector<int> up_rates, up_kernels, rb_kernels;
   std::vector<std::vector<int>> rb_dils;
   int up_init = 512, n_mels = 80;

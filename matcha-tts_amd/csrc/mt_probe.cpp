@@ -1,0 +1,79 @@
+#include "mt_probe.h"
+
+#include <mutex>
+#include <vector>
+
+namespace mt {
+namespace {
+std::mutex g_mu;
+int g_site = PROBE_NONE;
+std::vector<hipEvent_t> g_ev;  // 2 per launch: begin, end
+int g_n = 0, g_cap = 0;
+double g_flops = 0, g_bytes = 0;
+bool g_open = false;
+
+void release() {
+  for (hipEvent_t e : g_ev) (void)hipEventDestroy(e);
+  g_ev.clear();
+  g_n = g_cap = 0;
+  g_flops = g_bytes = 0;
+  g_site = PROBE_NONE;
+  g_open = false;
+}
+}  // namespace
+
+bool probe_armed(int site) { return g_site != PROBE_NONE && g_site == site; }
+
+void probe_begin(int site, hipStream_t st) {
+  if (!probe_armed(site)) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_n >= g_cap || g_open) return;
+  (void)hipEventRecord(g_ev[2 * g_n], st);
+  g_open = true;
+}
+
+void probe_end(int site, hipStream_t st, double flops, double bytes) {
+  if (!probe_armed(site)) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_open) return;
+  (void)hipEventRecord(g_ev[2 * g_n + 1], st);
+  g_open = false;
+  ++g_n;
+  g_flops += flops;
+  g_bytes += bytes;
+}
+
+int probe_start(int site, int max_launches) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  release();
+  MT_REQUIRE(site > PROBE_NONE && site <= PROBE_RBFUSE_C32, "probe: unknown site %d", site);
+  MT_REQUIRE(max_launches > 0 && max_launches <= (1 << 16), "probe: max_launches %d", max_launches);
+  g_ev.resize(2 * (size_t)max_launches);
+  for (hipEvent_t& e : g_ev) MT_CHECK_HIP(hipEventCreate(&e));
+  g_cap = max_launches;
+  g_site = site;
+  return 0;
+}
+
+int probe_stop(int* launches, double* total_ms, double* flops, double* bytes) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  double ms = 0;
+  int rc = 0;
+  for (int i = 0; i < g_n && rc == 0; ++i) {
+    float t = 0.f;
+    if (hipEventSynchronize(g_ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&t, g_ev[2 * i], g_ev[2 * i + 1]) != hipSuccess) {
+      set_error("probe: event timing failed");
+      rc = -1;
+    }
+    ms += t;
+  }
+  if (launches) *launches = g_n;
+  if (total_ms) *total_ms = ms;
+  if (flops) *flops = g_flops;
+  if (bytes) *bytes = g_bytes;
+  release();
+  return rc;
+}
+
+}  // namespace mt

@@ -1,0 +1,21 @@
+// Launch probe: HIP events recorded on the launching stream around every launch of one kernel
+// site, so a caller (bench.py) can time that kernel inside its own timed region and read the
+// algorithmic work the launches did. Off unless mt_probe_start() armed it; host-only state.
+#pragma once
+#include "mt_common.h"
+
+namespace mt {
+
+enum ProbeSite {
+  PROBE_NONE = 0,
+  PROBE_RBFUSE_C64 = 1,  // fused HiFi-GAN ResBlock stage, 64 channels (stage 3 of v1)
+  PROBE_RBFUSE_C32 = 2,  // fused HiFi-GAN ResBlock stage, 32 channels (stage 4 of v1)
+};
+
+bool probe_armed(int site);
+void probe_begin(int site, hipStream_t st);
+void probe_end(int site, hipStream_t st, double flops, double bytes);
+int probe_start(int site, int max_launches);
+int probe_stop(int* launches, double* total_ms, double* flops, double* bytes);
+
+}  // namespace mt

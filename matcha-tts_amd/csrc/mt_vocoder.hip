@@ -10,6 +10,7 @@
 #include <algorithm>
 
 #include "mt_model.h"
+#include "mt_rbfuse.h"
 
 namespace mt {
 
@@ -145,6 +146,49 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     u.slope = 0.1f;
     if ((rc = launch_conv<E, PF_LRELU, 0>(u, st))) return rc;
     L = u.Tout;
+    const int C = ups[i].cout;
+    bool uniform = true;
+    for (const auto& dl : rb_dils) uniform = uniform && dl.size() == rb_dils[0].size();
+    if (fuse && resblock == 1 && nk <= 3 && rbfuse_supported(dtype, C) && uniform && rb_dils[0].size() <= 3) {
+      // whole stage in one launch: y = (sum_j resblock_j(x)) / nk, intermediates in LDS
+      RBArgs r{};
+      r.x = X;
+      r.y = XS;
+      r.B = B;
+      r.L = L;
+      r.nk = nk;
+      r.npair = (int)rb_dils[0].size();
+      r.slope = 0.1f;
+      r.div = (float)nk;
+      int hm = 0;
+      for (int j = 0; j < nk; ++j) {
+        const int q = (rb_kernels[j] - 1) / 2;
+        int h = 0;
+        for (int d : rb_dils[j]) h += q * d + q;
+        hm = std::max(hm, h);
+      }
+      r.hmax = hm;
+      const int N = rbfuse_tile_n(C);
+      for (int j = 0; j < nk; ++j) {
+        const int q = (rb_kernels[j] - 1) / 2;
+        r.k[j] = rb_kernels[j];
+        int A = hm, Bv = hm + N;  // rows each conv must produce, from the output backwards
+        for (int p = r.npair - 1; p >= 0; --p) {
+          const int d = rb_dils[j][p];
+          r.dil[j][p] = d;
+          r.c1[j][p] = RBConv{P + rb1[i * nk + j][p].w_off, (const float*)(P + rb1[i * nk + j][p].b_off)};
+          r.c2[j][p] = RBConv{P + rb2[i * nk + j][p].w_off, (const float*)(P + rb2[i * nk + j][p].b_off)};
+          r.r2a[j][p] = A;
+          r.r2b[j][p] = Bv;
+          r.r1a[j][p] = A - q;
+          r.r1b[j][p] = Bv + q;
+          A -= q + q * d;
+          Bv += q + q * d;
+        }
+      }
+      if ((rc = launch_rbfuse(dtype, C, r, st))) return rc;
+      continue;
+    }
     for (int j = 0; j < nk; ++j) {
       const std::vector<GemmW>& c1 = rb1[i * nk + j];
       const std::vector<GemmW>& c2 = rb2[i * nk + j];

@@ -181,6 +181,9 @@ class VocoderEngine:
         self._packed = None
         self._fp = None
 
+    def set_fusion(self, enable: bool) -> None:
+        check(lib().mt_vocoder_set_fusion(self.h, int(bool(enable))), "vocoder_set_fusion")
+
     def __del__(self):
         try:
             if getattr(self, "h", None):
