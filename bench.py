@@ -46,7 +46,6 @@ def parse():
     p.add_argument("--no-denoise", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
-    p.add_argument("--roofline-reps", type=int, default=20)
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()
 
@@ -95,33 +94,25 @@ def step(m, g, den, x, xl, n_ts, denoise):
     return mel, yl, wav
 
 
-def roofline_leg(batch, t_y, precision, reps, device):
-    """Dominant kernel: the HiFi-GAN stage-2 ResBlock conv (128 ch, k=11, d=5) on B x 64*T_y frames
-    — the implicit-GEMM conv kernel's heaviest layer shape — relaunched alone through the op-level
-    C entry (same kernel code, TAG=1 symbol) and timed with HIP events on its stream."""
-    from matcha_hip import runtime as rt
-    C, k, d = 128, 11, 5
-    L = 64 * t_y
-    gen = torch.Generator(device="cpu").manual_seed(0)
-    x = torch.randn(batch, L, C, generator=gen).to(device)
-    W = (torch.randn(C, C, k, generator=gen) / math.sqrt(C * k)).to(device)
-    b = torch.zeros(C, device=device)
-    rt.op_conv1d(x, W, b, 1, d * (k - 1) // 2, d, False, 0.1, precision)  # warm
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        rt.op_conv1d(x, W, b, 1, d * (k - 1) // 2, d, False, 0.1, precision)
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / reps
-    esz = 2 if precision == "bf16" else 4
-    flops = 2.0 * C * C * k * batch * L
-    algo_bytes = 2.0 * batch * L * C * esz + C * C * k * esz
-    peak = 2500.0 if precision == "bf16" else 157.3  # dense TFLOP/s (MI355X_MICROARCH.md)
+def roofline(probe, precision):
+    """Dominant kernel of the step: the fused 64-channel HiFi-GAN ResBlock stage (mt_rbfuse,
+    stage 3 of v1: 3 resblocks x 3 pairs of 64x64 convs, k 3/7/11, on B x 128*T_y frames), timed by
+    HIP events recorded on its own stream around each of its launches INSIDE the timed region
+    (mt_probe_*). Algorithmic FLOPs per launch = 2 * 6 * 64 * 64 * (3+7+11) * B * 128 * T_y; its
+    algorithmic bytes = stage input + output (B * 128 * T_y * 64 * 2 B each) + weights. MFMA-bound
+    (intensity ~2,000 FLOP/B), so the peak is the dense bf16 MFMA rate. `traffic` is the HBM bytes
+    per launch measured with rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, committed
+    in profiles/r01_pmc_rbfuse64.json by tools_pmc.sh on this same bench command."""
+    if probe is None or probe["launches"] == 0:
+        return {"bound": "mfma", "achieved": None, "peak": 2500.0, "unit": "TFLOP/s", "frac": None,
+                "traffic": None, "kernel": "rbfuse_kernel<bf16,64> (bf16 path only)"}
+    n = probe["launches"]
+    ms = probe["ms"] / n
+    flops = probe["flops"] / n
     achieved = flops / (ms * 1e-3) / 1e12
+    peak = 2500.0  # dense bf16 MFMA TFLOP/s (MI355X_MICROARCH.md)
     traffic = None
-    pmc = os.path.join(HERE, "profiles", "r01_pmc_roofline.json")
+    pmc = os.path.join(HERE, "profiles", "r01_pmc_rbfuse64.json")
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
@@ -129,9 +120,10 @@ def roofline_leg(batch, t_y, precision, reps, device):
             traffic = None
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic,
-            "kernel": f"conv_kernel<{precision},TAG=1> ResBlock conv 128ch k11 d5",
-            "launch_ms": round(ms, 4), "flops_per_launch": flops, "algo_bytes_per_launch": algo_bytes,
-            "intensity_flop_per_byte": round(flops / algo_bytes, 1)}
+            "kernel": "rbfuse_kernel<bf16,64,192> fused HiFi-GAN stage-3 ResBlocks (64 ch)",
+            "launches": n, "launch_ms": round(ms, 4), "flops_per_launch": flops,
+            "algo_bytes_per_launch": probe["bytes"] / n,
+            "intensity_flop_per_byte": round(flops / (probe["bytes"] / n), 1)}
 
 
 def cpu_baseline(m_sd, g_sd, x, xl, n_ts, seconds):
@@ -195,12 +187,15 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    from matcha_hip import runtime as rt
+    rt.probe_start(rt.PROBE_RBFUSE_C64, 4 * a.steps)
     barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(m, g, den, x, xl, a.n_timesteps, denoise)
     barrier()
     el = time.perf_counter() - t0
+    probe = rt.probe_stop()
 
     tot_frames = frames
     if dist is not None:
@@ -228,7 +223,7 @@ def main():
     }
     if rank == 0:
         if world == 1:
-            out["roofline"] = roofline_leg(a.batch, t_y, a.precision, a.roofline_reps, device)
+            out["roofline"] = roofline(probe, a.precision)
             if not a.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline(msd, gsd, x_cpu, xl_cpu, a.n_timesteps, a.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -29,12 +29,13 @@ __device__ __forceinline__ float mish_e(float x) {
 }
 
 // Tile configuration (compile time): BM x BN output tile, WAVES_M x WAVES_N waves, TG taps and
-// CK bytes of input channels per K-stage (LDS rows of CK+16 bytes: conflict-free ds_read_b128
-// for CK in {64,128,256}), SMAX = largest stride served. Static LDS: two stage buffers + tables.
+// CK bytes of input channels per K-stage (LDS rows of CK+32 bytes: the 16-row x 4-column MFMA
+// fragment reads then hit 16 distinct 16-byte bank slots in every ds_read_b128 lane group, for CK
+// in {64,128,256}; CK+16 rows were 2-way conflicted), SMAX = largest stride served. Static LDS: two stage buffers + tables.
 template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, int TG_, int CK_, int SMAX_>
 struct Tile {
   static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, TG = TG_, SMAX = SMAX_;
-  static constexpr int CK = CK_, ROW = CK_ + 16, VPR = CK_ / 16, KS = CK_ / 64;
+  static constexpr int CK = CK_, ROW = CK_ + 32, VPR = CK_ / 16, KS = CK_ / 64;
   static constexpr int NT = 64 * WAVES_M * WAVES_N;
   static constexpr int DMAX = 5;  // largest dilation served (HiFi-GAN v1: 1, 3, 5)
   static constexpr int RBMAX = (BN - 1) * SMAX + (TG - 1) * DMAX + 1;
@@ -464,11 +465,15 @@ using T16x256 = Tile<16, 512, 1, 8, 4, 64, 1>;   // wave tile 16x64 (conv_post, 
 
 // tile variants for in-process A/B timing of the op-level entry (mt_op_conv1d_tile)
 using V1 = Tile<128, 256, 2, 4, 4, 64, 1>;
-using V2 = Tile<128, 256, 2, 4, 2, 128, 1>;
+using V2 = Tile<128, 128, 2, 4, 2, 128, 1>;
 using V3 = Tile<128, 512, 2, 4, 2, 64, 1>;
 using V4 = Tile<128, 256, 2, 4, 3, 64, 1>;
 using V5 = Tile<128, 128, 2, 4, 4, 64, 1>;
 using V6 = Tile<128, 128, 2, 4, 1, 256, 1>;
+using V7 = Tile<128, 128, 2, 2, 2, 64, 1>;   // 4 waves, 77 KB: two workgroups per CU
+using V8 = Tile<64, 128, 2, 2, 4, 64, 1>;    // 4 waves, 79 KB: two workgroups per CU
+using V9 = Tile<64, 256, 2, 4, 2, 64, 1>;    // 8 waves, 78 KB: two workgroups per CU
+using V10 = Tile<128, 128, 2, 2, 4, 64, 1>;  // 4 waves, one workgroup per CU
 
 template <class E, class TL, int PF, int EF, int TAG = 0>
 static int launch_tile(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
@@ -574,6 +579,10 @@ static int launch_variant(int variant, const ConvArgs& a, hipStream_t stream) {
     case 4: return launch_tile<E, V4, PF, 0, 1>(a, stream, nullptr);
     case 5: return launch_tile<E, V5, PF, 0, 1>(a, stream, nullptr);
     case 6: return launch_tile<E, V6, PF, 0, 1>(a, stream, nullptr);
+    case 7: return launch_tile<E, V7, PF, 0, 1>(a, stream, nullptr);
+    case 8: return launch_tile<E, V8, PF, 0, 1>(a, stream, nullptr);
+    case 9: return launch_tile<E, V9, PF, 0, 1>(a, stream, nullptr);
+    case 10: return launch_tile<E, V10, PF, 0, 1>(a, stream, nullptr);
     default: set_error("conv: unknown tile variant %d", variant); return -1;
   }
 }

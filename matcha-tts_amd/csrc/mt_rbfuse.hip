@@ -28,7 +28,9 @@ struct RBTile {
   static constexpr int NT = 512, NW = 8;
   static constexpr int HMAX = 60;
   static constexpr int W0 = N + 2 * HMAX;
-  static constexpr int ROW = C * (int)sizeof(E) + 16;  // conflict-free ds_read_b128 rows
+  // rows padded by 32 bytes: the MFMA fragment reads (16 rows x 4 16-byte columns, ds_read_b128 lane
+  // groups {0-3,12-15,20-27}, ...) then hit 16 distinct 16-byte bank slots per group
+  static constexpr int ROW = C * (int)sizeof(E) + 32;
   static constexpr int KC = C * (int)sizeof(E) / 64;   // 64-byte K slices per row
   static constexpr int VPR = C * (int)sizeof(E) / 16;  // 16-byte vectors per row
   static constexpr int FMJ = 2;                        // job = 32 output channels x 16 frames
@@ -36,9 +38,9 @@ struct RBTile {
   static constexpr int WPC = NW / CB;                  // waves per channel block
   static constexpr int JPW = ((W0 + 15) / 16 + WPC - 1) / WPC;  // frame blocks per wave (widest conv)
   static constexpr int OJ = N / 16 / WPC;              // frame blocks per wave in the last conv
-  // +32 spare rows: a partial last frame block reads up to 15 + q*d rows past a conv's range
+  // +16 spare rows: a partial last frame block reads up to 15 rows past the conv's input rows
   // (those columns are discarded), which must stay inside the buffer set
-  static constexpr int BUF = (W0 + 32) * ROW;
+  static constexpr int BUF = (W0 + 16) * ROW;
   static constexpr int LDS = 3 * BUF;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(N % (16 * WPC) == 0, "output frame blocks must split evenly over the waves");

@@ -324,3 +324,20 @@ def op_attention(qkv: torch.Tensor, mask: torch.Tensor, heads: int, precision="f
     check(lib().mt_op_attention(dt, ptr(qkv), ptr(mask), ptr(out), B, T, heads, stream_handle(qkv.device)),
           "op_attention")
     return out
+
+
+# ---------------------------------------------------------------------------------- launch probe
+PROBE_RBFUSE_C64, PROBE_RBFUSE_C32 = 1, 2
+
+
+def probe_start(site: int, max_launches: int) -> None:
+    """Arm HIP events around every launch of one kernel site (see mt_probe_start)."""
+    check(lib().mt_probe_start(int(site), int(max_launches)), "probe_start")
+
+
+def probe_stop() -> Dict[str, float]:
+    """Synchronize the probe's events; launches, summed kernel ms, algorithmic FLOPs and bytes."""
+    from ctypes import c_double
+    n, ms, fl, by = c_int(0), c_double(0), c_double(0), c_double(0)
+    check(lib().mt_probe_stop(byref(n), byref(ms), byref(fl), byref(by)), "probe_stop")
+    return {"launches": n.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}

@@ -220,3 +220,22 @@ def test_vocoder_mid_size_vs_oracle():
     ref = O.generator_forward({k: v.cpu() for k, v in gen.state_dict().items()}, mel, v1)
     wav = gen(mel.cuda()).cpu()
     assert (wav - ref).abs().max() < 2e-5
+
+
+def test_launch_probe_times_fused_stage():
+    """mt_probe_*: events around every fused 64-channel stage launch, algorithmic FLOPs per launch."""
+    from matcha_hip import runtime as rt
+    g, gen = _gen("bf16", True)
+    mel = t(g["mel"], DEV)
+    gen(mel)
+    rt.probe_start(rt.PROBE_RBFUSE_C64, 8)
+    for _ in range(3):
+        gen(mel)
+    p = rt.probe_stop()
+    B, T = mel.shape[0], mel.shape[2]
+    assert p["launches"] == 3 and p["ms"] > 0
+    assert p["flops"] == 3 * 2.0 * 6 * 64 * 64 * (3 + 7 + 11) * B * 128 * T
+    # disarmed after stop: no further recording
+    gen(mel)
+    rt.probe_start(rt.PROBE_RBFUSE_C32, 1)
+    assert rt.probe_stop()["launches"] == 0

@@ -10,7 +10,7 @@ shapes = [  # (name, C, k, d, frames)
     ("s2_k3d1", 128, 3, 1, 32 * 64 * 728),
     ("s1_k7d3", 256, 7, 3, 32 * 8 * 728),
 ]
-variants = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 2, 3, 4, 5, 6]
+variants = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else list(range(11))
 reps, rounds = 5, 3
 res = {}
 for name, C, k, d, L in shapes:
