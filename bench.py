@@ -79,11 +79,25 @@ def build_models(device, precision, seed):
     return m, g, den, {k: torch.from_numpy(v) for k, v in sd.items()}, dict(g.state_dict())
 
 
-def shard_inputs(rank, batch, seed):
-    """Rank r gets utterances [r*batch, (r+1)*batch) of one global synthetic set."""
+def shard_inputs(rank, world, batch, seed):
+    """Rank r gets utterances [r*batch, (r+1)*batch) of one global synthetic set of world*batch
+    utterances (weak scaling: the per-GPU batch is fixed), cropped to the shard's longest text."""
     from matcha_hip import synthetic
-    x, xl = synthetic.synthetic_text(batch, seed=seed + 1000 * rank)
-    return torch.from_numpy(x), torch.from_numpy(xl)
+    x, xl = synthetic.synthetic_text(batch * world, seed=seed)
+    x, xl = x[rank * batch:(rank + 1) * batch], xl[rank * batch:(rank + 1) * batch]
+    x = x[:, : int(xl.max())]
+    return torch.from_numpy(np.ascontiguousarray(x)), torch.from_numpy(np.ascontiguousarray(xl))
+
+
+def reduce_over_ranks(elapsed, frames, dist, device):
+    """Job time = MAX of the ranks' timed regions; job work = SUM of their useful frames."""
+    if dist is None:
+        return elapsed, frames
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    f = torch.tensor([frames], dtype=torch.float64, device=device)
+    dist.all_reduce(f, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(f.item())
 
 
 def step(m, g, den, x, xl, n_ts, denoise):
@@ -168,7 +182,7 @@ def main():
     torch.manual_seed(a.seed + rank)
 
     m, g, den, msd, gsd = build_models(device, a.precision, a.seed)
-    x_cpu, xl_cpu = shard_inputs(rank, a.batch, a.seed)
+    x_cpu, xl_cpu = shard_inputs(rank, world, a.batch, a.seed)
     x, xl = x_cpu.to(device), xl_cpu.to(device)
     denoise = not a.no_denoise
 
@@ -197,14 +211,7 @@ def main():
     el = time.perf_counter() - t0
     probe = rt.probe_stop()
 
-    tot_frames = frames
-    if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-        f = torch.tensor([frames], dtype=torch.float64, device=device)
-        dist.all_reduce(f, op=dist.ReduceOp.SUM)
-        tot_frames = int(f.item())
+    el, tot_frames = reduce_over_ranks(el, frames, dist, device)
 
     value = tot_frames * a.steps / el
     ms_per_step = el / a.steps * 1e3
