@@ -94,6 +94,11 @@ size_t mt_vocoder_packed_bytes(const mt_vocoder* v);
 /* fused ResBlock stages for the 32/64-channel stages in bf16 (default on; bit-identical to the
  * per-layer path, which 0 selects) */
 int mt_vocoder_set_fusion(mt_vocoder* v, int enable);
+/* LDS-DMA persistent convs (mt_vconv) for the wide (C % 128 == 0) bf16 ResBlock1 stages: inputs
+ * pre-activated by their producers, same rounding points as the generic per-layer path (default on;
+ * 0 selects the generic per-layer kernel). Replaces the same convs as mt_vocoder_forward
+ * (hifigan/models.py:90-97, 187-192). */
+int mt_vocoder_set_vconv(mt_vocoder* v, int enable);
 int mt_vocoder_pack(const mt_vocoder* v, const float* const* params, void* packed, void* stream);
 size_t mt_vocoder_workspace_bytes(const mt_vocoder* v, int B, int T);
 /* mel [B,80,T] fp32 -> wav [B,1,T*prod(up_rates)] fp32 */
@@ -138,6 +143,14 @@ int mt_op_conv1d(int dtype, const void* x, int B, int Tin, int cin, const float*
 int mt_op_conv1d_tile(int variant, int dtype, const void* x, int B, int Tin, int cin, const float* W,
                       const float* bias, int cout, int k, int stride, int pad, int dil, int transposed,
                       float slope, void* y, int Tout, void* ws, size_t ws_bytes, void* stream);
+/* Op-level entry of mt_vconv (tests / A-B timing): bf16 x [B][L][cin] already activated, fp32
+ * W [cout][cin][k], bias [cout], padding dil*(k-1)/2 ("same"), epilogue flags ef: 1 + resid,
+ * 2 accumulate into y, 4 / div, 8 y = lrelu(v), 16 also y2 = lrelu(v). One ResBlock1 conv of
+ * hifigan/models.py:90-97. */
+size_t mt_op_vconv_workspace_bytes(int cin, int cout, int k);
+int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const float* bias, int cout, int k, int dil,
+                int ef, const void* resid, void* y, void* y2, float slope, float div, void* ws, size_t ws_bytes,
+                void* stream);
 /* qkv [B][T][3*heads*64], mask [B][T] -> out [B][T][heads*64], reference mask semantics */
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                     void* stream);
@@ -146,11 +159,12 @@ int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, in
  * Launch probe (measurement only; no reference counterpart). Arms HIP events around every
  * launch of one kernel site, on the stream the kernel is launched on, so a benchmark can time
  * that kernel inside its own timed region. Sites: 1 = fused 64-channel HiFi-GAN ResBlock stage,
- * 2 = fused 32-channel stage. mt_probe_stop synchronizes the recorded events and returns the
+ * 2 = fused 32-channel stage, 3 = every mt_vconv launch (ResBlock convs of the wide stages). mt_probe_stop synchronizes the recorded events and returns the
  * number of launches, their summed duration and the algorithmic FLOPs / bytes they did.
  * ------------------------------------------------------------------------------------- */
 #define MT_PROBE_RBFUSE_C64 1
 #define MT_PROBE_RBFUSE_C32 2
+#define MT_PROBE_VCONV 3
 int mt_probe_start(int site, int max_launches);
 int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes);
 

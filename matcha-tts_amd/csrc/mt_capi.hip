@@ -5,6 +5,7 @@
 
 #include "../../include/matcha_hip.h"
 #include "mt_model.h"
+#include "mt_vconv.h"
 #include "mt_probe.h"
 
 namespace mt {
@@ -128,6 +129,11 @@ int mt_vocoder_set_fusion(mt_vocoder* v, int enable) {
   v->v.fuse = enable ? 1 : 0;
   return 0;
 }
+int mt_vocoder_set_vconv(mt_vocoder* v, int enable) {
+  MT_REQUIRE(v, "null vocoder");
+  v->v.vconv = enable ? 1 : 0;
+  return 0;
+}
 size_t mt_vocoder_packed_bytes(const mt_vocoder* v) { return v ? v->v.packed_bytes : 0; }
 int mt_vocoder_pack(const mt_vocoder* v, const float* const* params, void* packed, void* stream) {
   MT_REQUIRE(v && params && packed, "vocoder_pack: null argument");
@@ -209,6 +215,50 @@ int mt_op_conv1d(int dtype, const void* x, int B, int Tin, int cin, const float*
                  void* ws, size_t ws_bytes, void* stream) {
   return mt_op_conv1d_tile(-1, dtype, x, B, Tin, cin, W, bias, cout, k, stride, pad, dil, transposed, slope, y,
                            Tout, ws, ws_bytes, stream);
+}
+size_t mt_op_vconv_workspace_bytes(int cin, int cout, int k) {
+  mt::Packer pk;
+  mt::GemmW g = mt::make_conv(cout, cin, k, 1, 0, 1, {0}, 1, 2, pk);
+  pk.take(mt::vconv_packed_bytes(cin, cout, k));
+  pk.take(256);
+  (void)g;
+  return pk.off;
+}
+int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const float* bias, int cout, int k, int dil,
+                int ef, const void* resid, void* y, void* y2, float slope, float div, void* ws, size_t ws_bytes,
+                void* stream) {
+  MT_REQUIRE(x && W && bias && y && ws, "op_vconv: null argument");
+  MT_REQUIRE(mt::vconv_supported(cin, cout, k, dil, 1), "op_vconv: unsupported conv %dx%d k%d d%d", cin, cout, k, dil);
+  hipStream_t st = (hipStream_t)stream;
+  mt::Packer pk;
+  mt::GemmW g = mt::make_conv(cout, cin, k, 1, dil * (k - 1) / 2, dil, {0}, 1, 2, pk);
+  const size_t v_off = pk.take(mt::vconv_packed_bytes(cin, cout, k));
+  const size_t z_off = pk.take(256);
+  MT_REQUIRE(ws_bytes >= pk.off, "op_vconv: workspace %zu < %zu", ws_bytes, pk.off);
+  const float* params[2] = {W, bias};
+  char* P = (char*)ws;
+  int rc = mt::pack_gemm(g, MT_DTYPE_BF16, params, P, st);
+  if (rc) return rc;
+  if ((rc = mt::vconv_repack(P + g.w_off, g.Mpad, g.taps, g.cin_pad, cin, cout, P + v_off, st))) return rc;
+  if ((rc = mt::pack_vec(nullptr, 1, 64, 0, (float*)(P + z_off), st))) return rc;
+  mt::VConvArgs a{};
+  a.x = (const mt::bf16*)x;
+  a.B = B;
+  a.L = L;
+  a.cin = cin;
+  a.w = (const mt::bf16*)(P + v_off);
+  a.bias = (const float*)(P + g.b_off);
+  a.M = a.Mpad = cout;
+  a.taps = k;
+  a.dil = dil;
+  a.pad = g.pad;
+  a.y = (mt::bf16*)y;
+  a.y2 = (mt::bf16*)y2;
+  a.resid = (const mt::bf16*)resid;
+  a.slope = slope;
+  a.div = div;
+  a.zero = (const mt::bf16*)(P + z_off);
+  return mt::launch_vconv(ef, a, st);
 }
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                     void* stream) {

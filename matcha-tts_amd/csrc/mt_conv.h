@@ -32,6 +32,7 @@ enum : int {
   EF_TANH = 128,   // tanh(v)
   EF_EULER = 256,  // Euler/midpoint update of z (fp32 master) + estimator-input slot
   EF_OUTF32 = 512, // store fp32 whatever the element type
+  EF_DUAL = 1024,  // also store y2 = lrelu(round(v), slope): the activated copy a pre-activated consumer reads
 };
 
 struct ConvArgs {
@@ -47,6 +48,7 @@ struct ConvArgs {
   int Ncols, ups, opad, Tout;
   void* y;
   int ldy;
+  void* y2;             // EF_DUAL: [B][Tout][ldy]
   // prologue params
   const float* pmask;   // [B][Tin]
   float slope;

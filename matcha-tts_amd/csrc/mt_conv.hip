@@ -407,6 +407,12 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
               if (ok[r]) yp[r] = (bf16)v[r];
           }
         }
+        if constexpr ((EF & EF_DUAL) != 0) {
+          E* y2p = reinterpret_cast<E*>(a.y2) + orow * a.ldy + ch;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (ok[r]) y2p[r] = from_f<E>(lrelu_f(to_f(from_f<E>(v[r])), a.slope));
+        }
       }
     }
   }
@@ -499,6 +505,7 @@ static int check_args(const ConvArgs& a, int esize, int pf, int ef) {
              a.cout);
   MT_REQUIRE(a.taps >= 1 && a.dil >= 1 && a.stride >= 1 && a.ups >= 1, "conv: taps/dil/stride");
   MT_REQUIRE(a.x0 && a.w && a.bias && (a.y || (ef & EF_EULER)), "conv: null pointer");
+  MT_REQUIRE(!(ef & EF_DUAL) || a.y2, "conv: y2 missing");
   MT_REQUIRE(a.c0 == a.cin || a.x1, "conv: second source missing");
   if (pf & PF_LN) MT_REQUIRE(a.taps == 1 && a.stride == 1 && a.pad == 0 && a.ln_stats,
                              "conv: LN prologue needs a 1x1 GEMM and row statistics");
@@ -554,7 +561,8 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
   X(PF_LRELU, EF_RESID | EF_ACCUM | EF_DIV,                                            \
     CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32)                                \
   X(PF_LRELU, EF_RESID | EF_DIV, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32)   \
-  X(PF_LRELU, EF_TANH | EF_OUTF32, CFG_16 | CFG_32)
+  X(PF_LRELU, EF_TANH | EF_OUTF32, CFG_16 | CFG_32)                                     \
+  X(PF_LRELU, EF_DUAL, CFG_BIG | CFG_SMALLN)
 
 #define MT_DEFINE_LAUNCH(PFV, EFV, CFGV)                                                    \
   template <>                                                                             \

@@ -39,6 +39,8 @@ struct GemmW {
   int bsrc = -1;          // bias param or -1 (zeros)
   int ln_g = -1, ln_b = -1;  // LayerNorm (on the input channels) folded into W and bias
   size_t w_off = 0, b_off = 0;
+  size_t v_off = 0;  // vconv image [cin/64][taps][Mpad128][64] (bf16 HiFi-GAN convs, mt_vconv.h)
+  bool vc = false;
 };
 
 GemmW make_conv(int cout, int cin, int k, int stride, int pad, int dil, std::vector<int> w, int b,
@@ -119,6 +121,9 @@ struct Decoder {
 struct Vocoder {
   int resblock = 1, dtype = BF16, esize = 2;
   int fuse = 1;  // fused ResBlock stages (mt_rbfuse) where supported
+  int vconv = 1; // LDS-DMA persistent convs (mt_vconv) for the wide bf16 ResBlock stages
+  size_t zero_off = 0;  // 256 zero bytes in the packed buffer (vconv padding rows)
+  bool any_vc = false;
   std::vector<int> up_rates, up_kernels, rb_kernels;
   std::vector<std::vector<int>> rb_dils;
   int up_init = 512, n_mels = 80;
@@ -132,12 +137,15 @@ struct Vocoder {
   int init(int resblock, const std::vector<int>& up_rates, const std::vector<int>& up_kernels, int up_init,
            const std::vector<int>& rb_kernels, const std::vector<std::vector<int>>& rb_dils, int dtype);
   int pack(const float* const* p, void* packed, hipStream_t st) const;
+  bool stage_vc(int i) const;  // stage i runs its ResBlock convs through mt_vconv
   size_t frame_elems() const;  // max over stages of (samples per mel frame) x channels
   size_t workspace_bytes(int B, int T) const;
   int forward(const void* packed, const float* mel, int B, int T, float* wav, void* ws, size_t ws_bytes,
               hipStream_t st) const;
   template <class E>
   int forward_t(const char* P, const float* mel, int B, int T, float* wav, char* ws, hipStream_t st) const;
+  int stage_vconv(const char* P, int i, int B, int L, const char* X, const char* XA, char* XS, char* Tb, char* R,
+                  char* RA, hipStream_t st) const;
 };
 
 }  // namespace mt

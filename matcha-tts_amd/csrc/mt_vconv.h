@@ -1,0 +1,40 @@
+// Persistent LDS-DMA implicit-GEMM Conv1d for the wide HiFi-GAN stages (bf16, C_out % 128 == 0,
+// C_in % 64 == 0, stride 1): the resblock convs of stages 1 and 2 (hifigan/models.py:90-97), which
+// dominate the vocoder's MFMA work. Inputs arrive PRE-ACTIVATED (the producer's epilogue wrote
+// lrelu(x) next to x), so every operand byte goes global -> LDS by `global_load_lds_dwordx4` with no
+// VGPR round trip and no prologue transform (see mt_vconv.hip for the pipeline).
+#pragma once
+#include "mt_common.h"
+
+namespace mt {
+
+// epilogue flags: v = acc + bias, then in this order
+enum : int {
+  VE_RESID = 1,  // v += resid                        (ResBlock1 `xt + x`, models.py:96)
+  VE_ACCUM = 2,  // v = y_old + v                     (`xs += ...`, models.py:189-192)
+  VE_DIV = 4,    // v = v / div                       (`xs / num_kernels`, models.py:193)
+  VE_ACT = 8,    // y = lrelu(round(v))               (conv1: only lrelu(xt) is ever consumed)
+  VE_DUAL = 16,  // y = round(v), y2 = lrelu(round(v)) (chain state + the next conv1's input)
+};
+
+struct VConvArgs {
+  const bf16* x;      // [B][L][cin], already activated
+  int B, L, cin;
+  const bf16* w;      // [cin/64][taps][Mpad][64]
+  const float* bias;  // [M]
+  int M, Mpad, taps, dil, pad;
+  bf16* y;            // [B][L][M]
+  bf16* y2;           // [B][L][M] (VE_DUAL)
+  const bf16* resid;  // [B][L][M] (VE_RESID)
+  float div, slope;
+  const bf16* zero;   // >= 128 zero bytes: source of the conv's zero padding rows
+};
+
+bool vconv_supported(int cin, int cout, int k, int dil, int stride);
+// packed bytes of the [cin/64][taps][Mpad][64] image
+size_t vconv_packed_bytes(int cin, int cout, int k);
+// [Mpad0][taps][cin_pad] (pack_conv layout, bf16) -> [cin/64][taps][Mpad][64]
+int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st);
+int launch_vconv(int ef, const VConvArgs& a, hipStream_t st);
+
+}  // namespace mt

@@ -8,9 +8,11 @@
 // Buffers (each B x T x frame_elems elements): XS (stage input / resblock sum), X (upsampled),
 // Tb (first conv of a pair), R (resblock chain state, updated in place).
 #include <algorithm>
+#include <type_traits>
 
 #include "mt_model.h"
 #include "mt_rbfuse.h"
+#include "mt_vconv.h"
 
 namespace mt {
 
@@ -81,6 +83,28 @@ int Vocoder::init(int resblock_, const std::vector<int>& ur, const std::vector<i
       rb2.push_back(v2);
     }
   }
+  // wide bf16 ResBlock1 stages: every conv of the stage through mt_vconv (its own weight image)
+  any_vc = false;
+  if (dtype == BF16 && resblock == 1) {
+    for (size_t i = 0; i < ur.size(); ++i) {
+      bool ok = true;
+      for (int j = 0; j < nk; ++j)
+        for (size_t q = 0; q < rb1[i * nk + j].size(); ++q) {
+          const GemmW& a = rb1[i * nk + j][q];
+          const GemmW& b = rb2[i * nk + j][q];
+          ok = ok && vconv_supported(a.cin, a.cout, a.k, a.dil, a.s) && vconv_supported(b.cin, b.cout, b.k, b.dil, b.s);
+        }
+      if (!ok) continue;
+      for (int j = 0; j < nk; ++j)
+        for (auto* v : {&rb1[i * nk + j], &rb2[i * nk + j]})
+          for (GemmW& g : *v) {
+            g.vc = true;
+            g.v_off = pk.take(vconv_packed_bytes(g.cin, g.cout, g.k));
+          }
+      any_vc = true;
+    }
+    if (any_vc) zero_off = pk.take(256);
+  }
   {
     int w = L.add("conv_post.weight", {1, ch, 7});
     int b = L.add("conv_post.bias", {1});
@@ -101,7 +125,12 @@ int Vocoder::pack(const float* const* p, void* packed, hipStream_t st) const {
       if ((rc = pack_gemm(g, dtype, p, P, st))) return rc;
     for (const GemmW& g : rb2[i])
       if ((rc = pack_gemm(g, dtype, p, P, st))) return rc;
+    for (auto* v : {&rb1[i], &rb2[i]})
+      for (const GemmW& g : *v)
+        if (g.vc && (rc = vconv_repack(P + g.w_off, g.Mpad, g.taps, g.cin_pad, g.cin, g.cout, P + g.v_off, st)))
+          return rc;
   }
+  if (any_vc && (rc = pack_vec(nullptr, 1, 64, 0, (float*)(P + zero_off), st))) return rc;
   return pack_gemm(post, dtype, p, P, st);
 }
 
@@ -115,9 +144,77 @@ size_t Vocoder::frame_elems() const {
   return m;
 }
 
+bool Vocoder::stage_vc(int i) const {
+  const int nk = (int)rb_kernels.size();
+  return vconv && dtype == BF16 && resblock == 1 && !rb1[(size_t)i * nk].empty() && rb1[(size_t)i * nk][0].vc;
+}
+
 size_t Vocoder::workspace_bytes(int B, int T) const {
   const size_t big = align256((size_t)B * T * frame_elems() * esize);
-  return 4 * big + align256((size_t)B * T * n_mels * esize);
+  // + XA, RA: the activated copies the vconv stages read
+  return (any_vc ? 6 : 4) * big + align256((size_t)B * T * n_mels * esize);
+}
+
+// One wide ResBlock1 stage through mt_vconv (bf16). Per resblock j, pair q (models.py:90-97):
+//   Tb = lrelu(conv1(stateA))                         (VE_ACT: conv2 only ever reads lrelu(xt))
+//   R, RA = conv2(Tb) + state, lrelu(.)               (VE_DUAL, pairs before the last)
+//   XS (+)= conv2(Tb) + state (/ nk on the last resblock)  (last pair)
+// Rounding points equal the generic per-layer path's: every stored tensor is rounded to bf16 and the
+// activated copies are lrelu of the rounded values.
+int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, const char* XA, char* XS, char* Tb,
+                         char* R, char* RA, hipStream_t st) const {
+  const int nk = (int)rb_kernels.size();
+  const bf16* zero = (const bf16*)(P + zero_off);
+  int rc;
+  for (int j = 0; j < nk; ++j) {
+    const std::vector<GemmW>& c1 = rb1[(size_t)i * nk + j];
+    const std::vector<GemmW>& c2 = rb2[(size_t)i * nk + j];
+    const int np = (int)c1.size();
+    const char* state = X;
+    const char* stateA = XA;
+    for (int q = 0; q < np; ++q) {
+      const bool last = q == np - 1;
+      VConvArgs a{};
+      a.x = (const bf16*)stateA;
+      a.B = B;
+      a.L = L;
+      a.cin = c1[q].cin;
+      a.w = (const bf16*)(P + c1[q].v_off);
+      a.bias = (const float*)(P + c1[q].b_off);
+      a.M = a.Mpad = c1[q].cout;
+      a.taps = c1[q].k;
+      a.dil = c1[q].dil;
+      a.pad = c1[q].pad;
+      a.y = (bf16*)Tb;
+      a.slope = 0.1f;
+      a.div = 1.f;
+      a.zero = zero;
+      if ((rc = launch_vconv(VE_ACT, a, st))) return rc;
+      VConvArgs b = a;
+      b.x = (const bf16*)Tb;
+      b.w = (const bf16*)(P + c2[q].v_off);
+      b.bias = (const float*)(P + c2[q].b_off);
+      b.taps = c2[q].k;
+      b.dil = c2[q].dil;
+      b.pad = c2[q].pad;
+      b.resid = (const bf16*)state;
+      b.div = (float)nk;
+      int ef = VE_RESID;
+      if (!last) {
+        b.y = (bf16*)R;
+        b.y2 = (bf16*)RA;
+        ef |= VE_DUAL;
+        state = R;
+        stateA = RA;
+      } else {
+        b.y = (bf16*)XS;
+        if (j > 0) ef |= VE_ACCUM;
+        if (j == nk - 1) ef |= VE_DIV;
+      }
+      if ((rc = launch_vconv(ef, b, st))) return rc;
+    }
+  }
+  return 0;
 }
 
 template <class E>
@@ -130,6 +227,8 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
   char* Tb = ws + 2 * big;
   char* R = ws + 3 * big;
   char* xm = ws + 4 * big;
+  char* XA = ws + 4 * big + align256((size_t)B * T * n_mels * esize);
+  char* RA = XA + big;
   if ((rc = bct_to_btc(dtype, mel, B, n_mels, T, 1.f, xm, n_mels, 0, st))) return rc;
   {
     ConvArgs a = gemm_args(pre, P, B, T);
@@ -144,9 +243,19 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     u.x0 = XS;
     u.y = X;
     u.slope = 0.1f;
+    const int C = ups[i].cout;
+    if constexpr (std::is_same<E, bf16>::value) {
+      if (stage_vc((int)i)) {
+        // X and XA = lrelu(X): the three resblocks' first convs read XA, their residual X
+        u.y2 = XA;
+        if ((rc = launch_conv<E, PF_LRELU, EF_DUAL>(u, st))) return rc;
+        L = u.Tout;
+        if ((rc = stage_vconv(P, (int)i, B, L, X, XA, XS, Tb, R, RA, st))) return rc;
+        continue;
+      }
+    }
     if ((rc = launch_conv<E, PF_LRELU, 0>(u, st))) return rc;
     L = u.Tout;
-    const int C = ups[i].cout;
     bool uniform = true;
     for (const auto& dl : rb_dils) uniform = uniform && dl.size() == rb_dils[0].size();
     if (fuse && resblock == 1 && nk <= 3 && rbfuse_supported(dtype, C) && uniform && rb_dils[0].size() <= 3) {

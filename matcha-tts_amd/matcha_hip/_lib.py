@@ -43,6 +43,7 @@ SIGNATURES = {
     "mt_vocoder_param_shape": (c_int, [P, c_int, POINTER(c_int64), c_int]),
     "mt_vocoder_packed_bytes": (c_size_t, [P]),
     "mt_vocoder_set_fusion": (c_int, [P, c_int]),
+    "mt_vocoder_set_vconv": (c_int, [P, c_int]),
     "mt_vocoder_pack": (c_int, [P, POINTER(c_void_p), P, P]),
     "mt_vocoder_workspace_bytes": (c_size_t, [P, c_int, c_int]),
     "mt_vocoder_forward": (c_int, [P, P, P, c_int, c_int, P, P, c_size_t, P]),
@@ -57,6 +58,9 @@ SIGNATURES = {
                              c_int, c_float, P, c_int, P, c_size_t, P]),
     "mt_op_conv1d_tile": (c_int, [c_int, c_int, P, c_int, c_int, c_int, P, P, c_int, c_int, c_int, c_int, c_int,
                                   c_int, c_float, P, c_int, P, c_size_t, P]),
+    "mt_op_vconv_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mt_op_vconv": (c_int, [P, c_int, c_int, c_int, P, P, c_int, c_int, c_int, c_int, P, P, P, c_float, c_float, P,
+                            c_size_t, P]),
     "mt_op_attention": (c_int, [c_int, P, P, P, c_int, c_int, c_int, P]),
     "mt_probe_start": (c_int, [c_int, c_int]),
     "mt_probe_stop": (c_int, [P, P, P, P]),

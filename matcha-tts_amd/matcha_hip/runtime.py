@@ -184,6 +184,9 @@ class VocoderEngine:
     def set_fusion(self, enable: bool) -> None:
         check(lib().mt_vocoder_set_fusion(self.h, int(bool(enable))), "vocoder_set_fusion")
 
+    def set_vconv(self, enable: bool) -> None:
+        check(lib().mt_vocoder_set_vconv(self.h, int(bool(enable))), "vocoder_set_vconv")
+
     def __del__(self):
         try:
             if getattr(self, "h", None):
@@ -311,6 +314,32 @@ def op_conv1d(x_btc: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor]
                               int(transposed), -1.0 if slope is None else float(slope), ptr(y), tout, ws.data_ptr(),
                               ws.numel(), stream_handle(x.device)), "op_conv1d")
     return y
+
+
+def op_vconv(x_btc: torch.Tensor, W: torch.Tensor, bias: torch.Tensor, dil: int = 1, ef: int = 0,
+             resid: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None,
+             slope: float = 0.1, div: float = 1.0, ws: Optional[torch.Tensor] = None):
+    """Op-level test entry of mt_vconv: one "same"-padded bf16 Conv1d on an already activated
+    [B,L,C] input with the ResBlock epilogues (ef bits: 1 resid, 2 accumulate into y, 4 /div,
+    8 y=lrelu(v), 16 also y2=lrelu(v)). Returns (y, y2)."""
+    require_gpu(x_btc, what="op_vconv")
+    x = x_btc.to(torch.bfloat16).contiguous()
+    B, L, cin = x.shape
+    cout, k = W.shape[0], W.shape[2]
+    if y is None:
+        y = torch.empty((B, L, cout), dtype=torch.bfloat16, device=x.device)
+    if (ef & 16) and y2 is None:
+        y2 = torch.empty((B, L, cout), dtype=torch.bfloat16, device=x.device)
+    if resid is not None:
+        resid = resid.to(torch.bfloat16).contiguous()
+    L_ = lib()
+    nb = L_.mt_op_vconv_workspace_bytes(cin, cout, k)
+    if ws is None or ws.numel() < nb:
+        ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
+    W, bias = f32c(W), f32c(bias)
+    check(L_.mt_op_vconv(ptr(x), B, L, cin, ptr(W), ptr(bias), cout, k, dil, int(ef), ptr(resid), ptr(y), ptr(y2),
+                         float(slope), float(div), ws.data_ptr(), ws.numel(), stream_handle(x.device)), "op_vconv")
+    return y, y2
 
 
 def op_attention(qkv: torch.Tensor, mask: torch.Tensor, heads: int, precision="fp32") -> torch.Tensor:

@@ -103,3 +103,46 @@ def test_attention_reference_mask_semantics(precision, T, lens):
     for b, L in enumerate(lens):
         if L < T:
             assert torch.allclose(out[b, 0], out[b, -1], atol=1e-6)
+
+
+VCONV_CASES = [
+    # cin, cout, k, dil, B, L, ef   (ef bits: 1 resid, 2 accumulate, 4 /div, 8 y=lrelu(v), 16 y2=lrelu(v))
+    (128, 128, 11, 5, 2, 300, 1 | 16),     # stage-2 conv2 of a non-last pair: x + conv, and its lrelu copy
+    (128, 128, 3, 1, 1, 1000, 8),          # stage-2 conv1: only lrelu(conv) is stored
+    (256, 256, 7, 3, 2, 517, 1 | 2 | 4),   # stage-1 last pair of the last resblock: (xs + x + conv) / 3
+    (128, 128, 7, 1, 3, 100, 1),           # shorter than one 256-frame tile, 3 utterances
+    (256, 128, 3, 5, 2, 256, 1 | 2),       # exact tile multiple, accumulate
+    (128, 256, 11, 1, 1, 40, 0),           # more padding than frames
+]
+
+
+@pytest.mark.parametrize("case", VCONV_CASES, ids=lambda c: f"{c[0]}x{c[1]}k{c[2]}d{c[3]}B{c[4]}L{c[5]}ef{c[6]}")
+def test_vconv_lds_dma_conv(case):
+    """mt_vconv (persistent LDS-DMA conv, bf16) against an fp64 CPU conv of the same bf16 operands:
+    y = epilogue(conv1d(x, W, 'same' padding, dilation) + b). rel-RMS <= 4e-3 (bf16 output rounding)."""
+    from matcha_hip import runtime as rt
+    cin, cout, k, dil, B, L, ef = case
+    g = torch.Generator().manual_seed(cin + 3 * cout + k * 11 + dil + B + L)
+    x = torch.randn(B, L, cin, generator=g).bfloat16()
+    W = (torch.randn(cout, cin, k, generator=g) / math.sqrt(cin * k)).bfloat16().float()
+    b = 0.1 * torch.randn(cout, generator=g)
+    resid = torch.randn(B, L, cout, generator=g).bfloat16()
+    y0 = torch.randn(B, L, cout, generator=g).bfloat16()
+    y = y0.cuda().clone()
+    out, out2 = rt.op_vconv(x.cuda(), W.cuda(), b.cuda(), dil, ef, resid.cuda() if ef & 1 else None, y=y,
+                            slope=0.1, div=3.0)
+    torch.cuda.synchronize()
+    v = F.conv1d(x.double().permute(0, 2, 1), W.double(), b.double(), padding=dil * (k - 1) // 2,
+                 dilation=dil).permute(0, 2, 1)
+    if ef & 1:
+        v = v + resid.double()
+    if ef & 2:
+        v = y0.double() + v
+    if ef & 4:
+        v = v / 3.0
+    ref = F.leaky_relu(v, 0.1) if ef & 8 else v
+    assert rel_rms(out.double().cpu(), ref) <= 4e-3
+    if ef & 16:
+        assert rel_rms(out2.double().cpu(), F.leaky_relu(v, 0.1)) <= 4e-3
+        # the activated copy is lrelu of the stored (rounded) value, exactly
+        assert torch.equal(out2.cpu(), F.leaky_relu(out.float().cpu(), 0.1).bfloat16())

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""In-process A/B of the bf16 vocoder: mt_vconv wide stages on vs the generic per-layer kernel
+(interleaved rounds, one process, random-data mel). Usage: python tools_voc_ab.py [B] [T] [rounds]"""
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "matcha-tts_amd"))
+import torch  # noqa: E402
+
+from hifigan.config import v1  # noqa: E402
+from hifigan.env import AttrDict  # noqa: E402
+from hifigan.models import Generator  # noqa: E402
+from matcha_hip import synthetic  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+T = int(sys.argv[2]) if len(sys.argv) > 2 else 728
+R = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+g = Generator(AttrDict(v1), precision="bf16")
+sd = synthetic.make_state_dict([(k, tuple(v.shape)) for k, v in g.state_dict().items()], 7)
+g.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+g = g.cuda().eval()
+g.remove_weight_norm()
+mel = (torch.randn(B, 80, T) * 2 - 5).cuda()
+eng = g.engine()
+res = {True: [], False: []}
+for r in range(R + 1):
+    for on in (True, False):
+        eng.set_vconv(on)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        wav = g(mel)
+        torch.cuda.synchronize()
+        if r > 0:
+            res[on].append((time.perf_counter() - t0) * 1e3)
+for on in (True, False):
+    v = sorted(res[on])
+    print(f"vocoder B={B} T={T} vconv={on}: median {v[len(v)//2]:.2f} ms min {v[0]:.2f} ms", flush=True)
