@@ -221,12 +221,13 @@ size_t mt_op_vconv_workspace_bytes(int cin, int cout, int k) {
   mt::GemmW g = mt::make_conv(cout, cin, k, 1, 0, 1, {0}, 1, 2, pk);
   pk.take(mt::vconv_packed_bytes(cin, cout, k));
   pk.take(256);
+  pk.take(4096);
   (void)g;
   return pk.off;
 }
 int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const float* bias, int cout, int k, int dil,
-                int ef, const void* resid, void* y, void* y2, float slope, float div, void* ws, size_t ws_bytes,
-                void* stream) {
+                int ef, const void* resid, void* y, void* y2, float slope, float div, int pack, void* ws,
+                size_t ws_bytes, void* stream) {
   MT_REQUIRE(x && W && bias && y && ws, "op_vconv: null argument");
   MT_REQUIRE(mt::vconv_supported(cin, cout, k, dil, 1), "op_vconv: unsupported conv %dx%d k%d d%d", cin, cout, k, dil);
   hipStream_t st = (hipStream_t)stream;
@@ -234,13 +235,16 @@ int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const floa
   mt::GemmW g = mt::make_conv(cout, cin, k, 1, dil * (k - 1) / 2, dil, {0}, 1, 2, pk);
   const size_t v_off = pk.take(mt::vconv_packed_bytes(cin, cout, k));
   const size_t z_off = pk.take(256);
+  const size_t t_off = pk.take(4096);
   MT_REQUIRE(ws_bytes >= pk.off, "op_vconv: workspace %zu < %zu", ws_bytes, pk.off);
   const float* params[2] = {W, bias};
   char* P = (char*)ws;
-  int rc = mt::pack_gemm(g, MT_DTYPE_BF16, params, P, st);
-  if (rc) return rc;
-  if ((rc = mt::vconv_repack(P + g.w_off, g.Mpad, g.taps, g.cin_pad, cin, cout, P + v_off, st))) return rc;
-  if ((rc = mt::pack_vec(nullptr, 1, 64, 0, (float*)(P + z_off), st))) return rc;
+  int rc;
+  if (pack) {
+    if ((rc = mt::pack_gemm(g, MT_DTYPE_BF16, params, P, st))) return rc;
+    if ((rc = mt::vconv_repack(P + g.w_off, g.Mpad, g.taps, g.cin_pad, cin, cout, P + v_off, st))) return rc;
+    if ((rc = mt::pack_vec(nullptr, 1, 64, 0, (float*)(P + z_off), st))) return rc;
+  }
   mt::VConvArgs a{};
   a.x = (const mt::bf16*)x;
   a.B = B;
@@ -258,6 +262,7 @@ int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const floa
   a.slope = slope;
   a.div = div;
   a.zero = (const mt::bf16*)(P + z_off);
+  a.trash = (mt::bf16*)(P + t_off);
   return mt::launch_vconv(ef, a, st);
 }
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,

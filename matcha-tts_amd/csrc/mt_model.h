@@ -145,7 +145,7 @@ struct Vocoder {
   template <class E>
   int forward_t(const char* P, const float* mel, int B, int T, float* wav, char* ws, hipStream_t st) const;
   int stage_vconv(const char* P, int i, int B, int L, const char* X, const char* XA, char* XS, char* Tb, char* R,
-                  char* RA, hipStream_t st) const;
+                  char* RA, char* trash, hipStream_t st) const;
 };
 
 }  // namespace mt

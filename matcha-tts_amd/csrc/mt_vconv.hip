@@ -33,7 +33,9 @@ constexpr int WSLOT = BM * 128;                   // 16 KiB: 128 rows x 64 bf16 
 constexpr int NWSLOT = 4;                         // weight ring depth (3 steps in flight)
 constexpr int XROWS = 320;                        // >= BN + (taps - 1) * dil
 constexpr int XBUF = XROWS * 128;                 // 40 KiB per chunk buffer
-constexpr int LDS_BYTES = NWSLOT * WSLOT + 2 * XBUF;  // 144 KiB
+constexpr int MMAX = 512;                         // largest C_out (bias staged in LDS)
+constexpr int BIAS_OFF = NWSLOT * WSLOT + 2 * XBUF;
+constexpr int LDS_BYTES = BIAS_OFF + MMAX * 4;     // 146 KiB
 constexpr int NXW = XROWS / 8 / 8;                // X wave-instructions per wave per chunk
 constexpr int NWW = BM / 8 / 8;                   // W wave-instructions per wave per step
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -43,16 +45,74 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (n > 15 waits for 15: stricter, still correct)
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (n > 63 waits for 63: stricter, still correct)
 __device__ __forceinline__ void wait_vmcnt(int n) {
-#define MT_VMW(k) \
-  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
   switch (n) {
-    MT_VMW(0) MT_VMW(1) MT_VMW(2) MT_VMW(3) MT_VMW(4) MT_VMW(5) MT_VMW(6) MT_VMW(7)
-    MT_VMW(8) MT_VMW(9) MT_VMW(10) MT_VMW(11) MT_VMW(12) MT_VMW(13) MT_VMW(14)
-    default: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
+    case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+    case 23: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
+    case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
+    case 27: asm volatile("s_waitcnt vmcnt(27)" ::: "memory"); break;
+    case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 29: asm volatile("s_waitcnt vmcnt(29)" ::: "memory"); break;
+    case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+    case 31: asm volatile("s_waitcnt vmcnt(31)" ::: "memory"); break;
+    case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 33: asm volatile("s_waitcnt vmcnt(33)" ::: "memory"); break;
+    case 34: asm volatile("s_waitcnt vmcnt(34)" ::: "memory"); break;
+    case 35: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
+    case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+    case 37: asm volatile("s_waitcnt vmcnt(37)" ::: "memory"); break;
+    case 38: asm volatile("s_waitcnt vmcnt(38)" ::: "memory"); break;
+    case 39: asm volatile("s_waitcnt vmcnt(39)" ::: "memory"); break;
+    case 40: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+    case 41: asm volatile("s_waitcnt vmcnt(41)" ::: "memory"); break;
+    case 42: asm volatile("s_waitcnt vmcnt(42)" ::: "memory"); break;
+    case 43: asm volatile("s_waitcnt vmcnt(43)" ::: "memory"); break;
+    case 44: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
+    case 45: asm volatile("s_waitcnt vmcnt(45)" ::: "memory"); break;
+    case 46: asm volatile("s_waitcnt vmcnt(46)" ::: "memory"); break;
+    case 47: asm volatile("s_waitcnt vmcnt(47)" ::: "memory"); break;
+    case 48: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+    case 49: asm volatile("s_waitcnt vmcnt(49)" ::: "memory"); break;
+    case 50: asm volatile("s_waitcnt vmcnt(50)" ::: "memory"); break;
+    case 51: asm volatile("s_waitcnt vmcnt(51)" ::: "memory"); break;
+    case 52: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
+    case 53: asm volatile("s_waitcnt vmcnt(53)" ::: "memory"); break;
+    case 54: asm volatile("s_waitcnt vmcnt(54)" ::: "memory"); break;
+    case 55: asm volatile("s_waitcnt vmcnt(55)" ::: "memory"); break;
+    case 56: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+    case 57: asm volatile("s_waitcnt vmcnt(57)" ::: "memory"); break;
+    case 58: asm volatile("s_waitcnt vmcnt(58)" ::: "memory"); break;
+    case 59: asm volatile("s_waitcnt vmcnt(59)" ::: "memory"); break;
+    case 60: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
+    case 61: asm volatile("s_waitcnt vmcnt(61)" ::: "memory"); break;
+    case 62: asm volatile("s_waitcnt vmcnt(62)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
   }
-#undef MT_VMW
 }
 
 __device__ __forceinline__ void raw_barrier() {
@@ -79,6 +139,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
   const int Q = nmine * S;
   if (Q == 0) return;
+  // bias in LDS (one array with the staging images: a second __shared__ object costs vmcnt(0) waits)
+  for (int i = tid; i < a.M; i += NT) reinterpret_cast<float*>(smem + BIAS_OFF)[i] = a.bias[i];
+  __syncthreads();
 
   auto tile_of = [&](int ti, int& b, int& n0, int& m0) {
     const int tile = gl + ti * G;
@@ -89,9 +152,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   };
 
   const int lrow = lane >> 3, lp = lane & 7;
-  auto issue_w = [&](int ti, int c, int t, int slot) {
-    int b, n0, m0;
-    tile_of(ti, b, n0, m0);
+  // staging of one step's weights / one chunk's rows; (b, n0, m0) of the cursor's tile are kept
+  // decoded by the caller (no integer division per step)
+  auto issue_w = [&](int m0, int c, int t, int slot) {
     const bf16* base = a.w + ((size_t)(c * taps + t) * a.Mpad + m0) * 64;
     char* dst = smem + slot * WSLOT;
 #pragma unroll
@@ -102,10 +165,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       glds16(base + r * 64 + q * 8, dst + j * 1024);
     }
   };
-  auto issue_x = [&](int ti, int c, int buf) {
-    int b, n0, m0;
-    tile_of(ti, b, n0, m0);
-    const int R = BN + (taps - 1) * dil;
+  const int R = BN + (taps - 1) * dil;
+  auto issue_x = [&](int b, int n0, int c, int buf) {
     const int f0 = n0 - a.pad;
     const bf16* xb = a.x + (size_t)b * L * cin + c * 64;
     char* dst = smem + NWSLOT * WSLOT + buf * XBUF;
@@ -128,6 +189,28 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int g4 = lane >> 4, l16 = lane & 15;
+  // residual / accumulator values of the tile: loaded
+  // at the start of the tile's last step, consumed after its MFMAs
+  bf16x4 rv[4][4], yv[4][4];
+  auto epi_loads = [&](int ti) {
+    int b, n0, m0;
+    tile_of(ti, b, n0, m0);
+    const size_t rowbase = (size_t)b * L;
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) {
+      const int m = m0 + wm * 64 + fm * 16 + 4 * g4;
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) {
+        const int n = min(n0 + wn * 64 + fn * 16 + l16, L - 1);  // clamped: no per-block branch
+        const size_t o = (rowbase + n) * a.M + m;
+        if constexpr ((EF & VE_RESID) != 0) rv[fm][fn] = *reinterpret_cast<const bf16x4*>(a.resid + o);
+        if constexpr ((EF & VE_ACCUM) != 0) yv[fm][fn] = *reinterpret_cast<const bf16x4*>(a.y + o);
+      }
+    }
+  };
+  // Every lane stores (frames past L go to a trash line), so the store count per tile is a constant the
+  // vmcnt bookkeeping can add: NST younger VMEM operations the next steps' waits may leave in flight.
+  constexpr int NST = 16 * ((EF & VE_DUAL) ? 2 : 1);
   auto epilogue = [&](int ti) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
@@ -135,25 +218,19 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm) {
       const int m = m0 + wm * 64 + fm * 16 + 4 * g4;
-      if (m >= a.M) continue;
-      const f32x4 bias4 = *reinterpret_cast<const f32x4*>(a.bias + m);
+      const f32x4 bias4 = *reinterpret_cast<const f32x4*>(smem + BIAS_OFF + 4 * m);
 #pragma unroll
       for (int fn = 0; fn < 4; ++fn) {
-        const int n = n0 + wn * 64 + fn * 16 + l16;
-        if (n >= L) continue;
-        const size_t o = (rowbase + n) * a.M + m;
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[fm][fn][r] + bias4[r];
         if constexpr ((EF & VE_RESID) != 0) {
-          const bf16x4 rv = *reinterpret_cast<const bf16x4*>(a.resid + o);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = v[r] + (float)rv[r];
+          for (int r = 0; r < 4; ++r) v[r] = v[r] + (float)rv[fm][fn][r];
         }
         if constexpr ((EF & VE_ACCUM) != 0) {
-          const bf16x4 yv = *reinterpret_cast<const bf16x4*>(a.y + o);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (float)yv[r] + v[r];
+          for (int r = 0; r < 4; ++r) v[r] = (float)yv[fm][fn][r] + v[r];
         }
         if constexpr ((EF & VE_DIV) != 0) {
 #pragma unroll
@@ -162,112 +239,131 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
         bf16x4 o1, o2;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bf16 rv = (bf16)v[r];
-          const bf16 av = (bf16)lrelu_f((float)rv, a.slope);
-          o1[r] = (EF & VE_ACT) ? av : rv;
+          const bf16 rb = (bf16)v[r];
+          const bf16 av = (bf16)lrelu_f((float)rb, a.slope);
+          o1[r] = (EF & VE_ACT) ? av : rb;
           o2[r] = av;
         }
-        *reinterpret_cast<bf16x4*>(a.y + o) = o1;
-        if constexpr ((EF & VE_DUAL) != 0) *reinterpret_cast<bf16x4*>(a.y2 + o) = o2;
+        const int n = n0 + wn * 64 + fn * 16 + l16;
+        const bool ok = n < L;
+        const size_t o = (rowbase + n) * a.M + m;
+        bf16* p1 = ok ? a.y + o : a.trash + 4 * lane;
+        *reinterpret_cast<bf16x4*>(p1) = o1;
+        if constexpr ((EF & VE_DUAL) != 0) {
+          bf16* p2 = ok ? a.y2 + o : a.trash + 4 * lane;
+          *reinterpret_cast<bf16x4*>(p2) = o2;
+        }
       }
     }
   };
 
-  // ---- prologue: rows of chunk 0, weights of steps 0..2 ----
-  int issued = 0, mX = 0, mW0 = 0, mW1 = 0, mW2 = 0;
-  int xti = 0, xc = 0, xu = 0;  // next chunk to stage
-  int wti = 0, wc = 0, wt = 0, wq = 0;  // next weight step to stage
-  auto adv_x = [&]() {
-    if (++xc == nch) {
-      xc = 0;
-      ++xti;
-    }
-    ++xu;
-  };
-  auto adv_w = [&]() {
-    if (++wt == taps) {
-      wt = 0;
-      if (++wc == nch) {
-        wc = 0;
-        ++wti;
-      }
-    }
-    ++wq;
-  };
-  issue_x(0, 0, 0);
-  issued += NXW;
-  mX = issued;
-  adv_x();
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    int mk = issued;
+  // ---- staging cursors and DMA bookkeeping (all wave-uniform) ----
+  int issued = 0;                      // global_load_lds (+ epilogue store) instructions this wave issued
+  int mX = 0;                          // `issued` right after the latest chunk's rows
+  int xti = 0, xc = 0, xu = 0;         // next chunk to stage
+  int wti = 0, wc = 0, wt = 0, wq = 0; // next weight step to stage
+  int wb, wn0, wm0, xb_, xn0, xm0;  // decoded tiles of the weight / row cursors
+  tile_of(0, wb, wn0, wm0);
+  tile_of(0, xb_, xn0, xm0);
+  auto stage_w = [&]() -> int {
     if (wq < Q) {
-      issue_w(wti, wc, wt, wq & 3);
+      issue_w(wm0, wc, wt, wq & 3);
       issued += NWW;
-      mk = issued;
-      adv_w();
+      if (++wt == taps) {
+        wt = 0;
+        if (++wc == nch) {
+          wc = 0;
+          if (++wti < nmine) tile_of(wti, wb, wn0, wm0);
+        }
+      }
+      ++wq;
     }
-    if (i == 0) mW0 = mk;
-    else if (i == 1) mW1 = mk;
-    else mW2 = mk;
-  }
-
-  int ti = 0, c = 0, t = 0, u = 0;
-  for (int qq = 0; qq < Q; ++qq) {
-    // ---- wait for this step's weights (and, on a chunk's first tap, its rows); publish ----
-    const int need = t == 0 ? max(mW0, mX) : mW0;
-    wait_vmcnt(issued - need);
-    raw_barrier();
-    // ---- stage ahead: rows of the next chunk (on its predecessor's first tap), weights of step qq+3 ----
-    if (t == 0 && xti < nmine) {
-      issue_x(xti, xc, xu & 1);
+    return issued;
+  };
+  auto stage_x = [&]() {
+    if (xti < nmine) {
+      issue_x(xb_, xn0, xc, xu & 1);
       issued += NXW;
       mX = issued;
-      adv_x();
-    }
-    int mk = issued;
-    if (wq < Q) {
-      issue_w(wti, wc, wt, wq & 3);
-      issued += NWW;
-      mk = issued;
-      adv_w();
-    }
-    mW0 = mW1;
-    mW1 = mW2;
-    mW2 = mk;
-
-    // ---- MFMAs of step qq ----
-    const char* Ws = smem + (qq & 3) * WSLOT;
-    const char* Xs = smem + NWSLOT * WSLOT + (u & 1) * XBUF;
-    const int ha = (l16 >> 1) & 7;
-    const char* pa = Ws + (wm * 64 + l16) * 128;
-    const int rb0 = wn * 64 + l16 + t * dil;
-    const int hb = (rb0 >> 1) & 7;
-    const char* pb = Xs + rb0 * 128;
-    bf16x8 A[2][4], Bf[2][4];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int oa = ((ks * 4 + g4) ^ ha) * 16, ob = ((ks * 4 + g4) ^ hb) * 16;
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        A[ks][f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048 + oa);
-        Bf[ks][f] = *reinterpret_cast<const bf16x8*>(pb + f * 2048 + ob);
+      if (++xc == nch) {
+        xc = 0;
+        if (++xti < nmine) tile_of(xti, xb_, xn0, xm0);
       }
+      ++xu;
     }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < 4; ++fn) acc[fm][fn] = mfma16(A[ks][fm], Bf[ks][fn], acc[fm][fn]);
+  };
 
-    // ---- tile done: epilogue, reset ----
+  // Fragments of one K-slice (ks) of a step: 4 A (weights) + 4 B (frames) x 16 bytes per lane.
+  struct Frag {
+    bf16x8 A[4], B[4];
+  };
+  const int ha = (l16 >> 1) & 7;
+  auto read_frag = [&](Frag& F, int ks, int slot, int xbuf, int tap) {
+    const char* pa = smem + slot * WSLOT + (wm * 64 + l16) * 128;
+    const int rb0 = wn * 64 + l16 + tap * dil;
+    const int hb = (rb0 >> 1) & 7;
+    const char* pb = smem + NWSLOT * WSLOT + xbuf * XBUF + rb0 * 128;
+    const int oa = ((ks * 4 + g4) ^ ha) * 16, ob = ((ks * 4 + g4) ^ hb) * 16;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048 + oa);
+      F.B[f] = *reinterpret_cast<const bf16x8*>(pb + f * 2048 + ob);
+    }
+  };
+  // 16 MFMAs of one K-slice with the 8 reads of another slice interleaved, one per MFMA issue slot
+  auto mma_slice = [&](const Frag& F) {
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+  };
+
+  // ---- prologue: rows of chunk 0, weights of steps 0..2, K-slice 0 of step 0 ----
+  stage_x();
+  const int m0w = stage_w();
+  int mWa = stage_w();  // `issued` after the weights of step qq+1
+  int mWb = stage_w();  // ... of step qq+2
+  wait_vmcnt(issued - max(m0w, mX));
+  raw_barrier();
+  Frag F0, F1;  // F0: slice 0 of the step being computed (read one step ahead), F1: its slice 1
+  read_frag(F0, 0, 0, 0, 0);
+
+  int ti = 0, c = 0, t = 0, u = 0;  // step qq
+  int rt = 0, ru = 0;               // step qq + 1
+  for (int qq = 0; qq < Q; ++qq) {
+    if (++rt == taps) {
+      rt = 0;
+      ++ru;
+    }
+    // publish step qq+1's weights (and rows, on a chunk's first tap); every wave's reads of step qq-1
+    // are done (lgkmcnt), so its weight slot and, on a chunk change, the old row buffer may be restaged
+    if (qq + 1 < Q) wait_vmcnt(issued - (rt == 0 ? max(mWa, mX) : mWa));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    const bool tile_end = t == taps - 1 && c == nch - 1;
+    if constexpr ((EF & (VE_RESID | VE_ACCUM)) != 0)
+      if (tile_end) epi_loads(ti);
+    if (t == 0) stage_x();  // rows of chunk u+1 into the buffer chunk u-1 used
+    mWa = mWb;
+    mWb = stage_w();        // weights of step qq+3 into the slot step qq-1 used
+    // slice 0 of step qq (registers) || reads of slice 1 of step qq; slice 1 || slice 0 of step qq+1
+    read_frag(F1, 1, qq & 3, u & 1, t);
+    mma_slice(F0);
+    read_frag(F0, 0, (qq + 1) & 3, ru & 1, rt);
+    mma_slice(F1);
     if (++t == taps) {
       t = 0;
       ++u;
       if (++c == nch) {
         c = 0;
         epilogue(ti);
+        issued += NST;  // its stores join the counted VMEM stream
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -296,7 +392,8 @@ __global__ void vconv_repack_kernel(const bf16* __restrict__ src, int Mpad0, int
 }
 
 bool vconv_supported(int cin, int cout, int k, int dil, int stride) {
-  return stride == 1 && cin % 64 == 0 && cout % BM == 0 && BN + (k - 1) * dil <= XROWS;
+  // k >= 2: a chunk's rows are staged during its predecessor's first step and read one step later
+  return stride == 1 && k >= 2 && cin % 64 == 0 && cout % BM == 0 && cout <= MMAX && BN + (k - 1) * dil <= XROWS;
 }
 
 size_t vconv_packed_bytes(int cin, int cout, int k) {
@@ -326,9 +423,9 @@ static int cu_count() {
 }
 
 int launch_vconv(int ef, const VConvArgs& a, hipStream_t st) {
-  MT_REQUIRE(a.x && a.w && a.bias && a.y && a.zero, "vconv: null pointer");
-  MT_REQUIRE(a.B > 0 && a.L > 0 && a.cin % 64 == 0 && a.M % BM == 0 && a.Mpad == a.M, "vconv: geometry");
-  MT_REQUIRE(a.taps >= 1 && a.dil >= 1 && BN + (a.taps - 1) * a.dil <= XROWS, "vconv: taps %d dil %d", a.taps, a.dil);
+  MT_REQUIRE(a.x && a.w && a.bias && a.y && a.zero && a.trash, "vconv: null pointer");
+  MT_REQUIRE(a.B > 0 && a.L > 0 && a.cin % 64 == 0 && a.M % BM == 0 && a.Mpad == a.M && a.M <= MMAX, "vconv: geometry");
+  MT_REQUIRE(a.taps >= 2 && a.dil >= 1 && BN + (a.taps - 1) * a.dil <= XROWS, "vconv: taps %d dil %d", a.taps, a.dil);
   MT_REQUIRE(!(ef & VE_RESID) || a.resid, "vconv: resid");
   MT_REQUIRE(!(ef & VE_DUAL) || a.y2, "vconv: y2");
   const long ntiles = (long)a.B * ((a.L + BN - 1) / BN) * (a.Mpad / BM);

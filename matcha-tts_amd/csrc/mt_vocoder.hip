@@ -152,7 +152,7 @@ bool Vocoder::stage_vc(int i) const {
 size_t Vocoder::workspace_bytes(int B, int T) const {
   const size_t big = align256((size_t)B * T * frame_elems() * esize);
   // + XA, RA: the activated copies the vconv stages read
-  return (any_vc ? 6 : 4) * big + align256((size_t)B * T * n_mels * esize);
+  return (any_vc ? 6 * big + 4096 : 4 * big) + align256((size_t)B * T * n_mels * esize);
 }
 
 // One wide ResBlock1 stage through mt_vconv (bf16). Per resblock j, pair q (models.py:90-97):
@@ -162,7 +162,7 @@ size_t Vocoder::workspace_bytes(int B, int T) const {
 // Rounding points equal the generic per-layer path's: every stored tensor is rounded to bf16 and the
 // activated copies are lrelu of the rounded values.
 int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, const char* XA, char* XS, char* Tb,
-                         char* R, char* RA, hipStream_t st) const {
+                         char* R, char* RA, char* trash, hipStream_t st) const {
   const int nk = (int)rb_kernels.size();
   const bf16* zero = (const bf16*)(P + zero_off);
   int rc;
@@ -189,6 +189,7 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
       a.slope = 0.1f;
       a.div = 1.f;
       a.zero = zero;
+      a.trash = (bf16*)trash;
       if ((rc = launch_vconv(VE_ACT, a, st))) return rc;
       VConvArgs b = a;
       b.x = (const bf16*)Tb;
@@ -229,6 +230,7 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
   char* xm = ws + 4 * big;
   char* XA = ws + 4 * big + align256((size_t)B * T * n_mels * esize);
   char* RA = XA + big;
+  char* trash = RA + big;  // 4 KiB (vconv stores of frames past L)
   if ((rc = bct_to_btc(dtype, mel, B, n_mels, T, 1.f, xm, n_mels, 0, st))) return rc;
   {
     ConvArgs a = gemm_args(pre, P, B, T);
@@ -250,7 +252,7 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
         u.y2 = XA;
         if ((rc = launch_conv<E, PF_LRELU, EF_DUAL>(u, st))) return rc;
         L = u.Tout;
-        if ((rc = stage_vconv(P, (int)i, B, L, X, XA, XS, Tb, R, RA, st))) return rc;
+        if ((rc = stage_vconv(P, (int)i, B, L, X, XA, XS, Tb, R, RA, trash, st))) return rc;
         continue;
       }
     }

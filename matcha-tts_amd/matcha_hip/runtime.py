@@ -318,7 +318,7 @@ def op_conv1d(x_btc: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor]
 
 def op_vconv(x_btc: torch.Tensor, W: torch.Tensor, bias: torch.Tensor, dil: int = 1, ef: int = 0,
              resid: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None,
-             slope: float = 0.1, div: float = 1.0, ws: Optional[torch.Tensor] = None):
+             slope: float = 0.1, div: float = 1.0, ws: Optional[torch.Tensor] = None, pack: bool = True):
     """Op-level test entry of mt_vconv: one "same"-padded bf16 Conv1d on an already activated
     [B,L,C] input with the ResBlock epilogues (ef bits: 1 resid, 2 accumulate into y, 4 /div,
     8 y=lrelu(v), 16 also y2=lrelu(v)). Returns (y, y2)."""
@@ -335,10 +335,13 @@ def op_vconv(x_btc: torch.Tensor, W: torch.Tensor, bias: torch.Tensor, dil: int 
     L_ = lib()
     nb = L_.mt_op_vconv_workspace_bytes(cin, cout, k)
     if ws is None or ws.numel() < nb:
+        if not pack:
+            raise ValueError("op_vconv: pack=False needs the workspace a packing call filled")
         ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
     W, bias = f32c(W), f32c(bias)
     check(L_.mt_op_vconv(ptr(x), B, L, cin, ptr(W), ptr(bias), cout, k, dil, int(ef), ptr(resid), ptr(y), ptr(y2),
-                         float(slope), float(div), ws.data_ptr(), ws.numel(), stream_handle(x.device)), "op_vconv")
+                         float(slope), float(div), int(bool(pack)), ws.data_ptr(), ws.numel(),
+                         stream_handle(x.device)), "op_vconv")
     return y, y2
 
 

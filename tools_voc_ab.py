@@ -36,4 +36,6 @@ for r in range(R + 1):
             res[on].append((time.perf_counter() - t0) * 1e3)
 for on in (True, False):
     v = sorted(res[on])
+    if not v:
+        continue
     print(f"vocoder B={B} T={T} vconv={on}: median {v[len(v)//2]:.2f} ms min {v[0]:.2f} ms", flush=True)
