@@ -28,7 +28,7 @@ struct VConvArgs {
   const bf16* resid;  // [B][L][M] (VE_RESID)
   float div, slope;
   const bf16* zero;   // >= 128 zero bytes: source of the conv's zero padding rows
-  bf16* trash;        // >= 512 writable bytes: destination of the stores of frames past L
+  bf16* trash;        // >= 1 KiB writable: destination of the stores of frames past L
 };
 
 bool vconv_supported(int cin, int cout, int k, int dil, int stride);

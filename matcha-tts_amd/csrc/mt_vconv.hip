@@ -12,9 +12,10 @@
 //       rows are staged ONCE and every tap reads them shifted by t*dil rows)
 //   32 MFMAs per wave (2 K-slices x 4 x 4 fragments).
 // Every byte is staged by global_load_lds_dwordx4 (1 KiB per wave-instruction, lane-linear LDS
-// image); LDS rows are 128 B with the 16-byte chunk XOR-swizzled by (row >> 1) & 7 on the SOURCE
-// address and on the ds_read (cdna_hip_programming.md rule 21), so the 16-lane ds_read_b128 groups
-// of an MFMA fragment hit 16 distinct bank slots. Weights of step s+3 and the rows of chunk u+1 are
+// image); LDS rows are 128 B with the 16-byte chunk XOR-swizzled by (row & 6) on the SOURCE address and
+// on the ds_read (cdna_hip_programming.md rule 21): every ds_read_b128 lane group of an MFMA fragment
+// then hits 16 distinct bank slots for ANY row shift t*dil (exhaustively checked over the 16 shifts;
+// a (row >> 1) & 7 swizzle is 2-way on half of them). Weights of step s+3 and the rows of chunk u+1 are
 // in flight while step s computes: each wave counts the DMA instructions it issued and waits with a
 // COUNTED `s_waitcnt vmcnt(N)` for exactly the ones the step needs, then one raw s_barrier per step
 // publishes them (no __syncthreads: its fence would drain the prefetch). The loop runs across tile
@@ -161,7 +162,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     for (int i = 0; i < NWW; ++i) {
       const int j = wave * NWW + i;
       const int r = 8 * j + lrow;
-      const int q = lp ^ ((r >> 1) & 7);
+      const int q = lp ^ (r & 6);
       glds16(base + r * 64 + q * 8, dst + j * 1024);
     }
   };
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     for (int i = 0; i < NXW; ++i) {
       const int j = wave + 8 * i;
       const int r = 8 * j + lrow;
-      const int q = lp ^ ((r >> 1) & 7);
+      const int q = lp ^ (r & 6);
       const int f = f0 + r;
       const bool ok = r < R && f >= 0 && f < L;
       const bf16* src = ok ? xb + (size_t)f * cin + q * 8 : a.zero + q * 8;
@@ -189,72 +190,98 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int g4 = lane >> 4, l16 = lane & 15;
-  // residual / accumulator values of the tile: loaded
-  // at the start of the tile's last step, consumed after its MFMAs
-  bf16x4 rv[4][4], yv[4][4];
+  // Epilogue I/O is 16 bytes per lane: blocks X = (fm, fn) and Y = (fm + 1, fn) hold, per lane, 4
+  // channels of one frame each; v_permlane16_swap (odd 16-lane rows of X <-> even rows of Y) turns
+  // them into 8 consecutive channels per lane (row g4: X or Y by g4 & 1, channels +8 by g4 >> 1), so a
+  // wave moves 64 B contiguous per frame per instruction. The swap is an involution, so loaded
+  // residuals are swapped back into the accumulator layout the same way.
+  auto swap16 = [](uint32_t& x, uint32_t& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+  };
+  const int ch16 = wm * 64 + (g4 & 1) * 16 + (g4 >> 1) * 8;  // + fm * 16 (fm even): this lane's 8 channels
+  // residual / accumulator values of the tile, 16 B per lane: loaded at the start of the tile's last
+  // step, consumed after its MFMAs
+  u32x4 rv[2][4], yv[2][4];
   auto epi_loads = [&](int ti) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
     const size_t rowbase = (size_t)b * L;
 #pragma unroll
-    for (int fm = 0; fm < 4; ++fm) {
-      const int m = m0 + wm * 64 + fm * 16 + 4 * g4;
+    for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
       for (int fn = 0; fn < 4; ++fn) {
         const int n = min(n0 + wn * 64 + fn * 16 + l16, L - 1);  // clamped: no per-block branch
-        const size_t o = (rowbase + n) * a.M + m;
-        if constexpr ((EF & VE_RESID) != 0) rv[fm][fn] = *reinterpret_cast<const bf16x4*>(a.resid + o);
-        if constexpr ((EF & VE_ACCUM) != 0) yv[fm][fn] = *reinterpret_cast<const bf16x4*>(a.y + o);
+        const size_t o = (rowbase + n) * a.M + m0 + ch16 + fp * 32;
+        if constexpr ((EF & VE_RESID) != 0) rv[fp][fn] = *reinterpret_cast<const u32x4*>(a.resid + o);
+        if constexpr ((EF & VE_ACCUM) != 0) yv[fp][fn] = *reinterpret_cast<const u32x4*>(a.y + o);
       }
-    }
   };
   // Every lane stores (frames past L go to a trash line), so the store count per tile is a constant the
   // vmcnt bookkeeping can add: NST younger VMEM operations the next steps' waits may leave in flight.
-  constexpr int NST = 16 * ((EF & VE_DUAL) ? 2 : 1);
+  constexpr int NST = 8 * ((EF & VE_DUAL) ? 2 : 1);
+  auto bf2 = [](uint32_t w, int i) -> float { return __uint_as_float(i ? (w & 0xffff0000u) : (w << 16)); };
+  auto pack2 = [](bf16 lo, bf16 hi) -> uint32_t {
+    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+  };
   auto epilogue = [&](int ti) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
     const size_t rowbase = (size_t)b * L;
 #pragma unroll
-    for (int fm = 0; fm < 4; ++fm) {
-      const int m = m0 + wm * 64 + fm * 16 + 4 * g4;
-      const f32x4 bias4 = *reinterpret_cast<const f32x4*>(smem + BIAS_OFF + 4 * m);
+    for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
       for (int fn = 0; fn < 4; ++fn) {
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[fm][fn][r] + bias4[r];
+        // residual / old accumulator of blocks X (fm = 2fp) and Y (fm = 2fp+1) back in accumulator layout
+        uint32_t rx0 = 0, rx1 = 0, ry0 = 0, ry1 = 0, yx0 = 0, yx1 = 0, yy0 = 0, yy1 = 0;
         if constexpr ((EF & VE_RESID) != 0) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = v[r] + (float)rv[fm][fn][r];
+          rx0 = rv[fp][fn][0], rx1 = rv[fp][fn][1], ry0 = rv[fp][fn][2], ry1 = rv[fp][fn][3];
+          swap16(rx0, ry0);
+          swap16(rx1, ry1);
         }
         if constexpr ((EF & VE_ACCUM) != 0) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (float)yv[fm][fn][r] + v[r];
+          yx0 = yv[fp][fn][0], yx1 = yv[fp][fn][1], yy0 = yv[fp][fn][2], yy1 = yv[fp][fn][3];
+          swap16(yx0, yy0);
+          swap16(yx1, yy1);
         }
-        if constexpr ((EF & VE_DIV) != 0) {
+        uint32_t o1[2][2], o2[2][2];  // [X|Y][dword]
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = v[r] / a.div;
-        }
-        bf16x4 o1, o2;
+        for (int h = 0; h < 2; ++h) {
+          const int fm = 2 * fp + h;
+          const int m = m0 + wm * 64 + fm * 16 + 4 * g4;
+          const f32x4 bias4 = *reinterpret_cast<const f32x4*>(smem + BIAS_OFF + 4 * m);
+          const uint32_t rr[2] = {h ? ry0 : rx0, h ? ry1 : rx1};
+          const uint32_t yy[2] = {h ? yy0 : yx0, h ? yy1 : yx1};
+          bf16 ob[4], ab[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bf16 rb = (bf16)v[r];
-          const bf16 av = (bf16)lrelu_f((float)rb, a.slope);
-          o1[r] = (EF & VE_ACT) ? av : rb;
-          o2[r] = av;
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[fm][fn][r] + bias4[r];
+            if constexpr ((EF & VE_RESID) != 0) v = v + bf2(rr[r >> 1], r & 1);
+            if constexpr ((EF & VE_ACCUM) != 0) v = bf2(yy[r >> 1], r & 1) + v;
+            if constexpr ((EF & VE_DIV) != 0) v = v / a.div;
+            const bf16 rb = (bf16)v;
+            const bf16 av = (bf16)lrelu_f((float)rb, a.slope);
+            ob[r] = (EF & VE_ACT) ? av : rb;
+            ab[r] = av;
+          }
+          o1[h][0] = pack2(ob[0], ob[1]);
+          o1[h][1] = pack2(ob[2], ob[3]);
+          o2[h][0] = pack2(ab[0], ab[1]);
+          o2[h][1] = pack2(ab[2], ab[3]);
         }
+        swap16(o1[0][0], o1[1][0]);
+        swap16(o1[0][1], o1[1][1]);
         const int n = n0 + wn * 64 + fn * 16 + l16;
         const bool ok = n < L;
-        const size_t o = (rowbase + n) * a.M + m;
-        bf16* p1 = ok ? a.y + o : a.trash + 4 * lane;
-        *reinterpret_cast<bf16x4*>(p1) = o1;
+        const size_t o = (rowbase + n) * a.M + m0 + ch16 + fp * 32;
+        *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
         if constexpr ((EF & VE_DUAL) != 0) {
-          bf16* p2 = ok ? a.y2 + o : a.trash + 4 * lane;
-          *reinterpret_cast<bf16x4*>(p2) = o2;
+          swap16(o2[0][0], o2[1][0]);
+          swap16(o2[0][1], o2[1][1]);
+          *reinterpret_cast<u32x4*>(ok ? a.y2 + o : a.trash + 8 * lane) = u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]};
         }
       }
-    }
   };
 
   // ---- staging cursors and DMA bookkeeping (all wave-uniform) ----
@@ -297,11 +324,11 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   struct Frag {
     bf16x8 A[4], B[4];
   };
-  const int ha = (l16 >> 1) & 7;
+  const int ha = l16 & 6;
   auto read_frag = [&](Frag& F, int ks, int slot, int xbuf, int tap) {
     const char* pa = smem + slot * WSLOT + (wm * 64 + l16) * 128;
     const int rb0 = wn * 64 + l16 + tap * dil;
-    const int hb = (rb0 >> 1) & 7;
+    const int hb = rb0 & 6;
     const char* pb = smem + NWSLOT * WSLOT + xbuf * XBUF + rb0 * 128;
     const int oa = ((ks * 4 + g4) ^ ha) * 16, ob = ((ks * 4 + g4) ^ hb) * 16;
 #pragma unroll
