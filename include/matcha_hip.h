@@ -139,7 +139,8 @@ size_t mt_op_conv1d_workspace_bytes(int dtype, int cin, int cout, int k, int str
 int mt_op_conv1d(int dtype, const void* x, int B, int Tin, int cin, const float* W, const float* bias,
                  int cout, int k, int stride, int pad, int dil, int transposed, float slope, void* y,
                  int Tout, void* ws, size_t ws_bytes, void* stream);
-/* same with a fixed tile variant (in-process A/B timing; lrelu prologue only; -1 = automatic) */
+/* same with a fixed tile variant (in-process A/B timing; lrelu prologue only; -1 = automatic;
+ * variant + 0x1000 reuses the weights a previous call packed into ws) */
 int mt_op_conv1d_tile(int variant, int dtype, const void* x, int B, int Tin, int cin, const float* W,
                       const float* bias, int cout, int k, int stride, int pad, int dil, int transposed,
                       float slope, void* y, int Tout, void* ws, size_t ws_bytes, void* stream);

@@ -458,13 +458,15 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
 // ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
-enum : int { CFG_BIG = 1, CFG_SMALLN = 2, CFG_64 = 4, CFG_32 = 8, CFG_16 = 16 };
+enum : int { CFG_BIG = 1, CFG_SMALLN = 2, CFG_64 = 4, CFG_32 = 8, CFG_16 = 16, CFG_G6 = 32, CFG_C5 = 64 };
 
 // every tile is 8 waves (512 threads): 2 waves per SIMD at one workgroup per CU
 using TConv = Tile<128, 256, 2, 4, 4, 64, 1>;    // k >= 3 convs: 4 taps x 32 bf16 channels per stage
 using TConvT = Tile<128, 256, 2, 4, 2, 64, 1>;   // 2-tap polyphase ConvTranspose
 using TGemm = Tile<128, 256, 2, 4, 1, 128, 1>;   // 1x1 (Linear) GEMMs: 64 bf16 channels per stage
 using TSmall = Tile<128, 128, 2, 4, 2, 64, 2>;   // stride-2 conv or too few column tiles
+using TG6 = Tile<128, 128, 2, 4, 1, 256, 1>;     // 1x1 GEMMs with K >= 512 or M <= 384 (decoder): 256-byte stages
+using TC5 = Tile<128, 128, 2, 4, 4, 64, 1>;      // k >= 3 convs whose 128x256 grid would leave CUs idle
 using T64x256 = Tile<64, 512, 1, 8, 4, 64, 1>;   // wave tile 64x64 (HiFi-GAN 64-channel stage)
 using T32x256 = Tile<32, 512, 1, 8, 4, 64, 1>;   // wave tile 32x64 (32-channel stage)
 using T16x256 = Tile<16, 512, 1, 8, 4, 64, 1>;   // wave tile 16x64 (conv_post, M = 1)
@@ -480,6 +482,9 @@ using V7 = Tile<128, 128, 2, 2, 2, 64, 1>;   // 4 waves, 77 KB: two workgroups p
 using V8 = Tile<64, 128, 2, 2, 4, 64, 1>;    // 4 waves, 79 KB: two workgroups per CU
 using V9 = Tile<64, 256, 2, 4, 2, 64, 1>;    // 8 waves, 78 KB: two workgroups per CU
 using V10 = Tile<128, 128, 2, 2, 4, 64, 1>;  // 4 waves, one workgroup per CU
+using V13 = Tile<64, 128, 2, 2, 1, 128, 1>;  // 4 waves, 64 KB: 1x1 GEMMs, two workgroups per CU
+using V14 = Tile<64, 64, 2, 2, 1, 128, 1>;   // 4 waves, 1x1 GEMMs, small tiles
+using V15 = Tile<128, 64, 2, 2, 1, 128, 1>;  // 4 waves
 
 template <class E, class TL, int PF, int EF, int TAG = 0>
 static int launch_tile(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
@@ -533,6 +538,12 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
     if (M <= 64) return launch_tile<E, T64x256, PF, EF, TAG>(a, stream, ntiles_out);
   if constexpr ((CFGS & CFG_BIG) != 0) {
     const long wgs = (long)a.B * ((a.Ncols + 255) / 256) * ((M + 127) / 128);
+    // choices measured in-process on the decoder's shapes (tools_ab_gemm.py, B=32, T=728)
+    if constexpr ((CFGS & CFG_G6) != 0)
+      if (a.stride == 1 && a.taps == 1 && (a.cin >= 512 || M <= 384))
+        return launch_tile<E, TG6, PF, EF, TAG>(a, stream, ntiles_out);
+    if constexpr ((CFGS & CFG_C5) != 0)
+      if (a.stride == 1 && a.taps >= 3 && wgs < 192) return launch_tile<E, TC5, PF, EF, TAG>(a, stream, ntiles_out);
     if (a.stride == 1 && (wgs >= 192 || (CFGS & CFG_SMALLN) == 0)) {
       if (a.taps == 1) return launch_tile<E, TGemm, PF, EF, TAG>(a, stream, ntiles_out);
       if (a.taps == 2) return launch_tile<E, TConvT, PF, EF, TAG>(a, stream, ntiles_out);
@@ -546,14 +557,14 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
 
 // (PF, EF, tile configs) combinations used by the decoder and the vocoder.
 #define MT_CONV_COMBOS(X)                                                              \
-  X(PF_MASK, EF_GNSTATS, CFG_BIG | CFG_SMALLN)                                     \
-  X(PF_GN | PF_TB | PF_MASK, EF_GNSTATS, CFG_BIG | CFG_SMALLN)                     \
-  X(PF_MASK, EF_GNADD, CFG_BIG | CFG_SMALLN)                                       \
-  X(PF_LN, 0, CFG_BIG | CFG_SMALLN)                                                \
-  X(0, EF_RESID, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32)                   \
-  X(PF_LN, EF_SNAKE, CFG_BIG | CFG_SMALLN)                                         \
-  X(PF_MASK, 0, CFG_BIG | CFG_SMALLN)                                              \
-  X(PF_GN | PF_MASK, EF_MASK | EF_EULER, CFG_BIG | CFG_SMALLN)                     \
+  X(PF_MASK, EF_GNSTATS, CFG_BIG | CFG_SMALLN | CFG_G6 | CFG_C5)                                     \
+  X(PF_GN | PF_TB | PF_MASK, EF_GNSTATS, CFG_BIG | CFG_SMALLN | CFG_G6 | CFG_C5)                     \
+  X(PF_MASK, EF_GNADD, CFG_BIG | CFG_SMALLN | CFG_G6 | CFG_C5)                                       \
+  X(PF_LN, 0, CFG_BIG | CFG_SMALLN | CFG_G6 | CFG_C5)                                                \
+  X(0, EF_RESID, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32 | CFG_G6 | CFG_C5)                   \
+  X(PF_LN, EF_SNAKE, CFG_BIG | CFG_SMALLN | CFG_G6 | CFG_C5)                                         \
+  X(PF_MASK, 0, CFG_BIG | CFG_SMALLN | CFG_G6 | CFG_C5)                                              \
+  X(PF_GN | PF_MASK, EF_MASK | EF_EULER, CFG_BIG | CFG_SMALLN | CFG_G6 | CFG_C5)                     \
   X(0, 0, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32 | CFG_16)             \
   X(PF_LRELU, 0, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32 | CFG_16)      \
   X(PF_LRELU, EF_RESID, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32)            \
@@ -591,6 +602,11 @@ static int launch_variant(int variant, const ConvArgs& a, hipStream_t stream) {
     case 8: return launch_tile<E, V8, PF, 0, 1>(a, stream, nullptr);
     case 9: return launch_tile<E, V9, PF, 0, 1>(a, stream, nullptr);
     case 10: return launch_tile<E, V10, PF, 0, 1>(a, stream, nullptr);
+    case 11: return launch_tile<E, TGemm, PF, 0, 1>(a, stream, nullptr);
+    case 12: return launch_tile<E, TSmall, PF, 0, 1>(a, stream, nullptr);
+    case 13: return launch_tile<E, V13, PF, 0, 1>(a, stream, nullptr);
+    case 14: return launch_tile<E, V14, PF, 0, 1>(a, stream, nullptr);
+    case 15: return launch_tile<E, V15, PF, 0, 1>(a, stream, nullptr);
     default: set_error("conv: unknown tile variant %d", variant); return -1;
   }
 }
