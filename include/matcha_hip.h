@@ -46,6 +46,31 @@ const char* mt_last_error(void);
 int mt_abi_version(void);
 
 /* ---------------------------------------------------------------------------------------
+ * Text encoder + duration predictor (TextEncoder.forward, model.py:517-535; Encoder :428-439,
+ * RoPE MultiHeadAttention :294-364, ConvReluNorm prenet :171-208, DurationPredictor :210-229).
+ * Replaces the host PyTorch encoder that MatchaTTS.synthesize (model.py:1273) calls.
+ * Parameters are named relative to the TextEncoder module ("emb.weight",
+ * "encoder.attn_layers.0.conv_q.weight", "proj_w.norm_1.gamma", ...); "_rope_theta" is the fp32
+ * table 1/10000^(arange(0, d, 2)/d), d = int(head_dim * 0.5), of model.py:258-265.
+ * forward: x int64 [B][Tx] token ids, x_lengths int64 [B], spks fp32 [B][spk_emb_dim] (n_spks > 1)
+ * -> mu fp32 [B][80][Tx], logw fp32 [B][1][Tx], x_mask fp32 [B][1][Tx].
+ * ------------------------------------------------------------------------------------- */
+typedef struct mt_encoder mt_encoder;
+int mt_encoder_create(int n_vocab, int n_channels, int filter_channels, int n_heads, int n_layers, int kernel_size,
+                      int n_spks, int spk_emb_dim, int dp_filter_channels, int dp_kernel_size, int prenet, int dtype,
+                      mt_encoder** out);
+void mt_encoder_destroy(mt_encoder* e);
+int mt_encoder_num_params(const mt_encoder* e);
+int mt_encoder_param_name(const mt_encoder* e, int i, char* buf, int buflen);
+int mt_encoder_param_shape(const mt_encoder* e, int i, int64_t* shape, int maxdim);
+size_t mt_encoder_packed_bytes(const mt_encoder* e);
+int mt_encoder_pack(const mt_encoder* e, const float* const* params, void* packed, void* stream);
+size_t mt_encoder_workspace_bytes(const mt_encoder* e, int B, int Tx);
+int mt_encoder_forward(const mt_encoder* e, const void* packed, const int64_t* x, const int64_t* x_lengths,
+                       const float* spks, int B, int Tx, float* mu, float* logw, float* x_mask, void* ws,
+                       size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * U-Net estimator + CFM solver. Hyper-parameters are those of main.py:67-76
  * (channels=(256,256), attention_head_dim=64); c_cond = 2*n_feats (+ spk_emb_dim).
  * ------------------------------------------------------------------------------------- */

@@ -16,6 +16,9 @@ size_t denoise_workspace_bytes(int B, int L);
 int stft_magnitude(const float* audio, int B, int L, float* mag, hipStream_t st);
 }  // namespace mt
 
+struct mt_encoder {
+  mt::Encoder e;
+};
 struct mt_decoder {
   mt::Decoder d;
 };
@@ -45,6 +48,45 @@ const char* mt_last_error(void) { return mt::last_error(); }
 int mt_abi_version(void) { return 1; }
 
 // ---- decoder ----
+int mt_encoder_create(int n_vocab, int n_channels, int filter_channels, int n_heads, int n_layers, int kernel_size,
+                      int n_spks, int spk_emb_dim, int dp_filter_channels, int dp_kernel_size, int prenet, int dtype,
+                      mt_encoder** out) {
+  MT_REQUIRE(out, "null out");
+  mt_encoder* h = new (std::nothrow) mt_encoder();
+  MT_REQUIRE(h, "out of host memory");
+  int rc = h->e.init(n_vocab, n_channels, filter_channels, n_heads, n_layers, kernel_size, n_spks, spk_emb_dim,
+                     dp_filter_channels, dp_kernel_size, prenet, dtype);
+  if (rc) {
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return 0;
+}
+void mt_encoder_destroy(mt_encoder* e) { delete e; }
+int mt_encoder_num_params(const mt_encoder* e) { return e ? (int)e->e.params.names.size() : -1; }
+int mt_encoder_param_name(const mt_encoder* e, int i, char* buf, int buflen) {
+  MT_REQUIRE(e, "null encoder");
+  return param_name(e->e.params, i, buf, buflen);
+}
+int mt_encoder_param_shape(const mt_encoder* e, int i, int64_t* shape, int maxdim) {
+  MT_REQUIRE(e, "null encoder");
+  return param_shape(e->e.params, i, shape, maxdim);
+}
+size_t mt_encoder_packed_bytes(const mt_encoder* e) { return e ? e->e.packed_bytes : 0; }
+int mt_encoder_pack(const mt_encoder* e, const float* const* params, void* packed, void* stream) {
+  MT_REQUIRE(e && params && packed, "encoder_pack: null argument");
+  return e->e.pack(params, packed, (hipStream_t)stream);
+}
+size_t mt_encoder_workspace_bytes(const mt_encoder* e, int B, int Tx) { return e ? e->e.workspace_bytes(B, Tx) : 0; }
+int mt_encoder_forward(const mt_encoder* e, const void* packed, const int64_t* x, const int64_t* x_lengths,
+                       const float* spks, int B, int Tx, float* mu, float* logw, float* x_mask, void* ws,
+                       size_t ws_bytes, void* stream) {
+  MT_REQUIRE(e && packed, "encoder_forward: null argument");
+  return e->e.forward(packed, (const long long*)x, (const long long*)x_lengths, spks, B, Tx, mu, logw, x_mask, ws,
+                      ws_bytes, (hipStream_t)stream);
+}
+
 int mt_decoder_create(int c_cond, int n_mid, int n_blocks, int heads, int dtype, mt_decoder** out) {
   MT_REQUIRE(out, "null out");
   mt_decoder* h = new (std::nothrow) mt_decoder();

@@ -33,6 +33,8 @@ enum : int {
   EF_EULER = 256,  // Euler/midpoint update of z (fp32 master) + estimator-input slot
   EF_OUTF32 = 512, // store fp32 whatever the element type
   EF_DUAL = 1024,  // also store y2 = lrelu(round(v), slope): the activated copy a pre-activated consumer reads
+  EF_RELU = 2048,  // max(v, 0) right after the bias                 (text encoder FFN / duration predictor)
+  EF_FMASK = 4096, // v * emask as the LAST step                      ((x + proj(h)) * x_mask, prenet)
 };
 
 struct ConvArgs {

@@ -311,10 +311,14 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
       if (fr < 0 || fr >= a.Tout) continue;
       const size_t orow = (size_t)b * a.Tout + fr;
       float em = 1.f;
-      if constexpr ((EF & (EF_MASK | EF_GNADD)) != 0) em = a.emask[orow];
+      if constexpr ((EF & (EF_MASK | EF_GNADD | EF_FMASK)) != 0) em = a.emask[orow];
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[fm][fn][r] + bias4[r];
+      if constexpr ((EF & EF_RELU) != 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
       if constexpr ((EF & EF_SNAKE) != 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -357,6 +361,10 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
       if constexpr ((EF & EF_DIV) != 0) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = v[r] / a.div;
+      }
+      if constexpr ((EF & EF_FMASK) != 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] * em;
       }
       if constexpr ((EF & EF_TANH) != 0) {
 #pragma unroll
@@ -518,7 +526,7 @@ static int check_args(const ConvArgs& a, int esize, int pf, int ef) {
   if (ef & EF_GNADD) MT_REQUIRE(a.cout <= 256 && a.cout % 32 == 0 && a.gn_in && a.gy, "conv: GN epilogue");
   if (ef & EF_GNSTATS) MT_REQUIRE(a.M % 32 == 0 && a.gn_out && a.ups == 1, "conv: GN stats");
   if (pf & PF_MASK) MT_REQUIRE(a.pmask, "conv: pmask");
-  if (ef & (EF_MASK | EF_GNADD)) MT_REQUIRE(a.emask, "conv: emask");
+  if (ef & (EF_MASK | EF_GNADD | EF_FMASK)) MT_REQUIRE(a.emask, "conv: emask");
   if (ef & EF_RESID) MT_REQUIRE(a.resid, "conv: resid");
   if (ef & EF_EULER) MT_REQUIRE(a.zmaster && a.xin_z, "conv: euler buffers");
   if (ef & EF_SNAKE) MT_REQUIRE(a.snake_alpha && a.snake_ibeta, "conv: snake params");
@@ -573,7 +581,12 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
     CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32)                                \
   X(PF_LRELU, EF_RESID | EF_DIV, CFG_BIG | CFG_SMALLN | CFG_64 | CFG_32)   \
   X(PF_LRELU, EF_TANH | EF_OUTF32, CFG_16 | CFG_32)                                     \
-  X(PF_LRELU, EF_DUAL, CFG_BIG | CFG_SMALLN)
+  X(PF_LRELU, EF_DUAL, CFG_BIG | CFG_SMALLN)                                            \
+  X(0, EF_RESID | EF_FMASK, CFG_BIG | CFG_SMALLN | CFG_G6)                               \
+  X(PF_MASK, EF_RELU, CFG_BIG | CFG_SMALLN | CFG_C5)                                     \
+  X(PF_MASK, EF_MASK | EF_RESID, CFG_BIG | CFG_SMALLN | CFG_C5)                          \
+  X(0, EF_MASK, CFG_BIG | CFG_SMALLN | CFG_G6)                                           \
+  X(PF_MASK, EF_MASK | EF_OUTF32, CFG_16 | CFG_32)
 
 #define MT_DEFINE_LAUNCH(PFV, EFV, CFGV)                                                    \
   template <>                                                                             \

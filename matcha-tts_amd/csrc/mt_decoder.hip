@@ -88,8 +88,16 @@ int pack_gemm(const GemmW& g, int dtype, const float* const* params, char* P, hi
                    g.cin_pad, wdst, st);
     if (rc) return rc;
   }
-  rc = pack_vec(g.bsrc >= 0 ? params[g.bsrc] : nullptr, g.cout, g.M, 0, (float*)(P + g.b_off), st);
-  if (rc) return rc;
+  if (!g.bsrcs.empty()) {
+    const int rows_per = g.cout / (int)g.bsrcs.size();
+    for (size_t i = 0; i < g.bsrcs.size(); ++i) {
+      rc = pack_vec(params[g.bsrcs[i]], rows_per, rows_per, 0, (float*)(P + g.b_off) + i * rows_per, st);
+      if (rc) return rc;
+    }
+  } else {
+    rc = pack_vec(g.bsrc >= 0 ? params[g.bsrc] : nullptr, g.cout, g.M, 0, (float*)(P + g.b_off), st);
+    if (rc) return rc;
+  }
   if (g.ln_b >= 0) {  // LN(x) = x_hat*gamma + beta  ->  W(gamma) x_hat + (b + W beta)
     const int rows_per = g.cout / (int)g.wsrc.size();
     for (size_t i = 0; i < g.wsrc.size(); ++i) {

@@ -1,0 +1,474 @@
+// Text encoder + duration predictor on the GPU (model.py:148-535).
+//
+//   ids [B][Tx] -> emb * sqrt(C) -> prenet: 3 x (conv_k5(h*m) -> LN -> ReLU), (x + proj(h)) * m
+//   [-> ++ spks]  -> 6 x { x*m; x = LN1(x + conv_o(RoPE-MHA(x))); x = LN2(x + conv_2(relu(conv_1(x*m))*m)*m) } * m
+//   mu = proj_m(x) * m                                     -> [B][80][Tx] fp32
+//   logw = proj(LN(relu(conv_2(LN(relu(conv_1(x*m)))*m)))*m) * m   -> [B][1][Tx] fp32
+// Activations are [B][Tx][C] (channel-contiguous) in the element type; every Conv1d / 1x1 projection
+// runs on the implicit-GEMM conv kernel (mt_conv.h) with its mask / ReLU / residual fused, LayerNorms
+// run as one-wave-per-frame row kernels, attention as a RoPE-fused online-softmax kernel with the
+// reference's mask semantics (scores of masked (query, key) pairs := -1e4, model.py:353-354).
+#include <math.h>
+
+#include <algorithm>
+
+#include "mt_model.h"
+
+namespace mt {
+
+// ---------------------------------------------------------------------------------------
+// embedding (model.py:522) and x_mask (sequence_mask, model.py:42-46)
+// ---------------------------------------------------------------------------------------
+template <class E>
+__global__ void embed_kernel(const long long* __restrict__ ids, const long long* __restrict__ xlen, int Tx,
+                             const float* __restrict__ emb, int nvocab, int C, float scale, E* __restrict__ out,
+                             float* __restrict__ xmask) {
+  const int row = blockIdx.x;  // b * Tx + t
+  const int b = row / Tx, t = row - b * Tx;
+  long long id = ids[row];
+  id = id < 0 ? 0 : (id >= nvocab ? nvocab - 1 : id);
+  const float* e = emb + (size_t)id * C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) out[(size_t)row * C + c] = from_f<E>(e[c] * scale);
+  if (threadIdx.x == 0) xmask[row] = (long long)t < xlen[b] ? 1.f : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------
+// LayerNorm over channels of one frame (model.py:152-161: mean, mean((x-mean)^2), rsqrt(var+eps)),
+// one wave per frame; optional ReLU after it (prenet order, model.py:203-205) and frame mask.
+// ---------------------------------------------------------------------------------------
+template <class E, int VPL>
+__global__ __launch_bounds__(256) void rowln_kernel(const E* __restrict__ x, int rows, int C,
+                                                    const float* __restrict__ g, const float* __restrict__ bt,
+                                                    float eps, const float* __restrict__ mask, int relu,
+                                                    E* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const E* xr = x + (size_t)row * C;
+  float v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < C ? to_f(xr[c]) : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    const float d = c < C ? v[i] - mean : 0.f;
+    q += d * d;
+  }
+  const float rstd = 1.f / sqrtf(wave_sum(q) / (float)C + eps);
+  const float m = mask ? mask[row] : 1.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c >= C) continue;
+    float o = (v[i] - mean) * rstd * g[c] + bt[c];
+    if (relu) o = fmaxf(o, 0.f);
+    y[(size_t)row * C + c] = from_f<E>(o * m);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// RoPE multi-head self-attention (model.py:343-364, RotaryPositionalEmebeddings :244-292).
+// qkv [B][Tx][3W] (q | k | v, head h = channels h*dk .. h*dk+dk-1), out [B][Tx][W].
+// Workgroup = 64 queries x 4 lanes of one (utterance, head); lane p of a query owns dk/4 dims of q and
+// of its output. Keys stream through LDS 64 at a time, RoPE applied while staging (angle t*theta_i on
+// the pair (i, i + d/2) of the first d = dk/2 dims, the cached cos/sin table of the reference), then
+// scores = q.k / sqrt(dk) with masked pairs := -1e4 and an online softmax over all Tx keys.
+// ---------------------------------------------------------------------------------------
+template <class E, int DK>
+__global__ __launch_bounds__(256) void enc_attn_kernel(const E* __restrict__ qkv, const float* __restrict__ xmask,
+                                                       const float* __restrict__ theta, float inv_scale_div,
+                                                       int Tx, int heads, E* __restrict__ out) {
+  constexpr int DR = DK / 2, HR = DR / 2, DP = DK / 4;  // rope dims, half of them, dims per lane
+  constexpr int KS = DK + 1;                             // padded LDS row (floats)
+  __shared__ float Ks[64 * KS], Vs[64 * KS], Qs[64 * KS];
+  __shared__ float km[64];
+  const int tid = threadIdx.x;
+  const int qi = tid >> 2, p = tid & 3;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int t0 = blockIdx.x * 64;
+  const int W = heads * DK, ld = 3 * W;
+  const E* base = qkv + (size_t)b * Tx * ld;
+
+  // stage one 64-row block of q or k (RoPE applied) or v into an LDS tile
+  auto stage = [&](float* dst, int r0, int part, bool rope) {
+    for (int e = tid; e < 64 * DK; e += 256) {
+      const int r = e / DK, d = e - r * DK;
+      const int t = r0 + r;
+      float v = 0.f;
+      if (t < Tx) {
+        const E* src = base + (size_t)t * ld + part * W + h * DK;
+        v = to_f(src[d]);
+        if (rope && d < DR) {
+          const int i = d < HR ? d : d - HR;
+          const float ang = (float)t * theta[i];
+          const float cs = cosf(ang), sn = sinf(ang);
+          const float other = to_f(src[d < HR ? d + HR : d - HR]);
+          v = d < HR ? v * cs - other * sn : v * cs + other * sn;
+        }
+      }
+      dst[r * KS + d] = v;
+    }
+  };
+  stage(Qs, t0, 0, true);
+  __syncthreads();
+  float q[DP], o[DP];
+#pragma unroll
+  for (int i = 0; i < DP; ++i) {
+    q[i] = Qs[qi * KS + p * DP + i];
+    o[i] = 0.f;
+  }
+  const int tq = t0 + qi;
+  const float mq = tq < Tx ? xmask[(size_t)b * Tx + tq] : 0.f;
+  float mrun = -INFINITY, lrun = 0.f;
+  for (int k0 = 0; k0 < Tx; k0 += 64) {
+    __syncthreads();
+    stage(Ks, k0, 1, true);
+    stage(Vs, k0, 2, false);
+    if (tid < 64) km[tid] = k0 + tid < Tx ? xmask[(size_t)b * Tx + k0 + tid] : 0.f;
+    __syncthreads();
+    const int nk = min(64, Tx - k0);
+    float s[64];
+    float cmax = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < DP; ++i) d += q[i] * Ks[j * KS + p * DP + i];
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      float sc = d / inv_scale_div;
+      if (mq * km[j] == 0.f) sc = -1e4f;
+      s[j] = j < nk ? sc : -INFINITY;
+      cmax = fmaxf(cmax, s[j]);
+    }
+    const float mnew = fmaxf(mrun, cmax);
+    const float corr = expf(mrun - mnew);
+    lrun *= corr;
+#pragma unroll
+    for (int i = 0; i < DP; ++i) o[i] *= corr;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      const float pj = expf(s[j] - mnew);
+      lrun += pj;
+#pragma unroll
+      for (int i = 0; i < DP; ++i) o[i] += pj * Vs[j * KS + p * DP + i];
+    }
+    mrun = mnew;
+  }
+  if (tq < Tx) {
+    E* dst = out + ((size_t)b * Tx + tq) * W + h * DK + p * DP;
+#pragma unroll
+    for (int i = 0; i < DP; ++i) dst[i] = from_f<E>(o[i] / lrun);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// host
+// ---------------------------------------------------------------------------------------
+int Encoder::init(int n_vocab_, int n_ch, int filt, int heads_, int layers_, int ksize, int n_spks_, int spk_dim_,
+                  int dp_filt, int dp_k, int prenet_, int dtype_) {
+  MT_REQUIRE(n_vocab_ > 0 && n_ch > 0 && filt > 0 && layers_ >= 1 && ksize >= 1 && dp_k >= 1, "encoder: config");
+  MT_REQUIRE(dtype_ == F32 || dtype_ == BF16, "encoder: dtype");
+  n_vocab = n_vocab_;
+  C = n_ch;
+  F = filt;
+  heads = heads_;
+  layers = layers_;
+  k = ksize;
+  n_spks = n_spks_;
+  spk_dim = n_spks > 1 ? spk_dim_ : 0;
+  W = C + spk_dim;
+  DF = dp_filt;
+  dpk = dp_k;
+  prenet = prenet_;
+  dtype = dtype_;
+  esize = dtype == BF16 ? 2 : 4;
+  MT_REQUIRE(W % heads == 0, "encoder: width %d not divisible by %d heads", W, heads);
+  dk = W / heads;
+  MT_REQUIRE(dk == 96 || dk == 128 || dk == 64, "encoder: head dim %d not compiled in (64/96/128)", dk);
+  MT_REQUIRE(C <= 1024 && W <= 1024 && F <= 1024 && DF <= 1024, "encoder: width");
+  const int align = 64 / esize;
+  MT_REQUIRE(C % 16 == 0 && W % 16 == 0 && F % align == 0 && DF % align == 0, "encoder: channels must be 16-aligned");
+  Packer pk;
+  ParamList& L = params;
+  L = ParamList();
+  lay.clear();
+  pre.clear();
+  const long long Cl = C, Wl = W;
+  emb = L.add("emb.weight", {n_vocab, Cl});
+  emb_off = pk.take((size_t)n_vocab * C * 4);
+  if (prenet) {
+    for (int i = 0; i < 3; ++i) {
+      const std::string p = "prenet.";
+      int w = L.add(p + "conv_layers." + std::to_string(i) + ".weight", {Cl, Cl, 5});
+      int b = L.add(p + "conv_layers." + std::to_string(i) + ".bias", {Cl});
+      Pre q;
+      q.conv = make_conv(C, C, 5, 1, 2, 1, {w}, b, esize, pk);
+      q.g = L.add(p + "norm_layers." + std::to_string(i) + ".gamma", {Cl});
+      q.b = L.add(p + "norm_layers." + std::to_string(i) + ".beta", {Cl});
+      q.ln_off = pk.take(2 * C * 4);
+      pre.push_back(q);
+    }
+    int w = L.add("prenet.proj.weight", {Cl, Cl, 1});
+    int b = L.add("prenet.proj.bias", {Cl});
+    pre_proj = make_conv(C, C, 1, 1, 0, 1, {w}, b, esize, pk);
+  }
+  for (int i = 0; i < layers; ++i) {
+    const std::string a = "encoder.attn_layers." + std::to_string(i) + ".";
+    const std::string f = "encoder.ffn_layers." + std::to_string(i) + ".";
+    Layer l;
+    int wq = L.add(a + "conv_q.weight", {Wl, Wl, 1});
+    int bq = L.add(a + "conv_q.bias", {Wl});
+    int wk = L.add(a + "conv_k.weight", {Wl, Wl, 1});
+    int bk = L.add(a + "conv_k.bias", {Wl});
+    int wv = L.add(a + "conv_v.weight", {Wl, Wl, 1});
+    int bv = L.add(a + "conv_v.bias", {Wl});
+    int wo = L.add(a + "conv_o.weight", {Wl, Wl, 1});
+    int bo = L.add(a + "conv_o.bias", {Wl});
+    l.n1g = L.add("encoder.norm_layers_1." + std::to_string(i) + ".gamma", {Wl});
+    l.n1b = L.add("encoder.norm_layers_1." + std::to_string(i) + ".beta", {Wl});
+    int w1 = L.add(f + "conv_1.weight", {(long long)F, Wl, k});
+    int b1 = L.add(f + "conv_1.bias", {(long long)F});
+    int w2 = L.add(f + "conv_2.weight", {Wl, (long long)F, k});
+    int b2 = L.add(f + "conv_2.bias", {Wl});
+    l.n2g = L.add("encoder.norm_layers_2." + std::to_string(i) + ".gamma", {Wl});
+    l.n2b = L.add("encoder.norm_layers_2." + std::to_string(i) + ".beta", {Wl});
+    l.qkv = make_conv(3 * W, W, 1, 1, 0, 1, {wq, wk, wv}, -1, esize, pk);
+    l.qkv.bsrcs = {bq, bk, bv};
+    l.o = make_conv(W, W, 1, 1, 0, 1, {wo}, bo, esize, pk);
+    l.f1 = make_conv(F, W, k, 1, k / 2, 1, {w1}, b1, esize, pk);
+    l.f2 = make_conv(W, F, k, 1, k / 2, 1, {w2}, b2, esize, pk);
+    l.n1_off = pk.take(2 * W * 4);
+    l.n2_off = pk.take(2 * W * 4);
+    lay.push_back(l);
+  }
+  {
+    int w = L.add("proj_m.weight", {80, Wl, 1});
+    int b = L.add("proj_m.bias", {80});
+    proj_m = make_conv(80, W, 1, 1, 0, 1, {w}, b, esize, pk);
+  }
+  {
+    const long long D = DF;
+    int w1 = L.add("proj_w.conv_1.weight", {D, Wl, dpk});
+    int b1 = L.add("proj_w.conv_1.bias", {D});
+    dn1g = L.add("proj_w.norm_1.gamma", {D});
+    dn1b = L.add("proj_w.norm_1.beta", {D});
+    int w2 = L.add("proj_w.conv_2.weight", {D, D, dpk});
+    int b2 = L.add("proj_w.conv_2.bias", {D});
+    dn2g = L.add("proj_w.norm_2.gamma", {D});
+    dn2b = L.add("proj_w.norm_2.beta", {D});
+    int wp = L.add("proj_w.proj.weight", {1, D, 1});
+    int bp = L.add("proj_w.proj.bias", {1});
+    dp1 = make_conv(DF, W, dpk, 1, dpk / 2, 1, {w1}, b1, esize, pk);
+    dp2 = make_conv(DF, DF, dpk, 1, dpk / 2, 1, {w2}, b2, esize, pk);
+    dpp = make_conv(1, DF, 1, 1, 0, 1, {wp}, bp, esize, pk);
+    dn1_off = pk.take(2 * DF * 4);
+    dn2_off = pk.take(2 * DF * 4);
+  }
+  theta = L.add("_rope_theta", {dk / 4});  // 1 / 10000^(arange(0, dk/2, 2) / (dk/2)), host-computed
+  theta_off = pk.take(dk / 4 * 4);
+  packed_bytes = pk.off;
+  return 0;
+}
+
+int Encoder::pack(const float* const* p, void* packed, hipStream_t st) const {
+  char* P = (char*)packed;
+  int rc;
+#define PK(expr) \
+  if ((rc = (expr)) != 0) return rc
+  PK(pack_vec(p[emb], n_vocab * C, n_vocab * C, 0, (float*)(P + emb_off), st));
+  for (const Pre& q : pre) {
+    PK(pack_gemm(q.conv, dtype, p, P, st));
+    PK(pack_vec(p[q.g], C, C, 0, (float*)(P + q.ln_off), st));
+    PK(pack_vec(p[q.b], C, C, 0, (float*)(P + q.ln_off) + C, st));
+  }
+  if (prenet) PK(pack_gemm(pre_proj, dtype, p, P, st));
+  for (const Layer& l : lay) {
+    PK(pack_gemm(l.qkv, dtype, p, P, st));
+    PK(pack_gemm(l.o, dtype, p, P, st));
+    PK(pack_gemm(l.f1, dtype, p, P, st));
+    PK(pack_gemm(l.f2, dtype, p, P, st));
+    PK(pack_vec(p[l.n1g], W, W, 0, (float*)(P + l.n1_off), st));
+    PK(pack_vec(p[l.n1b], W, W, 0, (float*)(P + l.n1_off) + W, st));
+    PK(pack_vec(p[l.n2g], W, W, 0, (float*)(P + l.n2_off), st));
+    PK(pack_vec(p[l.n2b], W, W, 0, (float*)(P + l.n2_off) + W, st));
+  }
+  PK(pack_gemm(proj_m, dtype, p, P, st));
+  PK(pack_gemm(dp1, dtype, p, P, st));
+  PK(pack_gemm(dp2, dtype, p, P, st));
+  PK(pack_gemm(dpp, dtype, p, P, st));
+  PK(pack_vec(p[dn1g], DF, DF, 0, (float*)(P + dn1_off), st));
+  PK(pack_vec(p[dn1b], DF, DF, 0, (float*)(P + dn1_off) + DF, st));
+  PK(pack_vec(p[dn2g], DF, DF, 0, (float*)(P + dn2_off), st));
+  PK(pack_vec(p[dn2b], DF, DF, 0, (float*)(P + dn2_off) + DF, st));
+  PK(pack_vec(p[theta], dk / 4, dk / 4, 0, (float*)(P + theta_off), st));
+#undef PK
+  return 0;
+}
+
+size_t Encoder::workspace_bytes(int B, int Tx) const {
+  const size_t n = (size_t)B * Tx;
+  const int wmax = std::max(std::max(W, 3 * W), std::max(F, DF));
+  return 5 * align256(n * wmax * esize) + align256(n * 80 * esize) + align256(n * 4);
+}
+
+template <class E>
+static int rowln(const E* x, int rows, int C, const float* gb, float eps, const float* mask, int relu, E* y,
+                 hipStream_t st) {
+  const dim3 grid((rows + 3) / 4), blk(256);
+  if (C <= 256)
+    hipLaunchKernelGGL((rowln_kernel<E, 4>), grid, blk, 0, st, x, rows, C, gb, gb + C, eps, mask, relu, y);
+  else if (C <= 512)
+    hipLaunchKernelGGL((rowln_kernel<E, 8>), grid, blk, 0, st, x, rows, C, gb, gb + C, eps, mask, relu, y);
+  else
+    hipLaunchKernelGGL((rowln_kernel<E, 16>), grid, blk, 0, st, x, rows, C, gb, gb + C, eps, mask, relu, y);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+template <class E>
+int Encoder::forward_t(const char* P, const long long* ids, const long long* xlen, const float* spks, int B, int Tx,
+                       float* mu, float* logw, float* xmask, char* ws, hipStream_t st) const {
+  int rc;
+  const size_t n = (size_t)B * Tx;
+  const int wmax = std::max(std::max(W, 3 * W), std::max(F, DF));
+  const size_t big = align256(n * wmax * esize);
+  char* X = ws;             // encoder state [B][Tx][W]
+  char* A = ws + big;       // scratch
+  char* Bb = ws + 2 * big;  // scratch
+  char* Q = ws + 3 * big;   // qkv / prenet input
+  char* Hh = ws + 4 * big;  // FFN hidden
+  char* MU = ws + 5 * big;  // [B][Tx][80]
+  const float eps = 1e-4f;
+  // embedding * sqrt(C) and x_mask
+  hipLaunchKernelGGL((embed_kernel<E>), dim3((unsigned)n), dim3(256), 0, st, ids, xlen, Tx, (const float*)(P + emb_off),
+                     n_vocab, C, sqrtf((float)C), (E*)Q, xmask);
+  MT_CHECK_HIP(hipGetLastError());
+  // prenet (ConvReluNorm, model.py:196-208): h = relu(LN(conv(h*m))) x3, x = (x + proj(h)) * m
+  const char* cur = Q;
+  if (prenet) {
+    const char* h = Q;
+    char* bufs[2] = {A, Bb};
+    for (int i = 0; i < 3; ++i) {
+      ConvArgs a = gemm_args(pre[i].conv, P, B, Tx);
+      a.x0 = h;
+      a.y = Hh;
+      a.pmask = xmask;
+      if ((rc = launch_conv<E, PF_MASK, 0>(a, st))) return rc;
+      if ((rc = rowln<E>((const E*)Hh, (int)n, C, (const float*)(P + pre[i].ln_off), eps, nullptr, 1, (E*)bufs[i & 1], st)))
+        return rc;
+      h = bufs[i & 1];
+    }
+    ConvArgs a = gemm_args(pre_proj, P, B, Tx);
+    a.x0 = h;
+    a.y = W == C ? X : Hh;
+    a.ldy = C;
+    a.resid = Q;
+    a.ldr = C;
+    a.emask = xmask;
+    if ((rc = launch_conv<E, 0, EF_RESID | EF_FMASK>(a, st))) return rc;
+    cur = W == C ? X : Hh;
+  }
+  if (W != C) {  // ++ speaker embedding channels (model.py:526-527), x*m
+    if ((rc = spk_fill(dtype, spks, B, spk_dim, Tx, X, W, C, st))) return rc;
+    if ((rc = copy_rows(dtype, cur, C, (int)n, C, X, W, st))) return rc;
+  } else if (cur != X) {
+    if ((rc = copy_rows(dtype, cur, C, (int)n, C, X, W, st))) return rc;
+  }
+  // encoder layers (model.py:428-439); X holds x*m at every layer entry
+  if (!prenet || W != C) {  // mask the layer-0 input (the prenet's epilogue already did when it wrote X)
+    if ((rc = mask_rows(dtype, X, (int)n, W, xmask, st))) return rc;
+  }
+  const float sdiv = sqrtf((float)dk);
+  for (int i = 0; i < layers; ++i) {
+    const Layer& l = lay[i];
+    ConvArgs q = gemm_args(l.qkv, P, B, Tx);
+    q.x0 = X;
+    q.y = Q;
+    if ((rc = launch_conv<E, 0, 0>(q, st))) return rc;
+    const dim3 ga((Tx + 63) / 64, heads, B);
+    if (dk == 96)
+      hipLaunchKernelGGL((enc_attn_kernel<E, 96>), ga, dim3(256), 0, st, (const E*)Q, xmask,
+                         (const float*)(P + theta_off), sdiv, Tx, heads, (E*)A);
+    else if (dk == 128)
+      hipLaunchKernelGGL((enc_attn_kernel<E, 128>), ga, dim3(256), 0, st, (const E*)Q, xmask,
+                         (const float*)(P + theta_off), sdiv, Tx, heads, (E*)A);
+    else
+      hipLaunchKernelGGL((enc_attn_kernel<E, 64>), ga, dim3(256), 0, st, (const E*)Q, xmask,
+                         (const float*)(P + theta_off), sdiv, Tx, heads, (E*)A);
+    MT_CHECK_HIP(hipGetLastError());
+    ConvArgs o = gemm_args(l.o, P, B, Tx);
+    o.x0 = A;
+    o.y = Bb;
+    o.resid = X;
+    o.ldr = W;
+    if ((rc = launch_conv<E, 0, EF_RESID>(o, st))) return rc;
+    if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n1_off), eps, nullptr, 0, (E*)A, st))) return rc;
+    ConvArgs f1 = gemm_args(l.f1, P, B, Tx);
+    f1.x0 = A;
+    f1.y = Hh;
+    f1.pmask = xmask;
+    if ((rc = launch_conv<E, PF_MASK, EF_RELU>(f1, st))) return rc;
+    ConvArgs f2 = gemm_args(l.f2, P, B, Tx);
+    f2.x0 = Hh;
+    f2.y = Bb;
+    f2.pmask = xmask;
+    f2.emask = xmask;
+    f2.resid = A;
+    f2.ldr = W;
+    if ((rc = launch_conv<E, PF_MASK, EF_MASK | EF_RESID>(f2, st))) return rc;
+    // LN2, then the next layer's (or the final) x * x_mask
+    if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n2_off), eps, xmask, 0, (E*)X, st))) return rc;
+  }
+  // mu = proj_m(x) * m -> [B][80][Tx] fp32
+  {
+    ConvArgs a = gemm_args(proj_m, P, B, Tx);
+    a.x0 = X;
+    a.y = MU;
+    a.emask = xmask;
+    if ((rc = launch_conv<E, 0, EF_MASK>(a, st))) return rc;
+    if ((rc = btc_to_bct(dtype, MU, 80, 0, B, 80, Tx, mu, st))) return rc;
+  }
+  // duration predictor on x (model.py:217-229: conv -> relu -> LN, twice, then proj(h*m)*m)
+  {
+    ConvArgs a = gemm_args(dp1, P, B, Tx);
+    a.x0 = X;
+    a.y = Hh;
+    a.pmask = xmask;
+    if ((rc = launch_conv<E, PF_MASK, EF_RELU>(a, st))) return rc;
+    if ((rc = rowln<E>((const E*)Hh, (int)n, DF, (const float*)(P + dn1_off), eps, nullptr, 0, (E*)A, st))) return rc;
+    ConvArgs b = gemm_args(dp2, P, B, Tx);
+    b.x0 = A;
+    b.y = Hh;
+    b.pmask = xmask;
+    if ((rc = launch_conv<E, PF_MASK, EF_RELU>(b, st))) return rc;
+    if ((rc = rowln<E>((const E*)Hh, (int)n, DF, (const float*)(P + dn2_off), eps, nullptr, 0, (E*)A, st))) return rc;
+    ConvArgs c = gemm_args(dpp, P, B, Tx);
+    c.x0 = A;
+    c.y = logw;
+    c.ldy = 1;
+    c.pmask = xmask;
+    c.emask = xmask;
+    if ((rc = launch_conv<E, PF_MASK, EF_MASK | EF_OUTF32>(c, st))) return rc;
+  }
+  return 0;
+}
+
+int Encoder::forward(const void* packed, const long long* ids, const long long* xlen, const float* spks, int B, int Tx,
+                     float* mu, float* logw, float* xmask, void* ws, size_t ws_bytes, hipStream_t st) const {
+  MT_REQUIRE(B > 0 && Tx > 0 && ids && xlen && mu && logw && xmask, "encoder: empty input");
+  MT_REQUIRE(W == C || spks, "encoder: multi-speaker model needs spks [B][%d]", spk_dim);
+  MT_REQUIRE(ws_bytes >= workspace_bytes(B, Tx), "encoder: workspace %zu < %zu", ws_bytes, workspace_bytes(B, Tx));
+  if (dtype == BF16)
+    return forward_t<bf16>((const char*)packed, ids, xlen, spks, B, Tx, mu, logw, xmask, (char*)ws, st);
+  return forward_t<float>((const char*)packed, ids, xlen, spks, B, Tx, mu, logw, xmask, (char*)ws, st);
+}
+
+}  // namespace mt

@@ -21,6 +21,10 @@ int btc_to_bct(int dtype, const void* src, int ld, int coff, int B, int C, int T
                hipStream_t st);
 int spk_fill(int dtype, const float* spks, int B, int C, int T, void* dst, int ld, int coff, hipStream_t st);
 int mask_half(const float* m0, int B, int T0, float* m1, hipStream_t st);
+// dst[r][0..C) = src[r][0..C) (row strides ld_src / ld_dst, element type by dtype)
+int copy_rows(int dtype, const void* src, int ld_src, int rows, int C, void* dst, int ld_dst, hipStream_t st);
+// x[r][c] *= mask[r]
+int mask_rows(int dtype, void* x, int rows, int C, const float* mask, hipStream_t st);
 
 int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* emb, hipStream_t st);
 int rowdot(const float* x, int ldx, const float* W, const float* bias, float* y, int ldy, int yoff, int S,

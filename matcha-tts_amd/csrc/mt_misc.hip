@@ -389,4 +389,46 @@ int denorm_crop(const float* z, const float* mean, const float* stdv, int B, int
   return 0;
 }
 
+// ------------------------------------------------------------------------------------
+// row copy / row mask (text encoder: speaker-channel concat model.py:526-527, x * x_mask)
+// ------------------------------------------------------------------------------------
+template <class E>
+__global__ void copy_rows_kernel(const E* __restrict__ src, int lds, int rows, int C, E* __restrict__ dst, int ldd) {
+  const size_t total = (size_t)rows * C;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = i / C, c = i - r * C;
+    dst[r * ldd + c] = src[r * lds + c];
+  }
+}
+template <class E>
+__global__ void mask_rows_kernel(E* __restrict__ x, int rows, int C, const float* __restrict__ m) {
+  const size_t total = (size_t)rows * C;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = i / C;
+    x[i] = from_f<E>(to_f(x[i]) * m[r]);
+  }
+}
+int copy_rows(int dtype, const void* src, int ld_src, int rows, int C, void* dst, int ld_dst, hipStream_t st) {
+  const size_t total = (size_t)rows * C;
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 65535);
+  if (dtype == BF16)
+    hipLaunchKernelGGL(copy_rows_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)src, ld_src, rows, C,
+                       (bf16*)dst, ld_dst);
+  else
+    hipLaunchKernelGGL(copy_rows_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)src, ld_src, rows, C,
+                       (float*)dst, ld_dst);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+int mask_rows(int dtype, void* x, int rows, int C, const float* mask, hipStream_t st) {
+  const size_t total = (size_t)rows * C;
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 65535);
+  if (dtype == BF16)
+    hipLaunchKernelGGL(mask_rows_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (bf16*)x, rows, C, mask);
+  else
+    hipLaunchKernelGGL(mask_rows_kernel<float>, dim3(blocks), dim3(256), 0, st, (float*)x, rows, C, mask);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 }  // namespace mt

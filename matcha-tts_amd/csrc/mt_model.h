@@ -37,6 +37,7 @@ struct GemmW {
   int M = 0, Mpad = 0, taps = 1, cin_pad = 0, gpad = 0, ups = 1, opad = 0;
   std::vector<int> wsrc;  // weight params (several = rows stacked, e.g. Q|K|V)
   int bsrc = -1;          // bias param or -1 (zeros)
+  std::vector<int> bsrcs; // stacked biases, one per weight param (overrides bsrc), e.g. q|k|v
   int ln_g = -1, ln_b = -1;  // LayerNorm (on the input channels) folded into W and bias
   size_t w_off = 0, b_off = 0;
   size_t v_off = 0;  // vconv image [cin/64][taps][Mpad128][64] (bf16 HiFi-GAN convs, mt_vconv.h)
@@ -113,6 +114,44 @@ struct Decoder {
             void* ws, size_t ws_bytes, hipStream_t st) const;
   int step(const void* packed, const float* x, const float* mu_y, const float* mask, const float* spks,
            float t, int B, int T, float* out, void* ws, size_t ws_bytes, hipStream_t st) const;
+};
+
+// -------------------------------------------------------------------------------------
+// Text encoder + duration predictor (model.py:148-535), mt_encoder.hip
+// -------------------------------------------------------------------------------------
+struct Encoder {
+  int n_vocab = 0, C = 192, F = 768, heads = 2, layers = 6, k = 3, n_spks = 1, spk_dim = 0, W = 192;
+  int DF = 256, dpk = 3, prenet = 1, dtype = F32, esize = 4, dk = 96;
+  ParamList params;
+  size_t packed_bytes = 0;
+  int emb = -1;
+  size_t emb_off = 0;
+  struct Pre {
+    GemmW conv;
+    int g, b;
+    size_t ln_off;
+  };
+  std::vector<Pre> pre;
+  GemmW pre_proj;
+  struct Layer {
+    GemmW qkv, o, f1, f2;
+    int n1g, n1b, n2g, n2b;
+    size_t n1_off, n2_off;
+  };
+  std::vector<Layer> lay;
+  GemmW proj_m, dp1, dp2, dpp;
+  int dn1g, dn1b, dn2g, dn2b, theta;
+  size_t dn1_off, dn2_off, theta_off;
+
+  int init(int n_vocab, int n_channels, int filter_channels, int heads, int layers, int kernel, int n_spks,
+           int spk_dim, int dp_filter, int dp_kernel, int prenet, int dtype);
+  int pack(const float* const* p, void* packed, hipStream_t st) const;
+  size_t workspace_bytes(int B, int Tx) const;
+  int forward(const void* packed, const long long* ids, const long long* xlen, const float* spks, int B, int Tx,
+              float* mu, float* logw, float* xmask, void* ws, size_t ws_bytes, hipStream_t st) const;
+  template <class E>
+  int forward_t(const char* P, const long long* ids, const long long* xlen, const float* spks, int B, int Tx,
+                float* mu, float* logw, float* xmask, char* ws, hipStream_t st) const;
 };
 
 // -------------------------------------------------------------------------------------

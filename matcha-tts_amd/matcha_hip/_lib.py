@@ -24,6 +24,16 @@ P = c_void_p  # device pointer / opaque handle
 SIGNATURES = {
     "mt_last_error": (c_char_p, []),
     "mt_abi_version": (c_int, []),
+    "mt_encoder_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                  POINTER(c_void_p)]),
+    "mt_encoder_destroy": (None, [P]),
+    "mt_encoder_num_params": (c_int, [P]),
+    "mt_encoder_param_name": (c_int, [P, c_int, c_char_p, c_int]),
+    "mt_encoder_param_shape": (c_int, [P, c_int, POINTER(c_int64), c_int]),
+    "mt_encoder_packed_bytes": (c_size_t, [P]),
+    "mt_encoder_pack": (c_int, [P, POINTER(c_void_p), P, P]),
+    "mt_encoder_workspace_bytes": (c_size_t, [P, c_int, c_int]),
+    "mt_encoder_forward": (c_int, [P, P, P, P, P, c_int, c_int, P, P, P, P, c_size_t, P]),
     "mt_decoder_create": (c_int, [c_int, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
     "mt_decoder_destroy": (None, [P]),
     "mt_decoder_num_params": (c_int, [P]),

@@ -83,6 +83,75 @@ def sinus_freq(c_cond: int) -> torch.Tensor:
     return torch.exp(torch.arange(half).float() * -e)
 
 
+def rope_theta(head_dim: int) -> torch.Tensor:
+    """model.py:258-265 theta table, formed exactly as the reference does (fp32, CPU)."""
+    d = int(head_dim * 0.5)
+    return 1.0 / (10_000 ** (torch.arange(0, d, 2).float() / d))
+
+
+class EncoderEngine:
+    """mt_encoder handle: text encoder + duration predictor (model.py:452-535) for one config/dtype."""
+
+    def __init__(self, n_vocab: int, n_channels: int, filter_channels: int, n_heads: int, n_layers: int,
+                 kernel_size: int, n_spks: int, spk_emb_dim: int, dp_filter: int, dp_kernel: int, prenet: bool,
+                 precision: str):
+        self.dtype = dtype_code(precision)
+        self.width = n_channels + (spk_emb_dim if n_spks > 1 else 0)
+        self.head_dim = self.width // n_heads
+        h = c_void_p()
+        check(lib().mt_encoder_create(n_vocab, n_channels, filter_channels, n_heads, n_layers, kernel_size, n_spks,
+                                      spk_emb_dim, dp_filter, dp_kernel, int(bool(prenet)), self.dtype, byref(h)),
+              "encoder_create")
+        self.h = h
+        self.specs = _param_list(h, "mt_encoder_num_params", "mt_encoder_param_name", "mt_encoder_param_shape")
+        self.packed_bytes = lib().mt_encoder_packed_bytes(h)
+        self._packed = None
+        self._fp = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().mt_encoder_destroy(self.h)
+        except Exception:
+            pass
+
+    def pack(self, params: Dict[str, torch.Tensor], device: torch.device) -> torch.Tensor:
+        """params: TextEncoder-relative reference keys -> tensors."""
+        tensors = []
+        for name, shape in self.specs:
+            t = rope_theta(self.head_dim) if name == "_rope_theta" else params.get(name)
+            if t is None:
+                raise KeyError(f"text encoder parameter {name!r} missing")
+            if tuple(t.shape) != shape:
+                raise ValueError(f"{name}: shape {tuple(t.shape)} != expected {shape}")
+            tensors.append(t)
+        fp = fingerprint([t for (n, _), t in zip(self.specs, tensors) if n != "_rope_theta"]) + (str(device),)
+        if self._packed is not None and fp == self._fp:
+            return self._packed
+        dev = [t.detach().to(device=device, dtype=torch.float32).contiguous() for t in tensors]
+        packed = torch.empty(self.packed_bytes, dtype=torch.uint8, device=device)
+        arr = (c_void_p * len(dev))(*[t.data_ptr() for t in dev])
+        check(lib().mt_encoder_pack(self.h, arr, packed.data_ptr(), stream_handle(device)), "encoder_pack")
+        torch.cuda.current_stream(device).synchronize()  # staging copies die with `dev`
+        self._packed, self._fp = packed, fp
+        return packed
+
+    def forward(self, packed, x: torch.Tensor, x_lengths: torch.Tensor, spks: Optional[torch.Tensor] = None):
+        """x int64 [B,Tx], x_lengths int64 [B] -> mu [B,80,Tx], logw [B,1,Tx], x_mask [B,1,Tx] (fp32)."""
+        x = x.to(torch.int64).contiguous()
+        xl = x_lengths.to(torch.int64).contiguous()
+        B, Tx = x.shape
+        dev = x.device
+        mu = torch.empty(B, 80, Tx, dtype=torch.float32, device=dev)
+        logw = torch.empty(B, 1, Tx, dtype=torch.float32, device=dev)
+        x_mask = torch.empty(B, 1, Tx, dtype=torch.float32, device=dev)
+        L = lib()
+        ws = _Workspace.get(L.mt_encoder_workspace_bytes(self.h, B, Tx), dev)
+        check(L.mt_encoder_forward(self.h, packed.data_ptr(), ptr(x), ptr(xl), ptr(spks), B, Tx, ptr(mu), ptr(logw),
+                                   ptr(x_mask), ws.data_ptr(), ws.numel(), stream_handle(dev)), "encoder_forward")
+        return mu, logw, x_mask
+
+
 class DecoderEngine:
     """mt_decoder handle: U-Net estimator + CFM solver for one (c_cond, dtype)."""
 

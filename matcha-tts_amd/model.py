@@ -228,8 +228,10 @@ class TextEncoder(nn.Module):
     """model.py:452-535 -> (mu [B,n_feats,Tx], logw [B,1,Tx], x_mask [B,1,Tx])."""
 
     def __init__(self, encoder_type, encoder_params, duration_predictor_params, n_vocab, n_spks=1,
-                 spk_emb_dim=128):
+                 spk_emb_dim=128, precision: str = "fp32"):
         super().__init__()
+        self.precision = precision
+        self._engines = {}
         self.encoder_type = encoder_type
         self.n_vocab = n_vocab
         self.n_feats = _get(encoder_params, "n_feats")
@@ -251,16 +253,30 @@ class TextEncoder(nn.Module):
                                         _get(duration_predictor_params, "kernel_size"),
                                         _get(duration_predictor_params, "p_dropout"))
 
+    # ---- HIP plumbing (mt_encoder: the whole forward below is one C-ABI call) ----
+    def set_precision(self, precision: str):
+        rt.dtype_code(precision)
+        self.precision = precision
+        return self
+
+    def engine(self) -> rt.EncoderEngine:
+        if self.precision not in self._engines:
+            enc = self.encoder
+            self._engines[self.precision] = rt.EncoderEngine(
+                self.n_vocab, self.n_channels, enc.ffn_layers[0].conv_1.out_channels, enc.attn_layers[0].n_heads,
+                enc.n_layers, enc.ffn_layers[0].conv_1.kernel_size[0], self.n_spks, self.spk_emb_dim,
+                self.proj_w.conv_1.out_channels, self.proj_w.conv_1.kernel_size[0], isinstance(self.prenet, nn.Module),
+                self.precision)
+        return self._engines[self.precision]
+
     def forward(self, x, x_lengths, spks=None):
-        h = (self.emb(x) * math.sqrt(self.n_channels)).transpose(1, -1)
-        x_mask = sequence_mask(x_lengths, h.size(2)).unsqueeze(1).to(h.dtype)
-        h = self.prenet(h, x_mask)
-        if self.n_spks > 1:
-            h = torch.cat([h, spks.unsqueeze(-1).expand(-1, -1, h.shape[-1])], dim=1)
-        h = self.encoder(h, x_mask)
-        mu = self.proj_m(h) * x_mask
-        logw = self.proj_w(h.detach(), x_mask)
-        return mu, logw, x_mask
+        """model.py:503-535 on the GPU -> (mu [B,80,Tx], logw [B,1,Tx], x_mask [B,1,Tx]) fp32."""
+        rt.require_gpu(x, x_lengths, spks, what="TextEncoder.forward")
+        if self.n_spks > 1 and spks is None:
+            raise ValueError("multi-speaker TextEncoder needs spks [B, spk_emb_dim]")
+        eng = self.engine()
+        packed = eng.pack({k: v for k, v in self.state_dict(keep_vars=True).items()}, x.device)
+        return eng.forward(packed, x, x_lengths, rt.f32c(spks))
 
 
 # ======================================================================================
@@ -493,7 +509,7 @@ class MatchaTTS(nn.Module):
         self.register_buffer("mel_mean", torch.tensor(0.0))
         self.register_buffer("mel_std", torch.tensor(1.0))
         self.encoder = TextEncoder(_get(encoder_params, "encoder_type"), encoder_params, duration_predictor_params,
-                                   n_vocab, n_spks, spk_emb_dim)
+                                   n_vocab, n_spks, spk_emb_dim, precision=precision)
         n_feats = _get(encoder_params, "n_feats")
         dec_in = 2 * n_feats + (spk_emb_dim if n_spks > 1 else 0)
         est = Decoder(in_channels=dec_in, out_channels=n_feats, channels=_get(decoder_params, "channels"),
@@ -508,6 +524,7 @@ class MatchaTTS(nn.Module):
     def set_precision(self, precision: str):
         """'fp32' (parity mode, default) or 'bf16' (bf16 MFMA, fp32 accumulate)."""
         self.decoder.estimator.set_precision(precision)
+        self.encoder.set_precision(precision)
         return self
 
     def forward(self, x, x_lengths, y, y_lengths, spks=None):

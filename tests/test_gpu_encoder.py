@@ -1,0 +1,86 @@
+"""Text encoder + duration predictor on the MI355X (mt_encoder) against the CPU
+oracle (oracle/matcha_oracle.py:text_encoder, pinned to the reference by tests/golden/g6_*).
+
+fp32 parity mode: mu / logw max-abs <= 1e-4, x_mask exact. bf16: rel-RMS <= 2e-2.
+Cases: LJ (single speaker) and VCTK (spk-embedding channels), ragged lengths including a length-1
+utterance, Tx crossing the attention kernel's 64-key chunks, B = 1.
+"""
+import math
+
+import pytest
+import torch
+
+from conftest import HP, make_matcha, rel_rms
+from matcha_hip import synthetic
+from oracle import matcha_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _model(n_spks, precision, seed):
+    m = make_matcha(n_spks, precision)
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(
+        [(k, tuple(v.shape)) for k, v in m.state_dict().items()], seed).items()}
+    m.load_state_dict(sd)
+    return m.to(DEV).eval(), sd
+
+
+def _inputs(lengths, seed):
+    g = torch.Generator().manual_seed(seed)
+    Tx = max(lengths)
+    x = torch.randint(1, 178, (len(lengths), Tx), generator=g)
+    xl = torch.tensor(lengths, dtype=torch.int64)
+    for i, n in enumerate(lengths):
+        x[i, n:] = 0
+    return x, xl
+
+
+CASES = [
+    ("lj", 1, [37, 12, 1]),
+    ("lj_chunks", 1, [130, 65, 64]),
+    ("vctk", 4, [50, 23]),
+    ("lj_b1", 1, [9]),
+]
+
+
+@pytest.mark.parametrize("name,n_spks,lengths", CASES, ids=[c[0] for c in CASES])
+def test_text_encoder_fp32_matches_oracle(name, n_spks, lengths):
+    m, sd = _model(n_spks, "fp32", 11 + n_spks)
+    x, xl = _inputs(lengths, len(lengths) * 7 + n_spks)
+    spks = torch.randn(len(lengths), 64, generator=torch.Generator().manual_seed(5)) if n_spks > 1 else None
+    mu, logw, xm = m.encoder(x.to(DEV), xl.to(DEV), None if spks is None else spks.to(DEV))
+    torch.cuda.synchronize()
+    hp = dict(HP, n_spks=n_spks)
+    sub = {k[len("encoder."):]: v for k, v in sd.items() if k.startswith("encoder.")}
+    mu_o, logw_o, xm_o = O.text_encoder(sub, x, xl, hp, spks)
+    assert torch.equal(xm.cpu(), xm_o)
+    e_mu = (mu.cpu() - mu_o).abs().max().item()
+    e_w = (logw.cpu() - logw_o).abs().max().item()
+    assert e_mu < 1e-4 and e_w < 1e-4, (e_mu, e_w)
+
+
+def test_text_encoder_bf16_close():
+    m, sd = _model(1, "bf16", 21)
+    x, xl = _inputs([80, 41, 7], 3)
+    mu, logw, _ = m.encoder(x.to(DEV), xl.to(DEV))
+    sub = {k[len("encoder."):]: v for k, v in sd.items() if k.startswith("encoder.")}
+    mu_o, logw_o, _ = O.text_encoder(sub, x, xl, dict(HP, n_spks=1))
+    assert rel_rms(mu.cpu(), mu_o) < 2e-2
+    assert rel_rms(logw.cpu(), logw_o) < 2e-2
+
+
+def test_text_encoder_forced_duration_head_exact():
+    """With the bench's forced duration head (proj weight 0, bias ln 2.5) logw is exactly
+    ln(2.5) * x_mask in every precision, so the index path downstream is exact."""
+    for precision in ("fp32", "bf16"):
+        m = make_matcha(1, precision)
+        sd = {k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(
+            [(k, tuple(v.shape)) for k, v in m.state_dict().items()], 3,
+            force_log_duration=math.log(2.5)).items()}
+        m.load_state_dict(sd)
+        m = m.to(DEV).eval()
+        x, xl = _inputs([40, 17], 9)
+        _, logw, xm = m.encoder(x.to(DEV), xl.to(DEV))
+        ref = torch.full_like(logw, math.log(2.5)) * xm
+        assert torch.equal(logw, ref.to(torch.float32)), precision
