@@ -74,63 +74,79 @@ __global__ __launch_bounds__(256) void rowln_kernel(const E* __restrict__ x, int
 }
 
 // ---------------------------------------------------------------------------------------
-// RoPE multi-head self-attention (model.py:343-364, RotaryPositionalEmebeddings :244-292).
-// qkv [B][Tx][3W] (q | k | v, head h = channels h*dk .. h*dk+dk-1), out [B][Tx][W].
+// RoPE (RotaryPositionalEmebeddings.forward, model.py:276-290) applied in place to the q and k parts of
+// qkv [B][Tx][3W]: for head h, pair (i, i + d/2) of the first d = dk/2 dims, angle t * theta_i
+// (the cached cos/sin table, idx_theta2 = [idx_theta, idx_theta]); x_rope*cos + neg_half(x_rope)*sin.
+// ---------------------------------------------------------------------------------------
+template <class E>
+__global__ void rope_kernel(E* __restrict__ qkv, int rows, int Tx, int W, int heads, int dk,
+                            const float* __restrict__ theta) {
+  const int hr = dk / 4;
+  const size_t total = (size_t)rows * 2 * heads * hr;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e % hr);
+    size_t r = e / hr;
+    const int h = (int)(r % heads);
+    r /= heads;
+    const int part = (int)(r % 2);
+    const size_t row = r / 2;
+    const int t = (int)(row % Tx);
+    E* x = qkv + row * 3 * W + part * W + h * dk;
+    const float ang = (float)t * theta[i];
+    const float cs = cosf(ang), sn = sinf(ang);
+    const float a = to_f(x[i]), b = to_f(x[i + hr]);
+    x[i] = from_f<E>(a * cs - b * sn);
+    x[i + hr] = from_f<E>(b * cs + a * sn);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Multi-head self-attention core (MultiHeadAttention.attention, model.py:343-364) on RoPE'd qkv.
 // Workgroup = 64 queries x 4 lanes of one (utterance, head); lane p of a query owns dk/4 dims of q and
-// of its output. Keys stream through LDS 64 at a time, RoPE applied while staging (angle t*theta_i on
-// the pair (i, i + d/2) of the first d = dk/2 dims, the cached cos/sin table of the reference), then
-// scores = q.k / sqrt(dk) with masked pairs := -1e4 and an online softmax over all Tx keys.
+// of its output. Keys stream through LDS 64 at a time; scores = q.k / sqrt(dk), masked (query, key)
+// pairs := -1e4 (x_mask_i * x_mask_j == 0), online softmax over all Tx keys, out [B][Tx][W].
 // ---------------------------------------------------------------------------------------
 template <class E, int DK>
 __global__ __launch_bounds__(256) void enc_attn_kernel(const E* __restrict__ qkv, const float* __restrict__ xmask,
-                                                       const float* __restrict__ theta, float inv_scale_div,
-                                                       int Tx, int heads, E* __restrict__ out) {
-  constexpr int DR = DK / 2, HR = DR / 2, DP = DK / 4;  // rope dims, half of them, dims per lane
-  constexpr int KS = DK + 1;                             // padded LDS row (floats)
-  __shared__ float Ks[64 * KS], Vs[64 * KS], Qs[64 * KS];
+                                                       float sdiv, int Tx, int heads, E* __restrict__ out) {
+  constexpr int DP = DK / 4;   // dims per lane
+  constexpr int KS = DK + 4;   // LDS row (floats): 16-byte aligned, rows offset by 4 banks
+  __shared__ __attribute__((aligned(16))) float Ks[64 * KS];
+  __shared__ __attribute__((aligned(16))) float Vs[64 * KS];
   __shared__ float km[64];
   const int tid = threadIdx.x;
   const int qi = tid >> 2, p = tid & 3;
   const int h = blockIdx.y, b = blockIdx.z;
   const int t0 = blockIdx.x * 64;
   const int W = heads * DK, ld = 3 * W;
-  const E* base = qkv + (size_t)b * Tx * ld;
+  const E* base = qkv + (size_t)b * Tx * ld + h * DK;
 
-  // stage one 64-row block of q or k (RoPE applied) or v into an LDS tile
-  auto stage = [&](float* dst, int r0, int part, bool rope) {
-    for (int e = tid; e < 64 * DK; e += 256) {
-      const int r = e / DK, d = e - r * DK;
-      const int t = r0 + r;
-      float v = 0.f;
-      if (t < Tx) {
-        const E* src = base + (size_t)t * ld + part * W + h * DK;
-        v = to_f(src[d]);
-        if (rope && d < DR) {
-          const int i = d < HR ? d : d - HR;
-          const float ang = (float)t * theta[i];
-          const float cs = cosf(ang), sn = sinf(ang);
-          const float other = to_f(src[d < HR ? d + HR : d - HR]);
-          v = d < HR ? v * cs - other * sn : v * cs + other * sn;
-        }
-      }
-      dst[r * KS + d] = v;
-    }
-  };
-  stage(Qs, t0, 0, true);
-  __syncthreads();
-  float q[DP], o[DP];
-#pragma unroll
-  for (int i = 0; i < DP; ++i) {
-    q[i] = Qs[qi * KS + p * DP + i];
-    o[i] = 0.f;
-  }
   const int tq = t0 + qi;
+  float q[DP], o[DP];
+  {
+    const E* src = base + (size_t)min(tq, Tx - 1) * ld + p * DP;
+#pragma unroll
+    for (int i = 0; i < DP; ++i) {
+      q[i] = to_f(src[i]);
+      o[i] = 0.f;
+    }
+  }
   const float mq = tq < Tx ? xmask[(size_t)b * Tx + tq] : 0.f;
   float mrun = -INFINITY, lrun = 0.f;
   for (int k0 = 0; k0 < Tx; k0 += 64) {
     __syncthreads();
-    stage(Ks, k0, 1, true);
-    stage(Vs, k0, 2, false);
+    for (int e = tid; e < 64 * DK; e += 256) {
+      const int r = e / DK, d = e - r * DK;
+      const int t = k0 + r;
+      float kv = 0.f, vv = 0.f;
+      if (t < Tx) {
+        const E* src = base + (size_t)t * ld + d;
+        kv = to_f(src[W]);
+        vv = to_f(src[2 * W]);
+      }
+      Ks[r * KS + d] = kv;
+      Vs[r * KS + d] = vv;
+    }
     if (tid < 64) km[tid] = k0 + tid < Tx ? xmask[(size_t)b * Tx + k0 + tid] : 0.f;
     __syncthreads();
     const int nk = min(64, Tx - k0);
@@ -138,12 +154,16 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const E* __restrict__ qkv
     float cmax = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 64; ++j) {
+      const f32x4* kr = reinterpret_cast<const f32x4*>(Ks + j * KS + p * DP);
       float d = 0.f;
 #pragma unroll
-      for (int i = 0; i < DP; ++i) d += q[i] * Ks[j * KS + p * DP + i];
+      for (int i = 0; i < DP / 4; ++i) {
+        const f32x4 kk = kr[i];
+        d += q[4 * i] * kk[0] + q[4 * i + 1] * kk[1] + q[4 * i + 2] * kk[2] + q[4 * i + 3] * kk[3];
+      }
       d += __shfl_xor(d, 1, 64);
       d += __shfl_xor(d, 2, 64);
-      float sc = d / inv_scale_div;
+      float sc = d / sdiv;
       if (mq * km[j] == 0.f) sc = -1e4f;
       s[j] = j < nk ? sc : -INFINITY;
       cmax = fmaxf(cmax, s[j]);
@@ -157,8 +177,15 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const E* __restrict__ qkv
     for (int j = 0; j < 64; ++j) {
       const float pj = expf(s[j] - mnew);
       lrun += pj;
+      const f32x4* vr = reinterpret_cast<const f32x4*>(Vs + j * KS + p * DP);
 #pragma unroll
-      for (int i = 0; i < DP; ++i) o[i] += pj * Vs[j * KS + p * DP + i];
+      for (int i = 0; i < DP / 4; ++i) {
+        const f32x4 vv = vr[i];
+        o[4 * i] += pj * vv[0];
+        o[4 * i + 1] += pj * vv[1];
+        o[4 * i + 2] += pj * vv[2];
+        o[4 * i + 3] += pj * vv[3];
+      }
     }
     mrun = mnew;
   }
@@ -393,16 +420,20 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
     q.x0 = X;
     q.y = Q;
     if ((rc = launch_conv<E, 0, 0>(q, st))) return rc;
+    {
+      const size_t pairs = n * 2 * heads * (dk / 4);
+      const int blocks = (int)std::min<size_t>((pairs + 255) / 256, 65535);
+      hipLaunchKernelGGL((rope_kernel<E>), dim3(blocks), dim3(256), 0, st, (E*)Q, (int)n, Tx, W, heads, dk,
+                         (const float*)(P + theta_off));
+      MT_CHECK_HIP(hipGetLastError());
+    }
     const dim3 ga((Tx + 63) / 64, heads, B);
     if (dk == 96)
-      hipLaunchKernelGGL((enc_attn_kernel<E, 96>), ga, dim3(256), 0, st, (const E*)Q, xmask,
-                         (const float*)(P + theta_off), sdiv, Tx, heads, (E*)A);
+      hipLaunchKernelGGL((enc_attn_kernel<E, 96>), ga, dim3(256), 0, st, (const E*)Q, xmask, sdiv, Tx, heads, (E*)A);
     else if (dk == 128)
-      hipLaunchKernelGGL((enc_attn_kernel<E, 128>), ga, dim3(256), 0, st, (const E*)Q, xmask,
-                         (const float*)(P + theta_off), sdiv, Tx, heads, (E*)A);
+      hipLaunchKernelGGL((enc_attn_kernel<E, 128>), ga, dim3(256), 0, st, (const E*)Q, xmask, sdiv, Tx, heads, (E*)A);
     else
-      hipLaunchKernelGGL((enc_attn_kernel<E, 64>), ga, dim3(256), 0, st, (const E*)Q, xmask,
-                         (const float*)(P + theta_off), sdiv, Tx, heads, (E*)A);
+      hipLaunchKernelGGL((enc_attn_kernel<E, 64>), ga, dim3(256), 0, st, (const E*)Q, xmask, sdiv, Tx, heads, (E*)A);
     MT_CHECK_HIP(hipGetLastError());
     ConvArgs o = gemm_args(l.o, P, B, Tx);
     o.x0 = A;
