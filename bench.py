@@ -109,35 +109,47 @@ def step(m, g, den, x, xl, n_ts, denoise):
 
 
 def roofline(probe, precision):
-    """Dominant kernel of the step: the fused 64-channel HiFi-GAN ResBlock stage (mt_rbfuse,
-    stage 3 of v1: 3 resblocks x 3 pairs of 64x64 convs, k 3/7/11, on B x 128*T_y frames), timed by
-    HIP events recorded on its own stream around each of its launches INSIDE the timed region
-    (mt_probe_*). Algorithmic FLOPs per launch = 2 * 6 * 64 * 64 * (3+7+11) * B * 128 * T_y; its
-    algorithmic bytes = stage input + output (B * 128 * T_y * 64 * 2 B each) + weights. MFMA-bound
-    (intensity ~2,000 FLOP/B), so the peak is the dense bf16 MFMA rate. `traffic` is the HBM bytes
-    per launch measured with rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, committed
-    in profiles/r01_pmc_rbfuse64.json by tools_pmc.sh on this same bench command."""
+    """Dominant kernel of the step: mt_vconv, the LDS-DMA persistent implicit-GEMM conv that runs every
+    ResBlock conv of HiFi-GAN stages 1-3 (54 launches per step: 3 stages x 3 resblocks x 3 pairs x
+    2 convs; C = 256/128/64 on B x 8/64/128 * T_y frames, k = 3/7/11). Timed by HIP events recorded on
+    its launch stream around each of its launches INSIDE the timed region (mt_probe_*, site
+    PROBE_VCONV). Per launch: algorithmic FLOPs = 2 * C_out * C_in * k * B * L; algorithmic bytes =
+    input + output (+ residual, + accumulator, + activated copy) activations of B * L frames x C
+    channels in bf16, + weights (mt_vconv.hip launch_vconv). The family's intensity decides the bound:
+    below the bf16 ridge (2.5 PFLOP/s / 8 TB/s = 312.5 FLOP/B) it is HBM-bound and `achieved` is
+    algorithmic GB/s, above it MFMA-bound and `achieved` is TFLOP/s. `traffic` = HBM bytes per launch
+    from rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE on this same bench command
+    (profiles/r02_pmc_vconv.json, tools_round_profile.sh)."""
     if probe is None or probe["launches"] == 0:
-        return {"bound": "mfma", "achieved": None, "peak": 2500.0, "unit": "TFLOP/s", "frac": None,
-                "traffic": None, "kernel": "rbfuse_kernel<bf16,64> (bf16 path only)"}
+        return {"bound": "hbm", "achieved": None, "peak": 8000.0, "unit": "GB/s", "frac": None,
+                "traffic": None, "kernel": "vconv_kernel (bf16 path only)"}
     n = probe["launches"]
     ms = probe["ms"] / n
     flops = probe["flops"] / n
-    achieved = flops / (ms * 1e-3) / 1e12
-    peak = 2500.0  # dense bf16 MFMA TFLOP/s (MI355X_MICROARCH.md)
+    nbytes = probe["bytes"] / n
+    intensity = flops / nbytes
+    tflops = flops / (ms * 1e-3) / 1e12
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    peak_f, peak_b = 2500.0, 8000.0  # dense bf16 MFMA TFLOP/s, HBM GB/s (MI355X_MICROARCH.md)
+    ridge = peak_f * 1e12 / (peak_b * 1e9)
     traffic = None
-    pmc = os.path.join(HERE, "profiles", "r01_pmc_rbfuse64.json")
+    pmc = os.path.join(HERE, "profiles", "r02_pmc_vconv.json")
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+    if intensity >= ridge:
+        bound, achieved, peak, unit = "mfma", tflops, peak_f, "TFLOP/s"
+    else:
+        bound, achieved, peak, unit = "hbm", gbs, peak_b, "GB/s"
+    return {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": traffic,
-            "kernel": "rbfuse_kernel<bf16,64,192> fused HiFi-GAN stage-3 ResBlocks (64 ch)",
+            "kernel": "vconv_kernel<bf16> LDS-DMA implicit-GEMM conv, HiFi-GAN stage 1-3 ResBlock convs",
             "launches": n, "launch_ms": round(ms, 4), "flops_per_launch": flops,
-            "algo_bytes_per_launch": probe["bytes"] / n,
-            "intensity_flop_per_byte": round(flops / (probe["bytes"] / n), 1)}
+            "algo_bytes_per_launch": nbytes, "intensity_flop_per_byte": round(intensity, 1),
+            "tflops": round(tflops, 2), "mfma_frac": round(tflops / peak_f, 4),
+            "gbs": round(gbs, 1), "hbm_frac": round(gbs / peak_b, 4)}
 
 
 def cpu_baseline(m_sd, g_sd, x, xl, n_ts, seconds):
@@ -202,7 +214,7 @@ def main():
         torch.cuda.synchronize()
 
     from matcha_hip import runtime as rt
-    rt.probe_start(rt.PROBE_RBFUSE_C64, 4 * a.steps)
+    rt.probe_start(rt.PROBE_VCONV, 64 * a.steps)
     barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):

@@ -119,11 +119,12 @@ size_t mt_vocoder_packed_bytes(const mt_vocoder* v);
 /* fused ResBlock stages for the 32/64-channel stages in bf16 (default on; bit-identical to the
  * per-layer path, which 0 selects) */
 int mt_vocoder_set_fusion(mt_vocoder* v, int enable);
-/* LDS-DMA persistent convs (mt_vconv) for the wide (C % 128 == 0) bf16 ResBlock1 stages: inputs
- * pre-activated by their producers, same rounding points as the generic per-layer path (default on;
- * 0 selects the generic per-layer kernel). Replaces the same convs as mt_vocoder_forward
- * (hifigan/models.py:90-97, 187-192). */
-int mt_vocoder_set_vconv(mt_vocoder* v, int enable);
+/* LDS-DMA persistent convs (mt_vconv) for the bf16 ResBlock1 stages with C % 64 == 0: inputs
+ * pre-activated by their producers, same rounding points as the generic per-layer path. mode 1:
+ * the stages the fused ResBlock kernel does not serve (C = 128, 256); mode 2 (default, measured
+ * faster): also the 64-channel stage instead of the fused kernel; 0: the generic per-layer kernel. Replaces the same
+ * convs as mt_vocoder_forward (hifigan/models.py:90-97, 187-192). */
+int mt_vocoder_set_vconv(mt_vocoder* v, int mode);
 int mt_vocoder_pack(const mt_vocoder* v, const float* const* params, void* packed, void* stream);
 size_t mt_vocoder_workspace_bytes(const mt_vocoder* v, int B, int T);
 /* mel [B,80,T] fp32 -> wav [B,1,T*prod(up_rates)] fp32 */

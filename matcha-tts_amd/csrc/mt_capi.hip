@@ -173,7 +173,7 @@ int mt_vocoder_set_fusion(mt_vocoder* v, int enable) {
 }
 int mt_vocoder_set_vconv(mt_vocoder* v, int enable) {
   MT_REQUIRE(v, "null vocoder");
-  v->v.vconv = enable ? 1 : 0;
+  v->v.vconv = enable < 0 ? 0 : enable;
   return 0;
 }
 size_t mt_vocoder_packed_bytes(const mt_vocoder* v) { return v ? v->v.packed_bytes : 0; }

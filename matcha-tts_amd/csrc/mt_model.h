@@ -160,7 +160,7 @@ struct Encoder {
 struct Vocoder {
   int resblock = 1, dtype = BF16, esize = 2;
   int fuse = 1;  // fused ResBlock stages (mt_rbfuse) where supported
-  int vconv = 1; // LDS-DMA persistent convs (mt_vconv) for the wide bf16 ResBlock stages
+  int vconv = 2; // LDS-DMA persistent convs (mt_vconv): 1 = C >= 128 stages, 2 = also C = 64 (per layer)
   size_t zero_off = 0;  // 256 zero bytes in the packed buffer (vconv padding rows)
   bool any_vc = false;
   std::vector<int> up_rates, up_kernels, rb_kernels;

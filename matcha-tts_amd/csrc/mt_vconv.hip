@@ -29,17 +29,27 @@
 namespace mt {
 
 namespace {
-constexpr int BM = 128, BN = 256, NT = 512;
-constexpr int WSLOT = BM * 128;                   // 16 KiB: 128 rows x 64 bf16 channels
+constexpr int BN = 256, NT = 512;
 constexpr int NWSLOT = 4;                         // weight ring depth (3 steps in flight)
 constexpr int XROWS = 320;                        // >= BN + (taps - 1) * dil
 constexpr int XBUF = XROWS * 128;                 // 40 KiB per chunk buffer
 constexpr int MMAX = 512;                         // largest C_out (bias staged in LDS)
-constexpr int BIAS_OFF = NWSLOT * WSLOT + 2 * XBUF;
-constexpr int LDS_BYTES = BIAS_OFF + MMAX * 4;     // 146 KiB
 constexpr int NXW = XROWS / 8 / 8;                // X wave-instructions per wave per chunk
-constexpr int NWW = BM / 8 / 8;                   // W wave-instructions per wave per step
-static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+constexpr int BMP = 64;                           // packed weight rows are padded to a multiple of this
+// Tile geometry by output rows per workgroup: BM = 128 (waves 2 in M x 4 in N, 64x64 per wave) for
+// C_out % 128 == 0, BM = 64 (1 x 8 waves, 64x32 per wave) for the 64-channel stage.
+template <int BM_>
+struct VT {
+  static constexpr int BM = BM_;
+  static constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
+  static constexpr int WNC = BN / WAVES_N;        // frames per wave
+  static constexpr int FN = WNC / 16;             // 16-frame fragments per wave
+  static constexpr int WSLOT = BM * 128;          // BM rows x 64 bf16 channels
+  static constexpr int NWW = BM / 64;             // W wave-instructions per wave per step
+  static constexpr int BIAS_OFF = NWSLOT * WSLOT + 2 * XBUF;
+  static constexpr int LDS_BYTES = BIAS_OFF + MMAX * 4;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
 }  // namespace
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
@@ -124,12 +134,15 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int EF>
+template <int EF, int BMT>
 __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  using TT = VT<BMT>;
+  constexpr int BM = TT::BM, WSLOT = TT::WSLOT, NWW = TT::NWW, BIAS_OFF = TT::BIAS_OFF, FN = TT::FN;
+  constexpr int WNC = TT::WNC;
+  __shared__ __attribute__((aligned(1024))) char smem[TT::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave % TT::WAVES_M, wn = wave / TT::WAVES_M;
   const int taps = a.taps, dil = a.dil, L = a.L, cin = a.cin;
   const int nch = cin >> 6;
   const int S = nch * taps;
@@ -183,11 +196,11 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][FN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int g4 = lane >> 4, l16 = lane & 15;
   // Epilogue I/O is 16 bytes per lane: blocks X = (fm, fn) and Y = (fm + 1, fn) hold, per lane, 4
@@ -203,7 +216,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int ch16 = wm * 64 + (g4 & 1) * 16 + (g4 >> 1) * 8;  // + fm * 16 (fm even): this lane's 8 channels
   // residual / accumulator values of the tile, 16 B per lane: loaded at the start of the tile's last
   // step, consumed after its MFMAs
-  u32x4 rv[2][4], yv[2][4];
+  u32x4 rv[2][FN], yv[2][FN];
   auto epi_loads = [&](int ti) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
@@ -211,8 +224,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
-      for (int fn = 0; fn < 4; ++fn) {
-        const int n = min(n0 + wn * 64 + fn * 16 + l16, L - 1);  // clamped: no per-block branch
+      for (int fn = 0; fn < FN; ++fn) {
+        const int n = min(n0 + wn * WNC + fn * 16 + l16, L - 1);  // clamped: no per-block branch
         const size_t o = (rowbase + n) * a.M + m0 + ch16 + fp * 32;
         if constexpr ((EF & VE_RESID) != 0) rv[fp][fn] = *reinterpret_cast<const u32x4*>(a.resid + o);
         if constexpr ((EF & VE_ACCUM) != 0) yv[fp][fn] = *reinterpret_cast<const u32x4*>(a.y + o);
@@ -220,7 +233,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   };
   // Every lane stores (frames past L go to a trash line), so the store count per tile is a constant the
   // vmcnt bookkeeping can add: NST younger VMEM operations the next steps' waits may leave in flight.
-  constexpr int NST = 8 * ((EF & VE_DUAL) ? 2 : 1);
+  constexpr int NST = 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
   auto bf2 = [](uint32_t w, int i) -> float { return __uint_as_float(i ? (w & 0xffff0000u) : (w << 16)); };
   auto pack2 = [](bf16 lo, bf16 hi) -> uint32_t {
     return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
@@ -232,7 +245,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
-      for (int fn = 0; fn < 4; ++fn) {
+      for (int fn = 0; fn < FN; ++fn) {
         // residual / old accumulator of blocks X (fm = 2fp) and Y (fm = 2fp+1) back in accumulator layout
         uint32_t rx0 = 0, rx1 = 0, ry0 = 0, ry1 = 0, yx0 = 0, yx1 = 0, yy0 = 0, yy1 = 0;
         if constexpr ((EF & VE_RESID) != 0) {
@@ -272,7 +285,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
         }
         swap16(o1[0][0], o1[1][0]);
         swap16(o1[0][1], o1[1][1]);
-        const int n = n0 + wn * 64 + fn * 16 + l16;
+        const int n = n0 + wn * WNC + fn * 16 + l16;
         const bool ok = n < L;
         const size_t o = (rowbase + n) * a.M + m0 + ch16 + fp * 32;
         *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
@@ -322,33 +335,33 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
 
   // Fragments of one K-slice (ks) of a step: 4 A (weights) + 4 B (frames) x 16 bytes per lane.
   struct Frag {
-    bf16x8 A[4], B[4];
+    bf16x8 A[4], B[FN];
   };
   const int ha = l16 & 6;
   auto read_frag = [&](Frag& F, int ks, int slot, int xbuf, int tap) {
     const char* pa = smem + slot * WSLOT + (wm * 64 + l16) * 128;
-    const int rb0 = wn * 64 + l16 + tap * dil;
+    const int rb0 = wn * WNC + l16 + tap * dil;
     const int hb = rb0 & 6;
     const char* pb = smem + NWSLOT * WSLOT + xbuf * XBUF + rb0 * 128;
     const int oa = ((ks * 4 + g4) ^ ha) * 16, ob = ((ks * 4 + g4) ^ hb) * 16;
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048 + oa);
-      F.B[f] = *reinterpret_cast<const bf16x8*>(pb + f * 2048 + ob);
-    }
+    for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048 + oa);
+#pragma unroll
+    for (int f = 0; f < FN; ++f) F.B[f] = *reinterpret_cast<const bf16x8*>(pb + f * 2048 + ob);
   };
   // 16 MFMAs of one K-slice with the 8 reads of another slice interleaved, one per MFMA issue slot
   auto mma_slice = [&](const Frag& F) {
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-      for (int fn = 0; fn < 4; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+    constexpr int NR = 4 + FN, NMF = 4 * FN;  // reads of the other slice, MFMAs of this one
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NR; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF - NR, 0);
   };
 
   // ---- prologue: rows of chunk 0, weights of steps 0..2, K-slice 0 of step 0 ----
@@ -394,7 +407,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         ++ti;
       }
     }
@@ -420,17 +433,17 @@ __global__ void vconv_repack_kernel(const bf16* __restrict__ src, int Mpad0, int
 
 bool vconv_supported(int cin, int cout, int k, int dil, int stride) {
   // k >= 2: a chunk's rows are staged during its predecessor's first step and read one step later
-  return stride == 1 && k >= 2 && cin % 64 == 0 && cout % BM == 0 && cout <= MMAX && BN + (k - 1) * dil <= XROWS;
+  return stride == 1 && k >= 2 && cin % 64 == 0 && cout % 64 == 0 && cout <= MMAX && BN + (k - 1) * dil <= XROWS;
 }
 
 size_t vconv_packed_bytes(int cin, int cout, int k) {
-  const int Mpad = (cout + BM - 1) / BM * BM;
+  const int Mpad = (cout + BMP - 1) / BMP * BMP;
   return (size_t)(cin / 64) * k * Mpad * 64 * sizeof(bf16);
 }
 
 int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st) {
   MT_REQUIRE(cin % 64 == 0 && cin_pad >= cin, "vconv_repack: cin %d", cin);
-  const int Mpad = (cout + BM - 1) / BM * BM;
+  const int Mpad = (cout + BMP - 1) / BMP * BMP;
   const size_t total = (size_t)(cin / 64) * taps * Mpad * 64;
   const int blocks = (int)std::min<size_t>((total + 255) / 256, 65535);
   hipLaunchKernelGGL(vconv_repack_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)src, Mpad0, taps, cin_pad,
@@ -451,7 +464,8 @@ static int cu_count() {
 
 int launch_vconv(int ef, const VConvArgs& a, hipStream_t st) {
   MT_REQUIRE(a.x && a.w && a.bias && a.y && a.zero && a.trash, "vconv: null pointer");
-  MT_REQUIRE(a.B > 0 && a.L > 0 && a.cin % 64 == 0 && a.M % BM == 0 && a.Mpad == a.M && a.M <= MMAX, "vconv: geometry");
+  MT_REQUIRE(a.B > 0 && a.L > 0 && a.cin % 64 == 0 && a.M % 64 == 0 && a.Mpad == a.M && a.M <= MMAX, "vconv: geometry");
+  const int BM = a.M % 128 == 0 ? 128 : 64;
   MT_REQUIRE(a.taps >= 2 && a.dil >= 1 && BN + (a.taps - 1) * a.dil <= XROWS, "vconv: taps %d dil %d", a.taps, a.dil);
   MT_REQUIRE(!(ef & VE_RESID) || a.resid, "vconv: resid");
   MT_REQUIRE(!(ef & VE_DUAL) || a.y2, "vconv: y2");
@@ -461,8 +475,11 @@ int launch_vconv(int ef, const VConvArgs& a, hipStream_t st) {
   const int touts = 1 + ((ef & VE_RESID) ? 1 : 0) + ((ef & VE_ACCUM) ? 1 : 0) + ((ef & VE_DUAL) ? 1 : 0);
   const double bytes = 2.0 * a.B * a.L * ((double)a.cin + (double)a.M * touts) + 2.0 * a.M * a.cin * a.taps;
   probe_begin(PROBE_VCONV, st);
-#define MT_VCASE(E)                                                                  \
-  case E: hipLaunchKernelGGL(vconv_kernel<E>, dim3(G), dim3(NT), 0, st, a); break;
+#define MT_VCASE(E)                                                                                \
+  case E:                                                                                          \
+    if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128>), dim3(G), dim3(NT), 0, st, a);       \
+    else hipLaunchKernelGGL((vconv_kernel<E, 64>), dim3(G), dim3(NT), 0, st, a);                  \
+    break;
   switch (ef) {
     MT_VCASE(VE_ACT)
     MT_VCASE(VE_RESID | VE_DUAL)

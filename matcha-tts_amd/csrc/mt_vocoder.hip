@@ -146,7 +146,11 @@ size_t Vocoder::frame_elems() const {
 
 bool Vocoder::stage_vc(int i) const {
   const int nk = (int)rb_kernels.size();
-  return vconv && dtype == BF16 && resblock == 1 && !rb1[(size_t)i * nk].empty() && rb1[(size_t)i * nk][0].vc;
+  if (!(vconv && dtype == BF16 && resblock == 1 && !rb1[(size_t)i * nk].empty() && rb1[(size_t)i * nk][0].vc))
+    return false;
+  // stages the fused ResBlock kernel serves stay fused unless vconv mode 2 asks for the per-layer path
+  const int C = rb1[(size_t)i * nk][0].cout;
+  return vconv >= 2 || !(fuse && rbfuse_supported(dtype, C));
 }
 
 size_t Vocoder::workspace_bytes(int B, int T) const {

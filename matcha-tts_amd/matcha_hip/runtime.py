@@ -253,8 +253,9 @@ class VocoderEngine:
     def set_fusion(self, enable: bool) -> None:
         check(lib().mt_vocoder_set_fusion(self.h, int(bool(enable))), "vocoder_set_fusion")
 
-    def set_vconv(self, enable: bool) -> None:
-        check(lib().mt_vocoder_set_vconv(self.h, int(bool(enable))), "vocoder_set_vconv")
+    def set_vconv(self, mode) -> None:
+        """0 generic per-layer kernel, 1 (default) vconv for the 128/256-channel stages, 2 also for 64."""
+        check(lib().mt_vocoder_set_vconv(self.h, int(mode)), "vocoder_set_vconv")
 
     def __del__(self):
         try:
@@ -428,7 +429,7 @@ def op_attention(qkv: torch.Tensor, mask: torch.Tensor, heads: int, precision="f
 
 
 # ---------------------------------------------------------------------------------- launch probe
-PROBE_RBFUSE_C64, PROBE_RBFUSE_C32 = 1, 2
+PROBE_RBFUSE_C64, PROBE_RBFUSE_C32, PROBE_VCONV = 1, 2, 3
 
 
 def probe_start(site: int, max_launches: int) -> None:

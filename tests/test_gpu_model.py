@@ -139,11 +139,13 @@ def test_fused_resblock_stages_bit_identical_to_per_layer(T):
     mel = torch.randn(3, 80, T, generator=torch.Generator().manual_seed(T)) * 2 - 5
     mel = mel.to(DEV)
     eng = gen.engine()
+    eng.set_vconv(0)  # every stage the fused kernel does not take runs on the generic kernel in both runs
     eng.set_fusion(True)
     a = gen(mel)
     eng.set_fusion(False)
     b = gen(mel)
     eng.set_fusion(True)
+    eng.set_vconv(2)
     assert torch.equal(a, b), (a - b).abs().max().item()
 
 
@@ -157,14 +159,15 @@ def test_vconv_stages_match_generic_per_layer(T):
     mel = torch.randn(2, 80, T, generator=torch.Generator().manual_seed(100 + T)) * 2 - 5
     mel = mel.to(DEV)
     eng = gen.engine()
-    eng.set_vconv(True)
-    a = gen(mel).cpu()
-    eng.set_vconv(False)
+    eng.set_vconv(0)
     b = gen(mel).cpu()
-    eng.set_vconv(True)
-    assert torch.isfinite(a).all()
-    assert rel_rms(a, b) < 1e-2, rel_rms(a, b)
-    assert not torch.equal(a, b)  # the vconv path really ran
+    for mode in (1, 2):  # 2: the 64-channel stage per layer through vconv too (instead of the fused kernel)
+        eng.set_vconv(mode)
+        a = gen(mel).cpu()
+        assert torch.isfinite(a).all()
+        assert rel_rms(a, b) < 1e-2, (mode, rel_rms(a, b))
+        assert not torch.equal(a, b)  # the vconv path really ran
+    eng.set_vconv(2)
 
 
 def test_denoiser_fp32():
@@ -247,6 +250,7 @@ def test_launch_probe_times_fused_stage():
     from matcha_hip import runtime as rt
     g, gen = _gen("bf16", True)
     mel = t(g["mel"], DEV)
+    gen.engine().set_vconv(1)  # keep the 64-channel stage on the fused kernel for this test
     gen(mel)
     rt.probe_start(rt.PROBE_RBFUSE_C64, 8)
     for _ in range(3):
@@ -259,3 +263,20 @@ def test_launch_probe_times_fused_stage():
     gen(mel)
     rt.probe_start(rt.PROBE_RBFUSE_C32, 1)
     assert rt.probe_stop()["launches"] == 0
+    gen.engine().set_vconv(2)
+
+
+def test_launch_probe_times_vconv_launches():
+    """PROBE_VCONV: events around every mt_vconv launch of the default vocoder (stages 1-3: 3
+    resblocks x 3 pairs x 2 convs each), their algorithmic FLOPs summed."""
+    from matcha_hip import runtime as rt
+    g, gen = _gen("bf16", True)
+    mel = t(g["mel"], DEV)
+    gen(mel)
+    rt.probe_start(rt.PROBE_VCONV, 64)
+    gen(mel)
+    p = rt.probe_stop()
+    B, T = mel.shape[0], mel.shape[2]
+    assert p["launches"] == 54 and p["ms"] > 0
+    want = sum(2.0 * 6 * C * C * 21 * B * T * r for C, r in ((256, 8), (128, 64), (64, 128)))
+    assert abs(p["flops"] - want) <= 1e-9 * want

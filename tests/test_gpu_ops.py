@@ -113,6 +113,8 @@ VCONV_CASES = [
     (128, 128, 7, 1, 3, 100, 1),           # shorter than one 256-frame tile, 3 utterances
     (256, 128, 3, 5, 2, 256, 1 | 2),       # exact tile multiple, accumulate
     (128, 256, 11, 1, 1, 40, 0),           # more padding than frames
+    (64, 64, 11, 5, 2, 700, 1 | 16),       # 64-channel stage (64-row tiles)
+    (64, 64, 3, 1, 3, 255, 1 | 2 | 4),     # 64-channel, accumulate + divide
 ]
 
 

@@ -24,9 +24,10 @@ g = g.cuda().eval()
 g.remove_weight_norm()
 mel = (torch.randn(B, 80, T) * 2 - 5).cuda()
 eng = g.engine()
-res = {True: [], False: []}
+MODES = (2, 1, 0)
+res = {m: [] for m in MODES}
 for r in range(R + 1):
-    for on in (True, False):
+    for on in MODES:
         eng.set_vconv(on)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -34,7 +35,7 @@ for r in range(R + 1):
         torch.cuda.synchronize()
         if r > 0:
             res[on].append((time.perf_counter() - t0) * 1e3)
-for on in (True, False):
+for on in MODES:
     v = sorted(res[on])
     if not v:
         continue
