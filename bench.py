@@ -119,7 +119,7 @@ def roofline(probe, precision):
     below the bf16 ridge (2.5 PFLOP/s / 8 TB/s = 312.5 FLOP/B) it is HBM-bound and `achieved` is
     algorithmic GB/s, above it MFMA-bound and `achieved` is TFLOP/s. `traffic` = HBM bytes per launch
     from rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE on this same bench command
-    (profiles/r02_pmc_vconv.json, tools_round_profile.sh)."""
+    (profiles/r01_pmc_vconv.json, tools_round_profile.sh)."""
     if probe is None or probe["launches"] == 0:
         return {"bound": "hbm", "achieved": None, "peak": 8000.0, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel": "vconv_kernel (bf16 path only)"}
@@ -133,7 +133,7 @@ def roofline(probe, precision):
     peak_f, peak_b = 2500.0, 8000.0  # dense bf16 MFMA TFLOP/s, HBM GB/s (MI355X_MICROARCH.md)
     ridge = peak_f * 1e12 / (peak_b * 1e9)
     traffic = None
-    pmc = os.path.join(HERE, "profiles", "r02_pmc_vconv.json")
+    pmc = os.path.join(HERE, "profiles", "r01_pmc_vconv.json")
     if os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
