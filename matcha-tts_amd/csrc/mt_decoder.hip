@@ -11,8 +11,10 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "mt_model.h"
+#include "mt_vconv.h"
 
 namespace mt {
 
@@ -231,6 +233,14 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
       t.ln1_off = pk.take(2 * C * 4);
       t.ln3_off = pk.take(2 * C * 4);
       t.snake_off = pk.take(2 * TE * 4);
+      if (dtype == BF16) {  // the transformer-block GEMMs run on mt_vconv's 1x1 pipeline
+        for (GemmW* g : {&t.qkv, &t.out, &t.ff1, &t.ff2}) {
+          g->vc = vconv_supported(g->cin, g->cout, 1, 1, 1);
+          if (g->vc) g->v_off = pk.take(vconv_packed_bytes(g->cin, g->cout, 1));
+        }
+        t.wsq_off = pk.take((size_t)t.qkv.cout * 4);
+        t.wsf_off = pk.take((size_t)t.ff1.cout * 4);
+      }
       v.push_back(t);
     }
     tbs.push_back(v);
@@ -280,6 +290,7 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
     int bp = L.add("final_proj.bias", {NF});
     fproj = make_conv(NF, C, 1, 1, 0, 1, {wp}, bp, esize, pk);
   }
+  zero_off = pk.take(256);
   packed_bytes = pk.off;
   return 0;
 }
@@ -316,8 +327,13 @@ int Decoder::pack(const float* const* p, void* packed, hipStream_t st) const {
       PK(pack_vec(p[t.ln3b], C, C, 0, (float*)(P + t.ln3_off) + C, st));
       PK(pack_vec(p[t.alpha], TE, TE, 1, (float*)(P + t.snake_off), st));
       PK(pack_vec(p[t.beta], TE, TE, 2, (float*)(P + t.snake_off) + TE, st));
+      for (const GemmW* g : {&t.qkv, &t.out, &t.ff1, &t.ff2})
+        if (g->vc) PK(vconv_repack(P + g->w_off, g->Mpad, g->taps, g->cin_pad, g->cin, g->cout, P + g->v_off, st));
+      if (t.qkv.vc) PK(vconv_wsum(P + t.qkv.v_off, t.qkv.cin, 1, t.qkv.cout, (float*)(P + t.wsq_off), st));
+      if (t.ff1.vc) PK(vconv_wsum(P + t.ff1.v_off, t.ff1.cin, 1, t.ff1.cout, (float*)(P + t.wsf_off), st));
     }
   }
+  PK(pack_vec(nullptr, 1, 64, 0, (float*)(P + zero_off), st));
   PK(pack_gemm(down0, dtype, p, P, st));
   PK(pack_gemm(down1, dtype, p, P, st));
   PK(pack_gemm(up0, dtype, p, P, st));
@@ -347,6 +363,7 @@ size_t Decoder::workspace_bytes(int B, int T, int S) const {
   n += align256((size_t)S * c_cond * 4);              // emb
   n += 2 * align256((size_t)S * TE * 4);              // h1 h2
   n += align256((size_t)S * n_res * C * 4);           // tb
+  n += 4096;                                          // trash (vconv stores past the last frame)
   return n;
 }
 
@@ -382,6 +399,7 @@ Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
   w.h1 = (float*)take((size_t)S * TE * 4);
   w.h2 = (float*)take((size_t)S * TE * 4);
   w.tb = (float*)take((size_t)S * n_res * C * 4);
+  w.trash = take(4096);
   w.m0 = nullptr;
   return w;
 }
@@ -452,6 +470,48 @@ template <class E>
 int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, int B, int Tl,
                     hipStream_t st) const {
   int rc;
+  if constexpr (std::is_same<E, bf16>::value) {
+    if (t.qkv.vc && t.out.vc && t.ff1.vc && t.ff2.vc) {
+      // bf16: the four GEMMs on mt_vconv's 1x1 pipeline; LayerNorm folded into the QKV / FF1 epilogues
+      auto vargs = [&](const GemmW& g, const void* xin, void* y) {
+        VConvArgs a{};
+        a.x = (const bf16*)xin;
+        a.B = B;
+        a.L = Tl;
+        a.cin = g.cin;
+        a.w = (const bf16*)(P + g.v_off);
+        a.bias = (const float*)(P + g.b_off);
+        a.M = a.Mpad = g.cout;
+        a.taps = 1;
+        a.dil = 1;
+        a.pad = 0;
+        a.y = (bf16*)y;
+        a.div = 1.f;
+        a.slope = 0.f;
+        a.zero = (const bf16*)(P + zero_off);
+        a.trash = (bf16*)w.trash;
+        a.ln_stats = w.lns;
+        return a;
+      };
+      if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
+      VConvArgs q = vargs(t.qkv, x, w.qkv);
+      q.wsum = (const float*)(P + t.wsq_off);
+      if ((rc = launch_vconv(VE_LN, q, st))) return rc;
+      if ((rc = launch_attention(dtype, w.qkv, mask, w.ob, B, Tl, heads, st))) return rc;
+      VConvArgs o = vargs(t.out, w.ob, x);
+      o.resid = (const bf16*)x;
+      if ((rc = launch_vconv(VE_RESID, o, st))) return rc;
+      if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
+      VConvArgs f1 = vargs(t.ff1, x, w.ff);
+      f1.wsum = (const float*)(P + t.wsf_off);
+      f1.snake_alpha = (const float*)(P + t.snake_off);
+      f1.snake_ibeta = (const float*)(P + t.snake_off) + TE;
+      if ((rc = launch_vconv(VE_LN | VE_SNAKE, f1, st))) return rc;
+      VConvArgs f2 = vargs(t.ff2, w.ff, x);
+      f2.resid = (const bf16*)x;
+      return launch_vconv(VE_RESID, f2, st);
+    }
+  }
   if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
   ConvArgs q = gemm_args(t.qkv, P, B, Tl);
   q.x0 = x;

@@ -73,8 +73,10 @@ struct Decoder {
   struct TB {
     int ln1g, ln1b, ln3g, ln3b, alpha, beta;
     size_t ln1_off, ln3_off, snake_off;
+    size_t wsq_off = 0, wsf_off = 0;  // vconv: row sums of the LN-folded qkv / ff1 images
     GemmW qkv, out, ff1, ff2;
   };
+  size_t zero_off = 0;  // 256 zero bytes (vconv padding rows)
   std::vector<Res> res;                // down0, down1, mid..., up0, up1
   std::vector<std::vector<TB>> tbs;    // per resnet
   GemmW down0, down1, up0, up1, fconv, fproj;
@@ -86,7 +88,7 @@ struct Decoder {
   size_t workspace_bytes(int B, int T, int S) const;
 
   struct Work {
-    char *xin, *H0, *H1, *XA, *XB, *XC, *U, *XF, *y1, *y2, *qkv, *ob, *ff;
+    char *xin, *H0, *H1, *XA, *XB, *XC, *U, *XF, *y1, *y2, *qkv, *ob, *ff, *trash;
     float *zm, *m1, *emb, *h1, *h2, *tb, *lns;
     double *gn1, *gn2;
     const float* m0;

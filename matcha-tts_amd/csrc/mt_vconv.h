@@ -15,6 +15,9 @@ enum : int {
   VE_DIV = 4,    // v = v / div                       (`xs / num_kernels`, models.py:193)
   VE_ACT = 8,    // y = lrelu(round(v))               (conv1: only lrelu(xt) is ever consumed)
   VE_DUAL = 16,  // y = round(v), y2 = lrelu(round(v)) (chain state + the next conv1's input)
+  VE_LN = 32,    // LayerNorm of the input folded in: acc := rstd[n] * (acc - mean[n] * wsum[m])
+                 // (gamma folded into W, beta into the bias at pack time; model.py:733-741)
+  VE_SNAKE = 64, // v + ibeta[m] * sin(v * alpha[m])^2 after the bias (SnakeBeta, model.py:580-609)
 };
 
 struct VConvArgs {
@@ -29,6 +32,10 @@ struct VConvArgs {
   float div, slope;
   const bf16* zero;   // >= 128 zero bytes: source of the conv's zero padding rows
   bf16* trash;        // >= 1 KiB writable: destination of the stores of frames past L
+  const float* ln_stats;     // [B*L][2] (mean, rstd) of the input frames (VE_LN)
+  const float* wsum;         // [M] row sums of the packed (gamma-folded, bf16) weights (VE_LN)
+  const float* snake_alpha;  // [M] exp(alpha) (VE_SNAKE)
+  const float* snake_ibeta;  // [M] 1 / (exp(beta) + 1e-9)
 };
 
 bool vconv_supported(int cin, int cout, int k, int dil, int stride);
@@ -37,5 +44,7 @@ size_t vconv_packed_bytes(int cin, int cout, int k);
 // [Mpad0][taps][cin_pad] (pack_conv layout, bf16) -> [cin/64][taps][Mpad][64]
 int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st);
 int launch_vconv(int ef, const VConvArgs& a, hipStream_t st);
+// wsum[m] = sum over (chunk, tap, channel) of the packed bf16 image (VE_LN)
+int vconv_wsum(const void* img, int cin, int taps, int cout, float* wsum, hipStream_t st);
 
 }  // namespace mt
