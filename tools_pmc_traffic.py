@@ -3,16 +3,17 @@
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of wide
 coalesced reads, so it is doubled; WRITE_SIZE is exact for 16-B stores. Both are in KiB.
-Usage: python tools_pmc_traffic.py FETCH_CSV WRITE_CSV KERNEL_SUBSTR OUT_JSON "command"
+Usage: python tools_pmc_traffic.py FETCH_CSV WRITE_CSV KERNEL_REGEX OUT_JSON "command"
 Only the launches with the largest grid are used (the bench workload, not the denoiser's
 bias-spectrum run on a 1 x 80 x 88 zero mel)."""
 import csv
 import json
+import re
 import sys
 
 
 def per_launch(path, sub, counter):
-    rows = [r for r in csv.DictReader(open(path)) if sub in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    rows = [r for r in csv.DictReader(open(path)) if re.search(sub, r["Kernel_Name"]) and r["Counter_Name"] == counter]
     g = max(int(r["Grid_Size"]) for r in rows)
     vals = [float(r["Counter_Value"]) for r in rows if int(r["Grid_Size"]) == g]
     return sum(vals) / len(vals), len(vals), g, rows[0]["Kernel_Name"]
