@@ -29,23 +29,23 @@
 namespace mt {
 
 namespace {
-constexpr int BN = 256, NT = 512;
+constexpr int BN = 256, NT = 512;                // BN: frames per tile (128 for small 1x1 grids)
 constexpr int MMAX = 1024;                        // largest C_out (per-channel epilogue tables in LDS)
 constexpr int BMP = 64;                           // packed weight rows are padded to a multiple of this
 // Tile geometry by output rows per workgroup: BM = 128 (waves 2 in M x 4 in N, 64x64 per wave) for
 // C_out % 128 == 0, BM = 64 (1 x 8 waves, 64x32 per wave) for the 64-channel stage.
 // K1: 1x1 convs (Linear): a chunk's rows are exactly the tile's 256 frames and every step starts a new
 // chunk, so rows are staged two chunks ahead in three 32 KiB buffers and the weight ring is 3 deep.
-template <int BM_, bool K1_, int NPAR_>
+template <int BM_, bool K1_, int NPAR_, int BN_ = BN>
 struct VT {
-  static constexpr int BM = BM_;
+  static constexpr int BM = BM_, TBN = BN_;
   static constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
-  static constexpr int WNC = BN / WAVES_N;        // frames per wave
+  static constexpr int WNC = TBN / WAVES_N;       // frames per wave
   static constexpr int FN = WNC / 16;             // 16-frame fragments per wave
   static constexpr int WSLOT = BM * 128;          // BM rows x 64 bf16 channels
   static constexpr int NWW = BM / 64;             // W wave-instructions per wave per step
   static constexpr int NWSLOT = K1_ ? 3 : 4;      // weight ring (NWSLOT - 1 steps in flight)
-  static constexpr int XROWS = K1_ ? BN : 320;    // >= BN + (taps - 1) * dil
+  static constexpr int XROWS = K1_ ? TBN : 320;   // >= BN + (taps - 1) * dil
   static constexpr int XBUF = XROWS * 128;
   static constexpr int NXW = XROWS / 64;          // X wave-instructions per wave per chunk
   static constexpr int NXB = (K1_ || BM == 64) ? 3 : 2;  // row buffers: chunks staged NXB-1 ahead
@@ -59,73 +59,21 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (n > 63 waits for 63: stricter, still correct)
+// s_waitcnt vmcnt(k) for a wave-uniform runtime bound n, with k the largest of {0,2,4,7,10,15,23,31} <= n:
+// waiting for fewer outstanding operations than allowed is always correct (only stricter), and a
+// three-level branch tree keeps the scalar cost per step small (a 64-way switch was ~40 SALU + branches)
 __device__ __forceinline__ void wait_vmcnt(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
-    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
-    case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); break;
-    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-    case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
-    case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
-    case 23: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
-    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-    case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
-    case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
-    case 27: asm volatile("s_waitcnt vmcnt(27)" ::: "memory"); break;
-    case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
-    case 29: asm volatile("s_waitcnt vmcnt(29)" ::: "memory"); break;
-    case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
-    case 31: asm volatile("s_waitcnt vmcnt(31)" ::: "memory"); break;
-    case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-    case 33: asm volatile("s_waitcnt vmcnt(33)" ::: "memory"); break;
-    case 34: asm volatile("s_waitcnt vmcnt(34)" ::: "memory"); break;
-    case 35: asm volatile("s_waitcnt vmcnt(35)" ::: "memory"); break;
-    case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
-    case 37: asm volatile("s_waitcnt vmcnt(37)" ::: "memory"); break;
-    case 38: asm volatile("s_waitcnt vmcnt(38)" ::: "memory"); break;
-    case 39: asm volatile("s_waitcnt vmcnt(39)" ::: "memory"); break;
-    case 40: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
-    case 41: asm volatile("s_waitcnt vmcnt(41)" ::: "memory"); break;
-    case 42: asm volatile("s_waitcnt vmcnt(42)" ::: "memory"); break;
-    case 43: asm volatile("s_waitcnt vmcnt(43)" ::: "memory"); break;
-    case 44: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
-    case 45: asm volatile("s_waitcnt vmcnt(45)" ::: "memory"); break;
-    case 46: asm volatile("s_waitcnt vmcnt(46)" ::: "memory"); break;
-    case 47: asm volatile("s_waitcnt vmcnt(47)" ::: "memory"); break;
-    case 48: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
-    case 49: asm volatile("s_waitcnt vmcnt(49)" ::: "memory"); break;
-    case 50: asm volatile("s_waitcnt vmcnt(50)" ::: "memory"); break;
-    case 51: asm volatile("s_waitcnt vmcnt(51)" ::: "memory"); break;
-    case 52: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
-    case 53: asm volatile("s_waitcnt vmcnt(53)" ::: "memory"); break;
-    case 54: asm volatile("s_waitcnt vmcnt(54)" ::: "memory"); break;
-    case 55: asm volatile("s_waitcnt vmcnt(55)" ::: "memory"); break;
-    case 56: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
-    case 57: asm volatile("s_waitcnt vmcnt(57)" ::: "memory"); break;
-    case 58: asm volatile("s_waitcnt vmcnt(58)" ::: "memory"); break;
-    case 59: asm volatile("s_waitcnt vmcnt(59)" ::: "memory"); break;
-    case 60: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
-    case 61: asm volatile("s_waitcnt vmcnt(61)" ::: "memory"); break;
-    case 62: asm volatile("s_waitcnt vmcnt(62)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+  if (n < 7) {
+    if (n < 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (n < 4) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else if (n < 15) {
+    if (n < 10) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  } else {
+    if (n < 23) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+    else if (n < 31) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(31)" ::: "memory");
   }
 }
 
@@ -142,9 +90,10 @@ constexpr int vc_npar() {
   return 1 + ((EF & VE_LN) ? 1 : 0) + ((EF & VE_SNAKE) ? 2 : 0);
 }
 
-template <int EF, int BMT, bool K1>
+template <int EF, int BMT, bool K1, int BNT = BN>
 __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
-  using TT = VT<BMT, K1, vc_npar<EF>()>;
+  using TT = VT<BMT, K1, vc_npar<EF>(), BNT>;
+  constexpr int BN = TT::TBN;
   constexpr int BM = TT::BM, WSLOT = TT::WSLOT, NWW = TT::NWW, FN = TT::FN;
   constexpr int WNC = TT::WNC, NXB = TT::NXB, NWSLOT = TT::NWSLOT, XBUF = TT::XBUF, NXW = TT::NXW;
   constexpr int BIAS_OFF = TT::PAR_OFF;
@@ -552,7 +501,11 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
     a.B = 1;
   }
   const int BM = a.M % 128 == 0 ? 128 : 64;
-  const long ntiles = (long)a.B * ((a.L + BN - 1) / BN) * (a.Mpad / BM);
+  long ntiles = (long)a.B * ((a.L + BN - 1) / BN) * (a.Mpad / BM);
+  // 1x1 GEMMs whose 256-frame tiles would leave CUs idle (the decoder's half-resolution blocks):
+  // 128-frame tiles double the parallelism
+  const bool small = k1 && ntiles < (long)cu_count();
+  if (small) ntiles = (long)((a.L + 127) / 128) * (a.Mpad / BM);
   const int G = (int)std::min<long>(ntiles, cu_count());
   const double flops = 2.0 * a.M * a.cin * a.taps * (double)a.B * a.L;
   const int touts = 1 + ((ef & VE_RESID) ? 1 : 0) + ((ef & VE_ACCUM) ? 1 : 0) + ((ef & VE_DUAL) ? 1 : 0);
@@ -564,10 +517,15 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
     if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false>), dim3(G), dim3(NT), 0, st, a); \
     else hipLaunchKernelGGL((vconv_kernel<E, 64, false>), dim3(G), dim3(NT), 0, st, a);           \
     break;
-#define MT_VCASE1(E)                                                                               \
-  case E:                                                                                          \
-    if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, true>), dim3(G), dim3(NT), 0, st, a);  \
-    else hipLaunchKernelGGL((vconv_kernel<E, 64, true>), dim3(G), dim3(NT), 0, st, a);            \
+#define MT_VCASE1(E)                                                                                    \
+  case E:                                                                                               \
+    if (small) {                                                                                        \
+      if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, true, 128>), dim3(G), dim3(NT), 0, st, a); \
+      else hipLaunchKernelGGL((vconv_kernel<E, 64, true, 128>), dim3(G), dim3(NT), 0, st, a);           \
+    } else {                                                                                            \
+      if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, true>), dim3(G), dim3(NT), 0, st, a);     \
+      else hipLaunchKernelGGL((vconv_kernel<E, 64, true>), dim3(G), dim3(NT), 0, st, a);                \
+    }                                                                                                   \
     break;
   if (!k1) {
     switch (ef) {
