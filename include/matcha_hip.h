@@ -84,6 +84,11 @@ void mt_decoder_destroy(mt_decoder* d);
 int mt_decoder_num_params(const mt_decoder* d);
 int mt_decoder_param_name(const mt_decoder* d, int i, char* buf, int buflen);
 int mt_decoder_param_shape(const mt_decoder* d, int i, int64_t* shape, int maxdim); /* -> ndim */
+/* bf16: 1 (default) runs the ResnetBlock1D convs, the stride-1 down/up convs and the final block
+ * conv on the LDS-DMA persistent conv (mt_vconv; producers keep those inputs masked, GroupNorm+Mish
+ * applied by a separate pass); 0 = generic conv kernel with the GN/mask prologues. Same math as
+ * mt_decoder_step / mt_cfm_solve (model.py ResnetBlock1D, Block1D, Decoder.forward) either way. */
+int mt_decoder_set_vconv(mt_decoder* d, int enable);
 size_t mt_decoder_packed_bytes(const mt_decoder* d);
 /* params[i]: device fp32 tensor in reference layout for parameter i. */
 int mt_decoder_pack(const mt_decoder* d, const float* const* params, void* packed, void* stream);
@@ -192,6 +197,7 @@ int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, in
 #define MT_PROBE_RBFUSE_C64 1
 #define MT_PROBE_RBFUSE_C32 2
 #define MT_PROBE_VCONV 3
+#define MT_PROBE_VCONV_DEC 4
 int mt_probe_start(int site, int max_launches);
 int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes);
 

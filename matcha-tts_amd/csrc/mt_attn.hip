@@ -5,6 +5,12 @@
 // Workgroup = 4 waves = 64 queries of one (utterance, head); flash-style online softmax
 // over 64-key tiles, S = Q.K^T and O += P.V on MFMA (bf16: 16x16x32, f32: 16x16x4).
 //
+// Key split (flash-decoding): an unpadded utterance's 64-query tile is the launch's critical path
+// (T/64 dependent key-tile iterations), so grid.z carries NS key ranges per utterance; each writes
+// its unnormalised (o, m, l) to a workspace slot and attn_merge_kernel combines the slots in split
+// order (deterministic). The next key tile's K/V rows are fetched into registers while the current
+// tile computes.
+//
 // Reference mask semantics, kept exactly: masked keys are filled with
 // -torch.finfo(fp32).min = +3.4e38 (model.py:697), so for an utterance whose mask has ANY
 // zero at this level every query attends uniformly to the masked keys:
@@ -12,6 +18,7 @@
 // and for an utterance without padding the ordinary softmax over all keys applies.
 #include "mt_common.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace mt {
@@ -19,7 +26,8 @@ namespace mt {
 template <class E>
 __global__ __launch_bounds__(256) void attn_kernel(const E* __restrict__ qkv,
                                                    const float* __restrict__ mask,
-                                                   E* __restrict__ out, int T, int inner) {
+                                                   E* __restrict__ out, int T, int inner, int NS,
+                                                   float* __restrict__ part) {
   constexpr int CH = Chunk<E>::CH;          // elements per 64-byte chunk
   constexpr int VN = Vec16<E>::N;           // elements per 16 bytes
   constexpr int NDC = 64 / CH;              // d-chunks per head (bf16 2, f32 4)
@@ -33,7 +41,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const E* __restrict__ qkv,
   float* red = reinterpret_cast<float*>(Ps + 64 * ROW);  // [4][64]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 64;
+  const int b = blockIdx.z / NS, sp = blockIdx.z - b * NS, h = blockIdx.y, q0 = blockIdx.x * 64;
   const int ld = 3 * inner;
   const E* Q = qkv + (size_t)b * T * ld + h * 64;
   const E* K = Q + inner;
@@ -45,6 +53,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const E* __restrict__ qkv,
   int npad_local = 0;
   for (int j = tid; j < T; j += 256) npad_local += (mk[j] == 0.f) ? 1 : 0;
   if (__syncthreads_or(npad_local)) {
+    if (sp != 0) return;  // one block per query tile serves the uniform case
     // exact count of masked keys
     int* cnt = reinterpret_cast<int*>(red);
     if (tid == 0) cnt[0] = 0;
@@ -54,18 +63,36 @@ __global__ __launch_bounds__(256) void attn_kernel(const E* __restrict__ qkv,
     const int n = cnt[0];
     __syncthreads();
     const float p = 1.f / (float)n;
-    // thread (kg, d): partial sum over keys j = kg (mod 4)
-    const int kg = tid >> 6, d = tid & 63;
-    float s = 0.f;
-    for (int j = kg; j < T; j += 4)
-      if (mk[j] == 0.f) s += p * to_f(V[(size_t)j * ld + d]);
-    red[kg * 64 + d] = s;
+    // thread (kg, dc): 16-byte column chunk dc of keys j = kg (mod KG), several rows in flight
+    constexpr int NC = 64 / VN, KG = 256 / NC;
+    const int kg = tid / NC, dc = tid % NC;
+    float s[VN];
+#pragma unroll
+    for (int e = 0; e < VN; ++e) s[e] = 0.f;
+#pragma unroll 4
+    for (int j = kg; j < T; j += KG) {
+      const Vec16<E> v = load16(V + (size_t)j * ld + dc * VN);
+      const float w = mk[j] == 0.f ? p : 0.f;
+#pragma unroll
+      for (int e = 0; e < VN; ++e) s[e] += w * v.get(e);
+    }
+    float* part_s = reinterpret_cast<float*>(smem);  // [KG][64] (the K tile region is free here)
+#pragma unroll
+    for (int e = 0; e < VN; ++e) part_s[kg * 64 + dc * VN + e] = s[e];
     __syncthreads();
-    if (tid < 64) red[tid] = ((red[tid] + red[64 + tid]) + red[128 + tid]) + red[192 + tid];
+    if (tid < 64) {
+      float t = 0.f;
+      for (int k = 0; k < KG; ++k) t += part_s[k * 64 + tid];
+      red[tid] = t;
+    }
     __syncthreads();
-    for (int i = tid; i < 64 * 64; i += 256) {
-      const int q = q0 + (i >> 6), dd = i & 63;
-      if (q < T) O[(size_t)q * inner + dd] = from_f<E>(red[dd]);
+    for (int i = tid; i < 64 * NC; i += 256) {
+      const int q = q0 + i / NC, c = i % NC;
+      if (q >= T) continue;
+      Vec16<E> o;
+#pragma unroll
+      for (int e = 0; e < VN; ++e) o.set(e, red[c * VN + e]);
+      store16(O + (size_t)q * inner + c * VN, o);
     }
     return;
   }
@@ -88,23 +115,39 @@ __global__ __launch_bounds__(256) void attn_kernel(const E* __restrict__ qkv,
   }
 
   char* Pw = Ps + wave * 16 * ROW;
-  const int nkt = (T + 63) / 64;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int k0 = kt * 64;
-    // stage K rows and V^T
-    for (int v = tid; v < 64 * (64 / VN); v += 256) {
-      const int r = v / (64 / VN), s = v % (64 / VN);
-      const int key = k0 + r;
-      Vec16<E> kv = zero16<E>(), vv = zero16<E>();
-      if (key < T) {
-        kv = load16(K + (size_t)key * ld + s * VN);
-        vv = load16(V + (size_t)key * ld + s * VN);
-      }
-      store16(reinterpret_cast<E*>(Ks + r * ROW + s * 16), kv);
+  const int nkt_all = (T + 63) / 64;
+  const int per = (nkt_all + NS - 1) / NS;
+  const int kt0 = sp * per, kt1 = min(nkt_all, kt0 + per);
+  constexpr int NI = 64 * (64 / VN) / 256;  // 16-byte K (and V) pieces per thread per key tile
+  Vec16<E> kn[NI], vn[NI];
+  auto fetch = [&](int kt) {
 #pragma unroll
-      for (int i = 0; i < VN; ++i)
-        reinterpret_cast<E*>(Vt + (s * VN + i) * ROW)[r] = from_f<E>(vv.get(i));
+    for (int i = 0; i < NI; ++i) {
+      const int v = tid + i * 256;
+      const int r = v / (64 / VN), s = v % (64 / VN);
+      const int key = kt * 64 + r;
+      kn[i] = zero16<E>();
+      vn[i] = zero16<E>();
+      if (key < T) {
+        kn[i] = load16(K + (size_t)key * ld + s * VN);
+        vn[i] = load16(V + (size_t)key * ld + s * VN);
+      }
     }
+  };
+  if (kt0 < kt1) fetch(kt0);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int k0 = kt * 64;
+    // stage K rows and V^T from the prefetched registers, then fetch the next tile
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int v = tid + i * 256;
+      const int r = v / (64 / VN), s = v % (64 / VN);
+      store16(reinterpret_cast<E*>(Ks + r * ROW + s * 16), kn[i]);
+#pragma unroll
+      for (int e = 0; e < VN; ++e)
+        reinterpret_cast<E*>(Vt + (s * VN + e) * ROW)[r] = from_f<E>(vn[i].get(e));
+    }
+    if (kt + 1 < kt1) fetch(kt + 1);
     __syncthreads();
 
     // S = Q K^T : 16 queries x 64 keys per wave (4 fragments of 16 keys)
@@ -192,31 +235,102 @@ __global__ __launch_bounds__(256) void attn_kernel(const E* __restrict__ qkv,
   }
 
   // normalise and store: lane holds rows q = 4(lane>>4)+r, col d = 16 df + (lane&15)
+  if (NS == 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + wave * 16 + 4 * (lane >> 4) + r;
+      if (q >= T) continue;
+      const float inv = 1.f / l_run[r];
+#pragma unroll
+      for (int df = 0; df < 4; ++df) O[(size_t)q * inner + df * 16 + (lane & 15)] = from_f<E>(o[df][r] * inv);
+    }
+    return;
+  }
+  // split: slot = [64 q][64 d] o + [64 q] (m, l); an empty key range leaves m = -inf, l = 0
+  const int tile = (b * gridDim.y + h) * gridDim.x + blockIdx.x;
+  float* slot = part + ((size_t)tile * NS + sp) * (64 * 66);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int q = q0 + wave * 16 + 4 * (lane >> 4) + r;
-    if (q >= T) continue;
-    const float inv = 1.f / l_run[r];
+    const int ql = wave * 16 + 4 * (lane >> 4) + r;
 #pragma unroll
-    for (int df = 0; df < 4; ++df) O[(size_t)q * inner + df * 16 + (lane & 15)] = from_f<E>(o[df][r] * inv);
+    for (int df = 0; df < 4; ++df) slot[ql * 64 + df * 16 + (lane & 15)] = o[df][r];
+    if ((lane & 15) == 0) {
+      slot[64 * 64 + 2 * ql] = m_run[r];
+      slot[64 * 64 + 2 * ql + 1] = l_run[r];
+    }
   }
 }
 
+// combines the NS key-range slots of every query tile of the unpadded utterances, split order fixed
+template <class E>
+__global__ __launch_bounds__(256) void attn_merge_kernel(const float* __restrict__ part,
+                                                         const float* __restrict__ mask, E* __restrict__ out,
+                                                         int T, int inner, int NS) {
+  constexpr bool PRECISE = std::is_same<E, float>::value;
+  const int tid = threadIdx.x, b = blockIdx.z, h = blockIdx.y, q0 = blockIdx.x * 64;
+  const float* mk = mask + (size_t)b * T;
+  int npad_local = 0;
+  for (int j = tid; j < T; j += 256) npad_local += (mk[j] == 0.f) ? 1 : 0;
+  if (__syncthreads_or(npad_local)) return;  // the uniform path wrote this utterance
+  const int tile = (b * gridDim.y + h) * gridDim.x + blockIdx.x;
+  const float* slot0 = part + (size_t)tile * NS * (64 * 66);
+  const int ql = tid >> 2, dq = (tid & 3) * 16;
+  const int q = q0 + ql;
+  if (q >= T) return;
+  float mx = -INFINITY;
+  for (int k = 0; k < NS; ++k) mx = fmaxf(mx, slot0[(size_t)k * (64 * 66) + 64 * 64 + 2 * ql]);
+  float acc[16], lsum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int k = 0; k < NS; ++k) {
+    const float* sl = slot0 + (size_t)k * (64 * 66);
+    const float mk_ = sl[64 * 64 + 2 * ql];
+    if (mk_ == -INFINITY) continue;
+    const float wk = PRECISE ? expf(mk_ - mx) : __expf(mk_ - mx);
+    lsum += sl[64 * 64 + 2 * ql + 1] * wk;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] += sl[ql * 64 + dq + i] * wk;
+  }
+  const float inv = 1.f / lsum;
+  E* O = out + ((size_t)b * T + q) * inner + h * 64 + dq;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) O[i] = from_f<E>(acc[i] * inv);
+}
+
+static int attn_splits(int T) {
+  const int nkt = (T + 63) / 64;
+  return std::min(8, (nkt + 2) / 3);
+}
+size_t attention_part_bytes(int B, int T, int heads) {
+  const int NS = attn_splits(T);
+  return NS <= 1 ? 0 : (size_t)B * heads * ((T + 63) / 64) * NS * 64 * 66 * sizeof(float);
+}
+
 int launch_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T,
-                     int heads, hipStream_t stream) {
+                     int heads, hipStream_t stream, float* part) {
   MT_REQUIRE(B > 0 && T > 0 && heads > 0, "attention: empty geometry");
   const int inner = heads * 64;
   const int esz = dtype == BF16 ? 2 : 4;
   const size_t row = 64 * esz + 16;
   const size_t lds = 3 * 64 * row + 4 * 64 * sizeof(float);
-  dim3 grid((unsigned)((T + 63) / 64), (unsigned)heads, (unsigned)B);
+  const int nkt = (T + 63) / 64;
+  const int NS = part ? attn_splits(T) : 1;
+  dim3 grid((unsigned)nkt, (unsigned)heads, (unsigned)(B * NS));
   if (dtype == BF16)
     hipLaunchKernelGGL(attn_kernel<bf16>, grid, dim3(256), lds, stream, (const bf16*)qkv, mask,
-                       (bf16*)out, T, inner);
+                       (bf16*)out, T, inner, NS, part);
   else
     hipLaunchKernelGGL(attn_kernel<float>, grid, dim3(256), lds, stream, (const float*)qkv, mask,
-                       (float*)out, T, inner);
+                       (float*)out, T, inner, NS, part);
   MT_CHECK_HIP(hipGetLastError());
+  if (NS > 1) {
+    dim3 mg((unsigned)nkt, (unsigned)heads, (unsigned)B);
+    if (dtype == BF16)
+      hipLaunchKernelGGL(attn_merge_kernel<bf16>, mg, dim3(256), 0, stream, part, mask, (bf16*)out, T, inner, NS);
+    else
+      hipLaunchKernelGGL(attn_merge_kernel<float>, mg, dim3(256), 0, stream, part, mask, (float*)out, T, inner, NS);
+    MT_CHECK_HIP(hipGetLastError());
+  }
   return 0;
 }
 

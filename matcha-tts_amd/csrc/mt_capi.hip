@@ -109,6 +109,11 @@ int mt_decoder_param_shape(const mt_decoder* d, int i, int64_t* shape, int maxdi
   MT_REQUIRE(d, "null decoder");
   return param_shape(d->d.params, i, shape, maxdim);
 }
+int mt_decoder_set_vconv(mt_decoder* d, int enable) {
+  MT_REQUIRE(d, "null decoder");
+  d->d.vconv = enable ? 1 : 0;
+  return 0;
+}
 size_t mt_decoder_packed_bytes(const mt_decoder* d) { return d ? d->d.packed_bytes : 0; }
 int mt_decoder_pack(const mt_decoder* d, const float* const* params, void* packed, void* stream) {
   MT_REQUIRE(d && params && packed, "decoder_pack: null argument");

@@ -14,6 +14,7 @@
 #include <type_traits>
 
 #include "mt_model.h"
+#include "mt_probe.h"
 #include "mt_vconv.h"
 
 namespace mt {
@@ -178,6 +179,13 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
   t2b_off = pk.take(TE * 4);
   freq_off = pk.take(Cc / 2 * 4);
 
+  // bf16 convs mt_vconv serves (stride 1, C_in % 64 == 0) get its [cin/64][taps][M][64] image too
+  auto vcify = [&](GemmW& g) {
+    if (dtype == BF16 && g.kind == 0 && vconv_supported(g.cin, g.cout, g.k, g.dil, g.s)) {
+      g.vc = true;
+      g.v_off = pk.take(vconv_packed_bytes(g.cin, g.cout, g.k));
+    }
+  };
   auto add_res = [&](const std::string& p, int dim_in) {
     Res R;
     R.dim_in = dim_in;
@@ -196,6 +204,9 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
     R.c1 = make_conv(C, dim_in, 3, 1, 1, 1, {w1}, b1, esize, pk);
     R.c2 = make_conv(C, C, 3, 1, 1, 1, {w2}, b2, esize, pk);
     R.res = make_conv(C, dim_in, 1, 1, 0, 1, {wr}, br, esize, pk);
+    vcify(R.c1);
+    vcify(R.c2);
+    vcify(R.res);
     R.gn1_off = pk.take(2 * C * 4);
     R.gn2_off = pk.take(2 * C * 4);
     R.mlp_w_off = pk.take((size_t)C * TE * 4);
@@ -260,6 +271,7 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
     int w = L.add("down_blocks.1.2.weight", {C, C, 3});
     int b = L.add("down_blocks.1.2.bias", {C});
     down1 = make_conv(C, C, 3, 1, 1, 1, {w}, b, esize, pk);
+    vcify(down1);
   }
   for (int i = 0; i < n_mid; ++i) {
     add_res("mid_blocks." + std::to_string(i) + ".0", C);
@@ -278,6 +290,7 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
     int w = L.add("up_blocks.1.2.weight", {C, C, 3});
     int b = L.add("up_blocks.1.2.bias", {C});
     up1 = make_conv(C, C, 3, 1, 1, 1, {w}, b, esize, pk);
+    vcify(up1);
   }
   {
     int w = L.add("final_block.block.0.weight", {C, C, 3});
@@ -285,6 +298,7 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
     fgn_g = L.add("final_block.block.1.weight", {C});
     fgn_b = L.add("final_block.block.1.bias", {C});
     fconv = make_conv(C, C, 3, 1, 1, 1, {w}, b, esize, pk);
+    vcify(fconv);
     fgn_off = pk.take(2 * C * 4);
     int wp = L.add("final_proj.weight", {NF, C, 1});
     int bp = L.add("final_proj.bias", {NF});
@@ -310,6 +324,8 @@ int Decoder::pack(const float* const* p, void* packed, hipStream_t st) const {
     PK(pack_gemm(R.c1, dtype, p, P, st));
     PK(pack_gemm(R.c2, dtype, p, P, st));
     PK(pack_gemm(R.res, dtype, p, P, st));
+    for (const GemmW* g : {&R.c1, &R.c2, &R.res})
+      if (g->vc) PK(vconv_repack(P + g->w_off, g->Mpad, g->taps, g->cin_pad, g->cin, g->cout, P + g->v_off, st));
     PK(pack_vec(p[R.gn1g], C, C, 0, (float*)(P + R.gn1_off), st));
     PK(pack_vec(p[R.gn1b], C, C, 0, (float*)(P + R.gn1_off) + C, st));
     PK(pack_vec(p[R.gn2g], C, C, 0, (float*)(P + R.gn2_off), st));
@@ -342,13 +358,16 @@ int Decoder::pack(const float* const* p, void* packed, hipStream_t st) const {
   PK(pack_vec(p[fgn_g], C, C, 0, (float*)(P + fgn_off), st));
   PK(pack_vec(p[fgn_b], C, C, 0, (float*)(P + fgn_off) + C, st));
   PK(pack_gemm(fproj, dtype, p, P, st));
+  for (const GemmW* g : {&down1, &up1, &fconv})
+    if (g->vc) PK(vconv_repack(P + g->w_off, g->Mpad, g->taps, g->cin_pad, g->cin, g->cout, P + g->v_off, st));
 #undef PK
   return 0;
 }
 
 size_t Decoder::workspace_bytes(int B, int T, int S) const {
   const size_t BT = (size_t)B * T;
-  const size_t ntl = (size_t)(T + 63) / 64;
+  // GroupNorm partial slots: generic conv tiles of 64 frames or vconv tiles x waves, whichever is more
+  const size_t ntl = (size_t)std::max((T + 63) / 64, vconv_gn_parts(T, C));
   size_t n = 0;
   n += align256(BT * c_cond * esize);                 // xin
   n += 8 * align256(BT * C * esize);                  // H0 H1 XA XB XC U XF + y1
@@ -364,12 +383,13 @@ size_t Decoder::workspace_bytes(int B, int T, int S) const {
   n += 2 * align256((size_t)S * TE * 4);              // h1 h2
   n += align256((size_t)S * n_res * C * 4);           // tb
   n += 4096;                                          // trash (vconv stores past the last frame)
+  n += align256(attention_part_bytes(B, T, heads));   // attention key-split slots
   return n;
 }
 
 Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
   const size_t BT = (size_t)B * T;
-  const size_t ntl = (size_t)(T + 63) / 64;
+  const size_t ntl = (size_t)std::max((T + 63) / 64, vconv_gn_parts(T, C));
   char* p = (char*)ws;
   auto take = [&](size_t bytes) {
     char* r = p;
@@ -400,6 +420,7 @@ Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
   w.h2 = (float*)take((size_t)S * TE * 4);
   w.tb = (float*)take((size_t)S * n_res * C * 4);
   w.trash = take(4096);
+  w.apart = (float*)take(attention_part_bytes(B, T, heads));
   w.m0 = nullptr;
   return w;
 }
@@ -421,34 +442,94 @@ int Decoder::time_embed(const char* P, const Work& w, const TimeSched& ts, int S
   return 0;
 }
 
+VConvArgs Decoder::vargs(const GemmW& g, const char* P, const Work& w, const void* x, int B, int Tl,
+                         void* y) const {
+  VConvArgs a{};
+  a.x = (const bf16*)x;
+  a.B = B;
+  a.L = Tl;
+  a.cin = g.cin;
+  a.w = (const bf16*)(P + g.v_off);
+  a.bias = (const float*)(P + g.b_off);
+  a.M = a.Mpad = g.cout;
+  a.taps = g.k;
+  a.dil = g.dil;
+  a.pad = g.pad;
+  a.y = (bf16*)y;
+  a.div = 1.f;
+  a.slope = 0.f;
+  a.zero = (const bf16*)(P + zero_off);
+  a.trash = (bf16*)w.trash;
+  a.ln_stats = w.lns;
+  a.probe = PROBE_VCONV_DEC;
+  return a;
+}
+
+// ResnetBlock1D (model.py ResnetBlock1D / Block1D): out = block2(block1(x*m) + mlp(t)) * m + res(x*m)
+// Generic kernels: K1 conv3 with the input mask in its prologue + GN partials, K2 conv3 with GN/Mish/tb/mask
+// in its prologue + GN partials, K3 res 1x1 + mish(GN(y2))*m in its epilogue. On vconv (bf16, x already
+// masked by its producer): conv3 + GN partials -> gn_apply -> conv3 + GN partials -> gn_apply -> res 1x1
+// with the block output as its residual.
 template <class E>
 int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, const void* x1, int c0,
-                    int cin, void* out, const float* mask, int B, int Tl, const float* tb,
+                    int cin, bool x_masked, void* out, const float* mask, int B, int Tl, const float* tb,
                     hipStream_t st) const {
   int rc, nt1 = 0, nt2 = 0;
-  ConvArgs a = gemm_args(R.c1, P, B, Tl);
-  a.x0 = x0;
-  a.x1 = x1;
-  a.c0 = c0;
-  a.cin = cin;
-  a.y = w.y1;
-  a.pmask = mask;
-  a.gn_out = w.gn1;
-  if ((rc = launch_conv<E, PF_MASK, EF_GNSTATS>(a, st, &nt1))) return rc;
-
-  ConvArgs b = gemm_args(R.c2, P, B, Tl);
-  b.x0 = w.y1;
-  b.y = w.y2;
-  b.pmask = mask;
-  b.gn_in = w.gn1;
-  b.gn_ntiles = nt1;
-  b.gn_T = Tl;
-  b.gn_g = (const float*)(P + R.gn1_off);
-  b.gn_b = (const float*)(P + R.gn1_off) + C;
-  b.tb = tb;
-  b.gn_out = w.gn2;
-  if ((rc = launch_conv<E, PF_GN | PF_TB | PF_MASK, EF_GNSTATS>(b, st, &nt2))) return rc;
-
+  const float* g1 = (const float*)(P + R.gn1_off);
+  const float* g2 = (const float*)(P + R.gn2_off);
+  // block 1 -> y1 + gn1
+  if (x_masked && vc(R.c1)) {
+    VConvArgs a = vargs(R.c1, P, w, x0, B, Tl, w.y1);
+    a.x1 = (const bf16*)x1;
+    a.c0 = c0;
+    a.cin = cin;
+    a.gn_out = w.gn1;
+    if ((rc = launch_vconv(VE_GNSTATS, a, st))) return rc;
+    nt1 = vconv_gn_parts(Tl, C);
+  } else {
+    ConvArgs a = gemm_args(R.c1, P, B, Tl);
+    a.x0 = x0;
+    a.x1 = x1;
+    a.c0 = c0;
+    a.cin = cin;
+    a.y = w.y1;
+    a.pmask = mask;
+    a.gn_out = w.gn1;
+    if ((rc = launch_conv<E, PF_MASK, EF_GNSTATS>(a, st, &nt1))) return rc;
+  }
+  // block 2 -> y2 + gn2 (generic) or y1 + gn2 (vconv, its input h1 in y2)
+  const void* yb2 = w.y2;
+  if (vc(R.c2)) {
+    if ((rc = gn_apply(w.y1, B, Tl, C, w.gn1, nt1, g1, g1 + C, 1e-5f, tb, mask, w.y2, st))) return rc;
+    VConvArgs b = vargs(R.c2, P, w, w.y2, B, Tl, w.y1);
+    b.gn_out = w.gn2;
+    if ((rc = launch_vconv(VE_GNSTATS, b, st))) return rc;
+    nt2 = vconv_gn_parts(Tl, C);
+    yb2 = w.y1;
+  } else {
+    ConvArgs b = gemm_args(R.c2, P, B, Tl);
+    b.x0 = w.y1;
+    b.y = w.y2;
+    b.pmask = mask;
+    b.gn_in = w.gn1;
+    b.gn_ntiles = nt1;
+    b.gn_T = Tl;
+    b.gn_g = g1;
+    b.gn_b = g1 + C;
+    b.tb = tb;
+    b.gn_out = w.gn2;
+    if ((rc = launch_conv<E, PF_GN | PF_TB | PF_MASK, EF_GNSTATS>(b, st, &nt2))) return rc;
+  }
+  // residual 1x1 + block output
+  if (x_masked && vc(R.res)) {
+    if ((rc = gn_apply(yb2, B, Tl, C, w.gn2, nt2, g2, g2 + C, 1e-5f, nullptr, mask, w.y2, st))) return rc;
+    VConvArgs c = vargs(R.res, P, w, x0, B, Tl, out);
+    c.x1 = (const bf16*)x1;
+    c.c0 = c0;
+    c.cin = cin;
+    c.resid = (const bf16*)w.y2;
+    return launch_vconv(VE_RESID, c, st);
+  }
   ConvArgs c = gemm_args(R.res, P, B, Tl);
   c.x0 = x0;
   c.x1 = x1;
@@ -457,47 +538,28 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
   c.y = out;
   c.pmask = mask;
   c.emask = mask;
-  c.gy = w.y2;
+  c.gy = yb2;
   c.gn_in = w.gn2;
   c.gn_ntiles = nt2;
   c.gn_T = Tl;
-  c.gn_g = (const float*)(P + R.gn2_off);
-  c.gn_b = (const float*)(P + R.gn2_off) + C;
+  c.gn_g = g2;
+  c.gn_b = g2 + C;
   return launch_conv<E, PF_MASK, EF_GNADD>(c, st);
 }
 
 template <class E>
-int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, int B, int Tl,
-                    hipStream_t st) const {
+int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, bool mask_out, int B,
+                    int Tl, hipStream_t st) const {
   int rc;
   if constexpr (std::is_same<E, bf16>::value) {
     if (t.qkv.vc && t.out.vc && t.ff1.vc && t.ff2.vc) {
       // bf16: the four GEMMs on mt_vconv's 1x1 pipeline; LayerNorm folded into the QKV / FF1 epilogues
-      auto vargs = [&](const GemmW& g, const void* xin, void* y) {
-        VConvArgs a{};
-        a.x = (const bf16*)xin;
-        a.B = B;
-        a.L = Tl;
-        a.cin = g.cin;
-        a.w = (const bf16*)(P + g.v_off);
-        a.bias = (const float*)(P + g.b_off);
-        a.M = a.Mpad = g.cout;
-        a.taps = 1;
-        a.dil = 1;
-        a.pad = 0;
-        a.y = (bf16*)y;
-        a.div = 1.f;
-        a.slope = 0.f;
-        a.zero = (const bf16*)(P + zero_off);
-        a.trash = (bf16*)w.trash;
-        a.ln_stats = w.lns;
-        return a;
-      };
+      auto vargs = [&](const GemmW& g, const void* xin, void* y) { return this->vargs(g, P, w, xin, B, Tl, y); };
       if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
       VConvArgs q = vargs(t.qkv, x, w.qkv);
       q.wsum = (const float*)(P + t.wsq_off);
       if ((rc = launch_vconv(VE_LN, q, st))) return rc;
-      if ((rc = launch_attention(dtype, w.qkv, mask, w.ob, B, Tl, heads, st))) return rc;
+      if ((rc = launch_attention(dtype, w.qkv, mask, w.ob, B, Tl, heads, st, w.apart))) return rc;
       VConvArgs o = vargs(t.out, w.ob, x);
       o.resid = (const bf16*)x;
       if ((rc = launch_vconv(VE_RESID, o, st))) return rc;
@@ -509,7 +571,9 @@ int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const fl
       if ((rc = launch_vconv(VE_LN | VE_SNAKE, f1, st))) return rc;
       VConvArgs f2 = vargs(t.ff2, w.ff, x);
       f2.resid = (const bf16*)x;
-      return launch_vconv(VE_RESID, f2, st);
+      // the chain's last block hands its consumers (convs reading x * mask) a masked copy in place
+      f2.emask = mask;
+      return launch_vconv(mask_out ? VE_RESID | VE_MASK : VE_RESID, f2, st);
     }
   }
   if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
@@ -518,7 +582,7 @@ int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const fl
   q.y = w.qkv;
   q.ln_stats = w.lns;
   if ((rc = launch_conv<E, PF_LN, 0>(q, st))) return rc;
-  if ((rc = launch_attention(dtype, w.qkv, mask, w.ob, B, Tl, heads, st))) return rc;
+  if ((rc = launch_attention(dtype, w.qkv, mask, w.ob, B, Tl, heads, st, w.apart))) return rc;
   ConvArgs o = gemm_args(t.out, P, B, Tl);
   o.x0 = w.ob;
   o.y = x;
@@ -538,7 +602,8 @@ int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const fl
   f2.y = x;
   f2.resid = x;
   f2.ldr = C;
-  return launch_conv<E, 0, EF_RESID>(f2, st);
+  if ((rc = launch_conv<E, 0, EF_RESID>(f2, st))) return rc;
+  return mask_out ? mask_rows(dtype, x, B * Tl, C, mask, st) : 0;
 }
 
 template <class E>
@@ -548,33 +613,48 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   const float* m0 = w.m0;
   const float* m1 = w.m1;
   auto tbp = [&](int r) { return w.tb + ((size_t)ev * n_res + r) * C; };
+  // bf16 + vconv: every tensor a conv reads as x * mask is stored masked by its producer (the last
+  // transformer block of a chain, the down/up convs), so mt_vconv needs no input prologue
+  const bool mio = vconv && std::is_same<E, bf16>::value;
   auto tblocks = [&](int r, void* x, const float* m, int Tl) -> int {
-    for (const TB& t : tbs[r]) {
-      int e = tblock<E>(P, w, t, x, m, B, Tl, st);
+    const int nb = (int)tbs[r].size();
+    for (int j = 0; j < nb; ++j) {
+      int e = tblock<E>(P, w, tbs[r][j], x, m, mio && j == nb - 1, B, Tl, st);
       if (e) return e;
     }
     return 0;
   };
-  auto plain = [&](const GemmW& g, const void* x, const float* m, int Tl, void* out) -> int {
+  // m: the input mask; mo: the output frames' mask (masked-input mode)
+  auto plain = [&](const GemmW& g, const void* x, const float* m, const float* mo, int Tl, void* out) -> int {
+    if (mio && vc(g)) {
+      VConvArgs a = vargs(g, P, w, x, B, Tl, out);
+      a.emask = mo;
+      return launch_vconv(VE_MASK, a, st);
+    }
     ConvArgs a = gemm_args(g, P, B, Tl);
     a.x0 = x;
     a.y = out;
+    if (mio) {
+      a.emask = mo;
+      return launch_conv<E, 0, EF_MASK>(a, st);
+    }
     a.pmask = m;
     return launch_conv<E, PF_MASK, 0>(a, st);
   };
   // down 0 @T
-  if ((rc = resnet<E>(P, w, res[0], w.xin, nullptr, c_cond, c_cond, w.H0, m0, B, T, tbp(0), st))) return rc;
+  if ((rc = resnet<E>(P, w, res[0], w.xin, nullptr, c_cond, c_cond, false, w.H0, m0, B, T, tbp(0), st)))
+    return rc;
   if ((rc = tblocks(0, w.H0, m0, T))) return rc;
-  if ((rc = plain(down0, w.H0, m0, T, w.XA))) return rc;
+  if ((rc = plain(down0, w.H0, m0, m1, T, w.XA))) return rc;
   // down 1 @T/2
-  if ((rc = resnet<E>(P, w, res[1], w.XA, nullptr, C, C, w.H1, m1, B, T1, tbp(1), st))) return rc;
+  if ((rc = resnet<E>(P, w, res[1], w.XA, nullptr, C, C, mio, w.H1, m1, B, T1, tbp(1), st))) return rc;
   if ((rc = tblocks(1, w.H1, m1, T1))) return rc;
-  if ((rc = plain(down1, w.H1, m1, T1, w.XB))) return rc;
+  if ((rc = plain(down1, w.H1, m1, m1, T1, w.XB))) return rc;
   char* half[3] = {w.XA, w.XB, w.XC};
   int cur = 1;
   for (int i = 0; i < n_mid; ++i) {
     const int nx = (cur + 1) % 3;
-    if ((rc = resnet<E>(P, w, res[2 + i], half[cur], nullptr, C, C, half[nx], m1, B, T1, tbp(2 + i), st)))
+    if ((rc = resnet<E>(P, w, res[2 + i], half[cur], nullptr, C, C, mio, half[nx], m1, B, T1, tbp(2 + i), st)))
       return rc;
     if ((rc = tblocks(2 + i, half[nx], m1, T1))) return rc;
     cur = nx;
@@ -583,20 +663,26 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   {
     const int nx = (cur + 1) % 3;
     const int r = 2 + n_mid;
-    if ((rc = resnet<E>(P, w, res[r], half[cur], w.H1, C, 2 * C, half[nx], m1, B, T1, tbp(r), st))) return rc;
+    if ((rc = resnet<E>(P, w, res[r], half[cur], w.H1, C, 2 * C, mio, half[nx], m1, B, T1, tbp(r), st)))
+      return rc;
     if ((rc = tblocks(r, half[nx], m1, T1))) return rc;
-    if ((rc = plain(up0, half[nx], m1, T1, w.U))) return rc;  // ConvTranspose1d k4 s2 p1 -> T
+    if ((rc = plain(up0, half[nx], m1, m0, T1, w.U))) return rc;  // ConvTranspose1d k4 s2 p1 -> T
   }
   // up 1 @T: cat(U, skip=H0)
   {
     const int r = 3 + n_mid;
-    if ((rc = resnet<E>(P, w, res[r], w.U, w.H0, C, 2 * C, w.XF, m0, B, T, tbp(r), st))) return rc;
+    if ((rc = resnet<E>(P, w, res[r], w.U, w.H0, C, 2 * C, mio, w.XF, m0, B, T, tbp(r), st))) return rc;
     if ((rc = tblocks(r, w.XF, m0, T))) return rc;
-    if ((rc = plain(up1, w.XF, m0, T, w.U))) return rc;
+    if ((rc = plain(up1, w.XF, m0, m0, T, w.U))) return rc;
   }
   // final block + projection + ODE update
   int ntf = 0;
-  {
+  if (mio && vc(fconv)) {
+    VConvArgs a = vargs(fconv, P, w, w.U, B, T, w.y1);
+    a.gn_out = w.gn1;
+    if ((rc = launch_vconv(VE_GNSTATS, a, st))) return rc;
+    ntf = vconv_gn_parts(T, C);
+  } else {
     ConvArgs a = gemm_args(fconv, P, B, T);
     a.x0 = w.U;
     a.y = w.y1;

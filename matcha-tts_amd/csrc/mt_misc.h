@@ -26,6 +26,12 @@ int copy_rows(int dtype, const void* src, int ld_src, int rows, int C, void* dst
 // x[r][c] *= mask[r]
 int mask_rows(int dtype, void* x, int rows, int C, const float* mask, hipStream_t st);
 
+// ResnetBlock1D block tail (GroupNorm(8) -> Mish [-> + time bias] -> * mask, model.py Block1D/ResnetBlock1D)
+// for bf16 rows y[b][t][C] whose GroupNorm partial sums (fp64 (sum, sumsq) per (b, 32-channel group,
+// part), nparts per group) a conv epilogue produced: h = (mish(y * ga[b,c] + gs[b,c]) + tb[c]) * mask[b,t]
+int gn_apply(const void* y, int B, int T, int C, const double* part, int nparts, const float* gamma,
+             const float* beta, float eps, const float* tb, const float* mask, void* h, hipStream_t st);
+
 int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* emb, hipStream_t st);
 int rowdot(const float* x, int ldx, const float* W, const float* bias, float* y, int ldy, int yoff, int S,
            int O, int I, int pre, int post, hipStream_t st);
@@ -37,7 +43,10 @@ int alignment(const float* cum, const long long* ylen, int B, int Tx, int T, con
 int denorm_crop(const float* z, const float* mean, const float* stdv, int B, int C, int T, int Ty, float* mel,
                 hipStream_t st);
 
+// part (optional): key-split slots (attention_part_bytes, sized for the largest T launched on it);
+// with it an unpadded utterance's keys are split over several workgroups + a merge launch
 int launch_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
-                     hipStream_t stream);
+                     hipStream_t stream, float* part = nullptr);
+size_t attention_part_bytes(int B, int T, int heads);
 
 }  // namespace mt

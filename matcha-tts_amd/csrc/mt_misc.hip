@@ -265,33 +265,60 @@ int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* 
 
 // y[s][yoff + o] = post( sum_i W[o][i] * pre(x[s][i]) + bias[o] ); one wave per output o.
 // pre: 0 none, 1 mish ; post: 0 none, 1 silu
-__global__ void rowdot_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ W,
-                              const float* __restrict__ bias, float* __restrict__ y, int ldy,
-                              int yoff, int S, int O, int I, int pre, int post) {
-  const int lane = threadIdx.x & 63;
-  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (o >= O) return;
-  const float* w = W + (size_t)o * I;
-  for (int s = 0; s < S; ++s) {
-    const float* xs = x + (size_t)s * ldx;
-    float acc = 0.f;
-    for (int i = lane; i < I; i += 64) {
-      float xv = xs[i];
-      if (pre == 1) xv = xv * tanhf(log1pf(expf(xv)));
-      acc += w[i] * xv;
+// The time-embedding MLPs (model.py TimestepEmbedding, ResnetBlock1D.mlp): S <= 128 rows, I <= 1024.
+// pre(x) of RD_S rows is staged once per block in LDS, each wave keeps its output's weight row in
+// registers across all rows; per (s, o) the lane-strided sum + wave reduction order is fixed.
+constexpr int RD_S = 8, RD_NO = 2, RD_IMAX = 1024;
+__global__ __launch_bounds__(256) void rowdot_kernel(const float* __restrict__ x, int ldx,
+                                                     const float* __restrict__ W,
+                                                     const float* __restrict__ bias, float* __restrict__ y,
+                                                     int ldy, int yoff, int S, int O, int I, int pre, int post) {
+  __shared__ float xs[RD_S][RD_IMAX];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int KW = RD_IMAX / 64;
+  float wv[RD_NO][KW];
+  const int obase = (blockIdx.x * 4 + wave) * RD_NO;
+#pragma unroll
+  for (int j = 0; j < RD_NO; ++j)
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+      const int o = obase + j, i = lane + 64 * k;
+      wv[j][k] = (o < O && i < I) ? W[(size_t)o * I + i] : 0.f;
     }
-    acc = wave_sum(acc);
-    if (lane == 0) {
-      float v = acc + (bias ? bias[o] : 0.f);
-      if (post == 1) v = v / (1.f + expf(-v));
-      y[(size_t)s * ldy + yoff + o] = v;
+  for (int s0 = 0; s0 < S; s0 += RD_S) {
+    const int ns = min(RD_S, S - s0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < ns * I; e += 256) {
+      const int r = e / I, i = e - r * I;
+      float xv = x[(size_t)(s0 + r) * ldx + i];
+      if (pre == 1) xv = xv * tanhf(log1pf(expf(xv)));
+      xs[r][i] = xv;
+    }
+    __syncthreads();
+    for (int r = 0; r < ns; ++r) {
+#pragma unroll
+      for (int j = 0; j < RD_NO; ++j) {
+        const int o = obase + j;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < KW; ++k)
+          if (lane + 64 * k < I) acc += wv[j][k] * xs[r][lane + 64 * k];
+        acc = wave_sum(acc);
+        if (lane == 0 && o < O) {
+          float v = acc + (bias ? bias[o] : 0.f);
+          if (post == 1) v = v / (1.f + expf(-v));
+          y[(size_t)(s0 + r) * ldy + yoff + o] = v;
+        }
+      }
     }
   }
 }
 
 int rowdot(const float* x, int ldx, const float* W, const float* bias, float* y, int ldy, int yoff,
            int S, int O, int I, int pre, int post, hipStream_t st) {
-  hipLaunchKernelGGL(rowdot_kernel, dim3((O + 3) / 4), dim3(256), 0, st, x, ldx, W, bias, y, ldy, yoff,
+  MT_REQUIRE(I > 0 && I <= RD_IMAX && S > 0 && O > 0, "rowdot: I %d (max %d), S %d, O %d", I, RD_IMAX, S, O);
+  const int per = 4 * RD_NO;
+  hipLaunchKernelGGL(rowdot_kernel, dim3((O + per - 1) / per), dim3(256), 0, st, x, ldx, W, bias, y, ldy, yoff,
                      S, O, I, pre, post);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
@@ -427,6 +454,83 @@ int mask_rows(int dtype, void* x, int rows, int C, const float* mask, hipStream_
     hipLaunchKernelGGL(mask_rows_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (bf16*)x, rows, C, mask);
   else
     hipLaunchKernelGGL(mask_rows_kernel<float>, dim3(blocks), dim3(256), 0, st, (float*)x, rows, C, mask);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// one block = GN_FR frames of one utterance; C/8 threads x 8 channels (16 B) per frame row
+constexpr int GN_FR = 32;
+__global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ y, int T, int C,
+                                                       const double* __restrict__ part, int nparts,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float eps, const float* __restrict__ tb,
+                                                       const float* __restrict__ mask, bf16* __restrict__ h) {
+  __shared__ float ga[256], gs[256], gm[8], gr[8];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int G = C >> 5;
+  if (tid < G) {  // same merge order and formulas as the conv kernel's PF_GN pre-phase (mt_conv.hip)
+    const double* p = part + (size_t)(b * G + tid) * nparts * 2;
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = 0; i < nparts; ++i) {
+      s1 += p[2 * i];
+      s2 += p[2 * i + 1];
+    }
+    const double n = 32.0 * (double)T;
+    const double mean = s1 / n;
+    double var = s2 / n - mean * mean;
+    var = var < 0.0 ? 0.0 : var;
+    gm[tid] = (float)mean;
+    gr[tid] = (float)(1.0 / sqrt(var + (double)eps));
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    const float sc = gr[c >> 5] * gamma[c];
+    ga[c] = sc;
+    gs[c] = -sc * gm[c >> 5] + beta[c];
+  }
+  __syncthreads();
+  const int cpr = C >> 3;  // 16-byte groups per row
+  const int rows_per = 256 / cpr;
+  const int q = tid % cpr, c = 8 * q;
+  float tbv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) tbv[k] = tb ? tb[c + k] : 0.f;
+  // all of this thread's rows loaded before any math: GN_FR / rows_per 16-byte loads in flight
+  constexpr int NR = GN_FR / 8;  // rows per thread at C = 256 (fewer used at smaller C)
+  u32x4 v[NR];
+  float mk[NR];
+  const int t0 = blockIdx.x * GN_FR + tid / cpr;
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int t = min(t0 + j * rows_per, T - 1);
+    const size_t row = (size_t)b * T + t;
+    v[j] = *reinterpret_cast<const u32x4*>(y + row * C + c);
+    mk[j] = mask[row];
+  }
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int t = t0 + j * rows_per;
+    if (t >= T || t >= (int)(blockIdx.x + 1) * GN_FR) break;
+    const size_t row = (size_t)b * T + t;
+    u32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t w = v[j][e];
+      const float x0 = __uint_as_float(w << 16), x1 = __uint_as_float(w & 0xffff0000u);
+      const float r0 = (mish_f(x0 * ga[c + 2 * e] + gs[c + 2 * e]) + tbv[2 * e]) * mk[j];
+      const float r1 = (mish_f(x1 * ga[c + 2 * e + 1] + gs[c + 2 * e + 1]) + tbv[2 * e + 1]) * mk[j];
+      const bf16 h0 = (bf16)r0, h1 = (bf16)r1;
+      o[e] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    }
+    *reinterpret_cast<u32x4*>(h + row * C + c) = o;
+  }
+}
+
+int gn_apply(const void* y, int B, int T, int C, const double* part, int nparts, const float* gamma,
+             const float* beta, float eps, const float* tb, const float* mask, void* h, hipStream_t st) {
+  MT_REQUIRE(C % 32 == 0 && C <= 256 && C >= 64 && 256 % (C / 8) == 0 && nparts > 0, "gn_apply: C %d", C);
+  hipLaunchKernelGGL(gn_apply_kernel, dim3((T + GN_FR - 1) / GN_FR, B), dim3(256), 0, st, (const bf16*)y, T, C, part, nparts,
+                     gamma, beta, eps, tb, mask, (bf16*)h);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }

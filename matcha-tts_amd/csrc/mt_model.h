@@ -8,6 +8,7 @@
 
 #include "mt_conv.h"
 #include "mt_misc.h"
+#include "mt_vconv.h"
 
 namespace mt {
 
@@ -77,6 +78,9 @@ struct Decoder {
     GemmW qkv, out, ff1, ff2;
   };
   size_t zero_off = 0;  // 256 zero bytes (vconv padding rows)
+  // bf16: 1 = the ResnetBlock convs, down1 / up1 and the final block conv also run on mt_vconv (their
+  // inputs are then kept masked by their producers), 0 = generic conv kernel for those (A/B, tests)
+  int vconv = 1;
   std::vector<Res> res;                // down0, down1, mid..., up0, up1
   std::vector<std::vector<TB>> tbs;    // per resnet
   GemmW down0, down1, up0, up1, fconv, fproj;
@@ -91,6 +95,7 @@ struct Decoder {
     char *xin, *H0, *H1, *XA, *XB, *XC, *U, *XF, *y1, *y2, *qkv, *ob, *ff, *trash;
     float *zm, *m1, *emb, *h1, *h2, *tb, *lns;
     double *gn1, *gn2;
+    float* apart;  // attention key-split slots
     const float* m0;
   };
   Work carve(void* ws, int B, int T, int S) const;
@@ -104,10 +109,12 @@ struct Decoder {
   int eval(const char* P, const Work& w, int B, int T, int ev, const Euler& eu, hipStream_t st) const;
   template <class E>
   int resnet(const char* P, const Work& w, const Res& R, const void* x0, const void* x1, int c0, int cin,
-             void* out, const float* mask, int B, int Tl, const float* tb, hipStream_t st) const;
+             bool x_masked, void* out, const float* mask, int B, int Tl, const float* tb, hipStream_t st) const;
   template <class E>
-  int tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, int B, int Tl,
-             hipStream_t st) const;
+  int tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, bool mask_out, int B,
+             int Tl, hipStream_t st) const;
+  bool vc(const GemmW& g) const { return vconv && g.vc; }
+  VConvArgs vargs(const GemmW& g, const char* P, const Work& w, const void* x, int B, int Tl, void* y) const;
 
   int init_inputs(const Work& w, const float* z, float temperature, const float* mu_y, const float* spks,
                   int B, int T, hipStream_t st) const;

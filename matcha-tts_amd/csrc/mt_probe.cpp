@@ -46,7 +46,7 @@ void probe_end(int site, hipStream_t st, double flops, double bytes) {
 int probe_start(int site, int max_launches) {
   std::lock_guard<std::mutex> lk(g_mu);
   release();
-  MT_REQUIRE(site > PROBE_NONE && site <= PROBE_VCONV, "probe: unknown site %d", site);
+  MT_REQUIRE(site > PROBE_NONE && site <= PROBE_VCONV_DEC, "probe: unknown site %d", site);
   MT_REQUIRE(max_launches > 0 && max_launches <= (1 << 16), "probe: max_launches %d", max_launches);
   g_ev.resize(2 * (size_t)max_launches);
   for (hipEvent_t& e : g_ev) MT_CHECK_HIP(hipEventCreate(&e));

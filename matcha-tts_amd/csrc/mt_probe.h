@@ -10,7 +10,8 @@ enum ProbeSite {
   PROBE_NONE = 0,
   PROBE_RBFUSE_C64 = 1,  // fused HiFi-GAN ResBlock stage, 64 channels (stage 3 of v1)
   PROBE_RBFUSE_C32 = 2,  // fused HiFi-GAN ResBlock stage, 32 channels (stage 4 of v1)
-  PROBE_VCONV = 3,       // LDS-DMA persistent conv (HiFi-GAN stages 1-2 ResBlock convs)
+  PROBE_VCONV = 3,       // LDS-DMA persistent conv, HiFi-GAN ResBlock convs (k >= 3)
+  PROBE_VCONV_DEC = 4,   // LDS-DMA persistent conv, CFM decoder k = 3 convs (ResnetBlock, up/down, final)
 };
 
 bool probe_armed(int site);

@@ -18,11 +18,14 @@ enum : int {
   VE_LN = 32,    // LayerNorm of the input folded in: acc := rstd[n] * (acc - mean[n] * wsum[m])
                  // (gamma folded into W, beta into the bias at pack time; model.py:733-741)
   VE_SNAKE = 64, // v + ibeta[m] * sin(v * alpha[m])^2 after the bias (SnakeBeta, model.py:580-609)
+  VE_MASK = 128, // v * mask[frame] as the last step (a masked copy for consumers that read x * mask)
+  VE_GNSTATS = 256,  // per-(utterance, 32-channel group) partial sum / sum of squares of v (fp64) -> gn_out
 };
 
 struct VConvArgs {
-  const bf16* x;      // [B][L][cin], already activated
-  int B, L, cin;
+  const bf16* x;      // [B][L][c0], already activated: channels [0, c0)
+  const bf16* x1;     // [B][L][cin - c0]: channels [c0, cin) (a skip concatenation), or null
+  int B, L, cin, c0;  // c0 = cin for one source; a multiple of 64
   const bf16* w;      // [cin/64][taps][Mpad][64]
   const float* bias;  // [M]
   int M, Mpad, taps, dil, pad;
@@ -36,7 +39,13 @@ struct VConvArgs {
   const float* wsum;         // [M] row sums of the packed (gamma-folded, bf16) weights (VE_LN)
   const float* snake_alpha;  // [M] exp(alpha) (VE_SNAKE)
   const float* snake_ibeta;  // [M] 1 / (exp(beta) + 1e-9)
+  const float* emask;        // [B*L] frame mask (VE_MASK)
+  double* gn_out;            // [B][M/32][vconv_gn_parts(L, M)][2] (VE_GNSTATS)
+  int probe;                 // launch-probe site of k >= 2 launches (0: PROBE_VCONV)
 };
+
+// partial-sum slots per (utterance, group) that VE_GNSTATS writes: column tiles x waves across columns
+int vconv_gn_parts(int L, int M);
 
 bool vconv_supported(int cin, int cout, int k, int dil, int stride);
 // packed bytes of the [cin/64][taps][Mpad][64] image

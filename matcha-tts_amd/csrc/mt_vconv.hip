@@ -148,9 +148,12 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     }
   };
   const int R = BN + (taps - 1) * dil;
+  const int c0 = a.c0;
   auto issue_x = [&](int b, int n0, int c, int buf) {
     const int f0 = n0 - a.pad;
-    const bf16* xb = a.x + (size_t)b * L * cin + c * 64;
+    const bool lo = c * 64 < c0;  // chunk from the first or the second source (skip concatenation)
+    const int ldx = lo ? c0 : cin - c0;
+    const bf16* xb = lo ? a.x + (size_t)b * L * c0 + c * 64 : a.x1 + (size_t)b * L * (cin - c0) + (c * 64 - c0);
     char* dst = smem + NWSLOT * WSLOT + buf * XBUF;
 #pragma unroll
     for (int i = 0; i < NXW; ++i) {
@@ -159,7 +162,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
       const bool ok = r < R && f >= 0 && f < L;
-      const bf16* src = ok ? xb + (size_t)f * cin + q * 8 : a.zero + q * 8;
+      const bf16* src = ok ? xb + (size_t)f * ldx + q * 8 : a.zero + q * 8;
       glds16(src, dst + j * 1024);
     }
   };
@@ -186,6 +189,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   // step, consumed after its MFMAs
   u32x4 rv[2][FN], yv[2][FN];
   float2 lns[FN];  // (mean, rstd) of each fragment column's frame (VE_LN)
+  float mk[FN];    // frame mask of each fragment column (VE_MASK)
   auto epi_loads = [&](int ti) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
@@ -200,6 +204,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
         if constexpr ((EF & VE_ACCUM) != 0) yv[fp][fn] = *reinterpret_cast<const u32x4*>(a.y + o);
         if constexpr ((EF & VE_LN) != 0)
           if (fp == 0) lns[fn] = *reinterpret_cast<const float2*>(a.ln_stats + 2 * (rowbase + n));
+        if constexpr ((EF & VE_MASK) != 0)
+          if (fp == 0) mk[fn] = a.emask[rowbase + n];
       }
   };
   // Every lane stores (frames past L go to a trash line), so the store count per tile is a constant the
@@ -213,6 +219,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
     const size_t rowbase = (size_t)b * L;
+    double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};  // VE_GNSTATS: this lane's sums per 32-channel group
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -256,6 +263,13 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
             if constexpr ((EF & VE_RESID) != 0) v = v + bf2(rr[r >> 1], r & 1);
             if constexpr ((EF & VE_ACCUM) != 0) v = bf2(yy[r >> 1], r & 1) + v;
             if constexpr ((EF & VE_DIV) != 0) v = v / a.div;
+            if constexpr ((EF & VE_GNSTATS) != 0) {
+              if (n0 + wn * WNC + fn * 16 + l16 < L) {
+                gs[fp] += (double)v;
+                gq[fp] += (double)v * (double)v;
+              }
+            }
+            if constexpr ((EF & VE_MASK) != 0) v = v * mk[fn];
             const bf16 rb = (bf16)v;
             const bf16 av = (bf16)lrelu_f((float)rb, a.slope);
             ob[r] = (EF & VE_ACT) ? av : rb;
@@ -278,6 +292,21 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
           *reinterpret_cast<u32x4*>(ok ? a.y2 + o : a.trash + 8 * lane) = u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]};
         }
       }
+    if constexpr ((EF & VE_GNSTATS) != 0) {
+      // fm pair fp covers channels m0 + wm*64 + 32*fp .. +31: one GroupNorm(8) group of the 256 channels
+      const int nparts = ntn * TT::WAVES_N, part = (n0 / BN) * TT::WAVES_N + wn;
+      const int G = a.M / 32;
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp) {
+        const double s1 = wave_sum_d(gs[fp]), s2 = wave_sum_d(gq[fp]);
+        if (lane == 0) {
+          const int g = (m0 + wm * 64) / 32 + fp;
+          double* o = a.gn_out + (((size_t)b * G + g) * nparts + part) * 2;
+          o[0] = s1;
+          o[1] = s2;
+        }
+      }
+    }
   };
 
   // ---- staging cursors and DMA bookkeeping (all wave-uniform) ----
@@ -382,7 +411,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();
     const bool tile_end = t == taps - 1 && c == nch - 1;
-    if constexpr ((EF & (VE_RESID | VE_ACCUM | VE_LN)) != 0)
+    if constexpr ((EF & (VE_RESID | VE_ACCUM | VE_LN | VE_MASK)) != 0)
       if (tile_end) epi_loads(ti);
     if (t == 0) stage_x();  // rows of chunk u+NXB-1 into the buffer chunk u-1 used
     if constexpr (NWSLOT > 3) {  // weights of step qq + NWSLOT - 1 into the slot step qq-1 used
@@ -483,6 +512,11 @@ int vconv_wsum(const void* img, int cin, int taps, int cout, float* wsum, hipStr
   return 0;
 }
 
+int vconv_gn_parts(int L, int M) {
+  const int BM = M % 128 == 0 ? 128 : 64;
+  return (L + BN - 1) / BN * (8 / (BM / 64));
+}
+
 int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(a0.x && a0.w && a0.bias && a0.y && a0.zero && a0.trash, "vconv: null pointer");
   MT_REQUIRE(a0.B > 0 && a0.L > 0 && a0.cin % 64 == 0 && a0.M % 64 == 0 && a0.Mpad == a0.M && a0.M <= MMAX,
@@ -493,8 +527,13 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(!(ef & VE_DUAL) || a0.y2, "vconv: y2");
   MT_REQUIRE(!(ef & VE_LN) || (a0.ln_stats && a0.wsum), "vconv: LN stats / weight sums");
   MT_REQUIRE(!(ef & VE_SNAKE) || (a0.snake_alpha && a0.snake_ibeta), "vconv: snake params");
-  const bool k1 = a0.taps == 1;
+  MT_REQUIRE(!(ef & VE_MASK) || a0.emask, "vconv: mask");
+  MT_REQUIRE(!(ef & VE_GNSTATS) || (a0.gn_out && a0.taps > 1 && a0.M % 32 == 0), "vconv: GN statistics");
   VConvArgs a = a0;
+  if (a.c0 == 0) a.c0 = a.cin;  // one source
+  MT_REQUIRE(a.c0 == a.cin || (a.x1 && a.c0 % 64 == 0 && a.c0 > 0 && a.c0 < a.cin), "vconv: channel split %d/%d",
+             a.c0, a.cin);
+  const bool k1 = a0.taps == 1;
   if (k1) {  // no halo: the utterances' frames are one contiguous sequence of B*L columns
     MT_REQUIRE(a0.pad == 0, "vconv: 1x1 conv with padding");
     a.L = a0.B * a0.L;
@@ -511,7 +550,8 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   const int touts = 1 + ((ef & VE_RESID) ? 1 : 0) + ((ef & VE_ACCUM) ? 1 : 0) + ((ef & VE_DUAL) ? 1 : 0);
   const double bytes = 2.0 * a.B * a.L * ((double)a.cin + (double)a.M * touts) + 2.0 * a.M * a.cin * a.taps;
   // the probe site covers the HiFi-GAN ResBlock convs (k >= 3), the bench's roofline family
-  if (!k1) probe_begin(PROBE_VCONV, st);
+  const int site = a.probe ? a.probe : PROBE_VCONV;
+  if (!k1) probe_begin(site, st);
 #define MT_VCASE(E)                                                                                \
   case E:                                                                                          \
     if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false>), dim3(G), dim3(NT), 0, st, a); \
@@ -535,6 +575,8 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE(VE_RESID | VE_ACCUM)
       MT_VCASE(VE_RESID | VE_DIV)
       MT_VCASE(VE_RESID | VE_ACCUM | VE_DIV)
+      MT_VCASE(VE_GNSTATS)
+      MT_VCASE(VE_MASK)
       MT_VCASE(0)
       default: set_error("vconv: epilogue %d not compiled in", ef); return -1;
     }
@@ -543,6 +585,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE1(VE_LN)
       MT_VCASE1(VE_LN | VE_SNAKE)
       MT_VCASE1(VE_RESID)
+      MT_VCASE1(VE_RESID | VE_MASK)
       MT_VCASE1(0)
       default: set_error("vconv: 1x1 epilogue %d not compiled in", ef); return -1;
     }
@@ -550,7 +593,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
 #undef MT_VCASE
 #undef MT_VCASE1
   MT_CHECK_HIP(hipGetLastError());
-  if (!k1) probe_end(PROBE_VCONV, st, flops, bytes);
+  if (!k1) probe_end(site, st, flops, bytes);
   return 0;
 }
 

@@ -198,6 +198,10 @@ class DecoderEngine:
         self._packed, self._fp = packed, fp
         return packed
 
+    def set_vconv(self, enable) -> None:
+        """bf16: 1 (default) ResnetBlock / down / up / final convs on mt_vconv, 0 generic conv kernel."""
+        check(lib().mt_decoder_set_vconv(self.h, int(bool(enable))), "decoder_set_vconv")
+
     def solve(self, packed, z_noise, temperature, mu_y, mask, spks, n_timesteps, solver="euler",
               out=None):
         B, C, T = mu_y.shape
@@ -254,7 +258,7 @@ class VocoderEngine:
         check(lib().mt_vocoder_set_fusion(self.h, int(bool(enable))), "vocoder_set_fusion")
 
     def set_vconv(self, mode) -> None:
-        """0 generic per-layer kernel, 1 (default) vconv for the 128/256-channel stages, 2 also for 64."""
+        """0 generic per-layer kernel, 1 vconv for the 128/256-channel stages, 2 (default) also for 64."""
         check(lib().mt_vocoder_set_vconv(self.h, int(mode)), "vocoder_set_vconv")
 
     def __del__(self):
@@ -429,7 +433,7 @@ def op_attention(qkv: torch.Tensor, mask: torch.Tensor, heads: int, precision="f
 
 
 # ---------------------------------------------------------------------------------- launch probe
-PROBE_RBFUSE_C64, PROBE_RBFUSE_C32, PROBE_VCONV = 1, 2, 3
+PROBE_RBFUSE_C64, PROBE_RBFUSE_C32, PROBE_VCONV, PROBE_VCONV_DEC = 1, 2, 3, 4
 
 
 def probe_start(site: int, max_launches: int) -> None:

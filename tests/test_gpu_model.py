@@ -233,6 +233,34 @@ def test_decoder_mid_size_vs_oracle_and_determinism():
     assert (one - out1[1:2]).abs().max() < 1e-4
 
 
+@pytest.mark.parametrize("T,lens", [(200, [200, 151, 98]), (600, [600, 411, 130])])
+def test_decoder_bf16_vconv_path_vs_generic_and_oracle(T, lens):
+    """bf16 decoder with its k=3 / ResnetBlock convs on mt_vconv (producer-masked inputs, GroupNorm
+    partials from the conv epilogue, skip concatenation as two sources) vs the generic conv path and
+    vs the fp32 oracle; ragged rows so padded frames at both U-Net levels are exercised."""
+    from oracle import matcha_oracle as O
+    from matcha_hip import synthetic
+    dec = make_decoder(160, "bf16")
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(
+        [(k, tuple(v.shape)) for k, v in dec.state_dict().items()], 7).items()}
+    dec = _load(dec, sd)
+    B = len(lens)
+    g = torch.Generator().manual_seed(T)
+    x, mu = torch.randn(B, 80, T, generator=g), torch.randn(B, 80, T, generator=g)
+    mask = (torch.arange(T)[None] < torch.tensor(lens)[:, None]).float()[:, None]
+    tt = torch.full((B,), 0.6)
+    args = (x.cuda(), mask.cuda(), (mu * mask).cuda(), tt.cuda())
+    dec.engine().set_vconv(0)
+    gen = dec(*args).cpu()
+    dec.engine().set_vconv(1)
+    out = dec(*args).cpu()
+    assert torch.equal(out, dec(*args).cpu())  # deterministic
+    ref = O.decoder_forward(sd, x, mask, mu * mask, tt)
+    assert rel_rms(out, gen) < 1e-2, rel_rms(out, gen)
+    assert rel_rms(out, ref) < 2e-2, rel_rms(out, ref)
+    assert rel_rms(gen, ref) < 2e-2
+
+
 def test_vocoder_mid_size_vs_oracle():
     from oracle import matcha_oracle as O
     from hifigan.config import v1
