@@ -60,7 +60,7 @@ struct Tile {
 template <class E, class TL, int PF, int EF, int TAG = 0>
 __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
   constexpr int BM = TL::BM, BN = TL::BN, WAVES_M = TL::WAVES_M, WAVES_N = TL::WAVES_N;
-  constexpr int NT = TL::NT, NWAVES = WAVES_M * WAVES_N, TG = TL::TG;
+  constexpr int NT = TL::NT, TG = TL::TG;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int FM = WM / 16, FN = WN / 16;
   constexpr int VN = Vec16<E>::N;                 // elements per 16 bytes
@@ -586,6 +586,7 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
   X(PF_MASK, EF_RELU, CFG_BIG | CFG_SMALLN | CFG_C5)                                     \
   X(PF_MASK, EF_MASK | EF_RESID, CFG_BIG | CFG_SMALLN | CFG_C5)                          \
   X(0, EF_MASK, CFG_BIG | CFG_SMALLN | CFG_G6)                                           \
+  X(0, EF_DUAL, CFG_BIG | CFG_SMALLN)                                                    \
   X(PF_MASK, EF_MASK | EF_OUTF32, CFG_16 | CFG_32)
 
 #define MT_DEFINE_LAUNCH(PFV, EFV, CFGV)                                                    \

@@ -43,6 +43,7 @@ struct GemmW {
   size_t w_off = 0, b_off = 0;
   size_t v_off = 0;  // vconv image [cin/64][taps][Mpad128][64] (bf16 HiFi-GAN convs, mt_vconv.h)
   bool vc = false;
+  int vrows = 0;     // ConvTranspose on vconv: polyphase rows per image (M / vrows images back to back)
 };
 
 GemmW make_conv(int cout, int cin, int k, int stride, int pad, int dil, std::vector<int> w, int b,
@@ -193,7 +194,11 @@ struct Vocoder {
   template <class E>
   int forward_t(const char* P, const float* mel, int B, int T, float* wav, char* ws, hipStream_t st) const;
   int stage_vconv(const char* P, int i, int B, int L, const char* X, const char* XA, char* XS, char* Tb, char* R,
-                  char* RA, char* trash, hipStream_t st) const;
+                  char* RA, char* trash, bool act_out, hipStream_t st) const;
+  // upsampler i runs on vconv: its input lrelu(xs) is written by the producer (conv_pre / stage i-1)
+  bool ups_vc(int i) const;
+  int ups_vconv(const char* P, int i, int B, int L, const char* xa, char* X, char* XA, bool dual, char* trash,
+                hipStream_t st) const;
 };
 
 }  // namespace mt

@@ -41,7 +41,15 @@ struct VConvArgs {
   const float* snake_ibeta;  // [M] 1 / (exp(beta) + 1e-9)
   const float* emask;        // [B*L] frame mask (VE_MASK)
   double* gn_out;            // [B][M/32][vconv_gn_parts(L, M)][2] (VE_GNSTATS)
-  int probe;                 // launch-probe site of k >= 2 launches (0: PROBE_VCONV)
+  int probe;                 // launch-probe site of k >= 2 launches (0: PROBE_VCONV, < 0: none)
+  // Output placement (all 0 = the plain [B][L][M] layout). ConvTranspose1d as a polyphase conv
+  // (rows = phase x C_out) writes column n, row m to element n * ldy + m - yshift of its utterance,
+  // kept when it lies in [0, ylim); plain / dual epilogues only.
+  int Lout;            // output columns per utterance
+  int ldy;             // elements between consecutive columns of y
+  int yshift;
+  int ylim;
+  long long ystride;   // elements per utterance of y
 };
 
 // partial-sum slots per (utterance, group) that VE_GNSTATS writes: column tiles x waves across columns

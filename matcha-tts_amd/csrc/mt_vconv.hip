@@ -106,7 +106,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int taps = a.taps, dil = a.dil, L = a.L, cin = a.cin;
   const int nch = cin >> 6;
   const int S = nch * taps;
-  const int ntn = (L + BN - 1) / BN, ntm = a.Mpad / BM;
+  const int ntn = (a.Lout + BN - 1) / BN, ntm = a.Mpad / BM;
   const int ntiles = a.B * ntn * ntm;
   const int G = gridDim.x, g = blockIdx.x;
   const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
@@ -218,7 +218,6 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   auto epilogue = [&](int ti) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
-    const size_t rowbase = (size_t)b * L;
     double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};  // VE_GNSTATS: this lane's sums per 32-channel group
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
@@ -283,8 +282,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
         swap16(o1[0][0], o1[1][0]);
         swap16(o1[0][1], o1[1][1]);
         const int n = n0 + wn * WNC + fn * 16 + l16;
-        const bool ok = n < L;
-        const size_t o = (rowbase + n) * a.M + m0 + ch16 + fp * 32;
+        const int e = n * a.ldy + m0 + ch16 + fp * 32 - a.yshift;  // element of this utterance's output
+        const bool ok = n < a.Lout && e >= 0 && e < a.ylim;
+        const size_t o = (size_t)b * a.ystride + e;
         *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
         if constexpr ((EF & VE_DUAL) != 0) {
           swap16(o2[0][0], o2[1][0]);
@@ -461,7 +461,6 @@ __global__ void vconv_repack_kernel(const bf16* __restrict__ src, int Mpad0, int
 }
 
 bool vconv_supported(int cin, int cout, int k, int dil, int stride) {
-  // k >= 2: a chunk's rows are staged during its predecessor's first step and read one step later
   // k >= 2 convs stage a chunk's rows during its predecessor's first step and read them a step later;
   // 1x1 convs use the K1 pipeline (rows staged two chunks ahead)
   return stride == 1 && cin % 64 == 0 && cout % 64 == 0 && cout <= MMAX && (k == 1 || BN + (k - 1) * dil <= 320);
@@ -534,24 +533,36 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(a.c0 == a.cin || (a.x1 && a.c0 % 64 == 0 && a.c0 > 0 && a.c0 < a.cin), "vconv: channel split %d/%d",
              a.c0, a.cin);
   const bool k1 = a0.taps == 1;
+  const bool placed = a0.Lout || a0.ldy || a0.yshift || a0.ylim || a0.ystride;
+  MT_REQUIRE(!placed || (!k1 && (ef & ~VE_DUAL) == 0 && a0.Lout > 0 && a0.ldy >= a0.M && a0.ylim > 0 &&
+                         a0.ystride >= a0.ylim && a0.yshift % 8 == 0 && a0.ldy % 8 == 0),
+             "vconv: placed output (ConvTranspose) geometry / epilogue %d", ef);
   if (k1) {  // no halo: the utterances' frames are one contiguous sequence of B*L columns
     MT_REQUIRE(a0.pad == 0, "vconv: 1x1 conv with padding");
     a.L = a0.B * a0.L;
     a.B = 1;
   }
+  if (!placed) {
+    MT_REQUIRE((long long)a.L * a.M < (1ll << 31), "vconv: %d frames x %d channels", a.L, a.M);
+    a.Lout = a.L;
+    a.ldy = a.M;
+    a.ylim = a.L * a.M;
+    a.ystride = (long long)a.L * a.M;
+  }
   const int BM = a.M % 128 == 0 ? 128 : 64;
-  long ntiles = (long)a.B * ((a.L + BN - 1) / BN) * (a.Mpad / BM);
+  long ntiles = (long)a.B * ((a.Lout + BN - 1) / BN) * (a.Mpad / BM);
   // 1x1 GEMMs whose 256-frame tiles would leave CUs idle (the decoder's half-resolution blocks):
   // 128-frame tiles double the parallelism
   const bool small = k1 && ntiles < (long)cu_count();
   if (small) ntiles = (long)((a.L + 127) / 128) * (a.Mpad / BM);
   const int G = (int)std::min<long>(ntiles, cu_count());
-  const double flops = 2.0 * a.M * a.cin * a.taps * (double)a.B * a.L;
+  const double flops = 2.0 * a.M * a.cin * a.taps * (double)a.B * a.Lout;
   const int touts = 1 + ((ef & VE_RESID) ? 1 : 0) + ((ef & VE_ACCUM) ? 1 : 0) + ((ef & VE_DUAL) ? 1 : 0);
-  const double bytes = 2.0 * a.B * a.L * ((double)a.cin + (double)a.M * touts) + 2.0 * a.M * a.cin * a.taps;
+  const double bytes = 2.0 * a.B * ((double)a.L * a.cin + (double)a.Lout * a.M * touts) + 2.0 * a.M * a.cin * a.taps;
   // the probe site covers the HiFi-GAN ResBlock convs (k >= 3), the bench's roofline family
   const int site = a.probe ? a.probe : PROBE_VCONV;
-  if (!k1) probe_begin(site, st);
+  const bool probed = !k1 && site > 0;
+  if (probed) probe_begin(site, st);
 #define MT_VCASE(E)                                                                                \
   case E:                                                                                          \
     if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false>), dim3(G), dim3(NT), 0, st, a); \
@@ -577,6 +588,9 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE(VE_RESID | VE_ACCUM | VE_DIV)
       MT_VCASE(VE_GNSTATS)
       MT_VCASE(VE_MASK)
+      MT_VCASE(VE_DUAL)
+      MT_VCASE(VE_RESID | VE_DIV | VE_DUAL)
+      MT_VCASE(VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL)
       MT_VCASE(0)
       default: set_error("vconv: epilogue %d not compiled in", ef); return -1;
     }
@@ -593,7 +607,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
 #undef MT_VCASE
 #undef MT_VCASE1
   MT_CHECK_HIP(hipGetLastError());
-  if (!k1) probe_end(site, st, flops, bytes);
+  if (probed) probe_end(site, st, flops, bytes);
   return 0;
 }
 

@@ -103,7 +103,18 @@ int Vocoder::init(int resblock_, const std::vector<int>& ur, const std::vector<i
           }
       any_vc = true;
     }
-    if (any_vc) zero_off = pk.take(256);
+    if (any_vc) {
+      zero_off = pk.take(256);
+      // upsamplers as polyphase convs (rows = phase x C_out, <= 1024 rows per image)
+      for (GemmW& g : ups) {
+        const int ng = (g.M + 1023) / 1024;
+        const int rows = g.M / ng;
+        if (g.M % ng || g.cout % 8 || !vconv_supported(g.cin, rows, g.taps, 1, 1)) continue;
+        g.vc = true;
+        g.vrows = rows;
+        g.v_off = pk.take((size_t)ng * vconv_packed_bytes(g.cin, rows, g.taps));
+      }
+    }
   }
   {
     int w = L.add("conv_post.weight", {1, ch, 7});
@@ -118,8 +129,15 @@ int Vocoder::pack(const float* const* p, void* packed, hipStream_t st) const {
   char* P = (char*)packed;
   int rc;
   if ((rc = pack_gemm(pre, dtype, p, P, st))) return rc;
-  for (const GemmW& g : ups)
+  for (const GemmW& g : ups) {
     if ((rc = pack_gemm(g, dtype, p, P, st))) return rc;
+    if (!g.vc) continue;
+    for (int gi = 0; gi < g.M / g.vrows; ++gi) {
+      const char* src = P + g.w_off + (size_t)gi * g.vrows * g.taps * g.cin_pad * esize;
+      char* dst = P + g.v_off + (size_t)gi * vconv_packed_bytes(g.cin, g.vrows, g.taps);
+      if ((rc = vconv_repack(src, g.vrows, g.taps, g.cin_pad, g.cin, g.vrows, dst, st))) return rc;
+    }
+  }
   for (size_t i = 0; i < rb1.size(); ++i) {
     for (const GemmW& g : rb1[i])
       if ((rc = pack_gemm(g, dtype, p, P, st))) return rc;
@@ -153,6 +171,50 @@ bool Vocoder::stage_vc(int i) const {
   return vconv >= 2 || !(fuse && rbfuse_supported(dtype, C));
 }
 
+bool Vocoder::ups_vc(int i) const {
+  return vconv && dtype == BF16 && ups[(size_t)i].vc && (i == 0 || stage_vc(i - 1));
+}
+
+// ConvTranspose1d(k = taps*s, stride s, pad p) on vconv: column n (n in [0, L+1)) of the polyphase conv
+// computes rows (phase, c) = sum_t W[phase, c, t] . xa[n - (taps-1) + t]; it is output frame
+// s*n + phase - p, i.e. element n * (s*C) + phase*C + c - p*C of the utterance's [Tout][C] output, and
+// exactly the frames in [0, Tout) are kept (hifigan/models.py:184-186; the generic kernel's ConvT
+// mapping, mt_conv.hip ups/opad)
+int Vocoder::ups_vconv(const char* P, int i, int B, int L, const char* xa, char* X, char* XA, bool dual,
+                       char* trash, hipStream_t st) const {
+  const GemmW& g = ups[(size_t)i];
+  int Tout = 0, Ncols = 0;
+  gemm_geom(g, L, &Tout, &Ncols);
+  int rc;
+  for (int gi = 0; gi < g.M / g.vrows; ++gi) {
+    VConvArgs a{};
+    a.x = (const bf16*)xa;
+    a.B = B;
+    a.L = L;
+    a.cin = g.cin;
+    a.w = (const bf16*)(P + g.v_off + (size_t)gi * vconv_packed_bytes(g.cin, g.vrows, g.taps));
+    a.bias = (const float*)(P + g.b_off) + (size_t)gi * g.vrows;
+    a.M = a.Mpad = g.vrows;
+    a.taps = g.taps;
+    a.dil = 1;
+    a.pad = g.gpad;
+    a.y = (bf16*)X;
+    a.y2 = (bf16*)XA;
+    a.slope = 0.1f;
+    a.div = 1.f;
+    a.zero = (const bf16*)(P + zero_off);
+    a.trash = (bf16*)trash;
+    a.probe = -1;
+    a.Lout = Ncols;
+    a.ldy = g.M;
+    a.yshift = g.opad * g.cout - gi * g.vrows;
+    a.ylim = Tout * g.cout;
+    a.ystride = (long long)Tout * g.cout;
+    if ((rc = launch_vconv(dual ? VE_DUAL : 0, a, st))) return rc;
+  }
+  return 0;
+}
+
 size_t Vocoder::workspace_bytes(int B, int T) const {
   const size_t big = align256((size_t)B * T * frame_elems() * esize);
   // + XA, RA: the activated copies the vconv stages read
@@ -166,7 +228,7 @@ size_t Vocoder::workspace_bytes(int B, int T) const {
 // Rounding points equal the generic per-layer path's: every stored tensor is rounded to bf16 and the
 // activated copies are lrelu of the rounded values.
 int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, const char* XA, char* XS, char* Tb,
-                         char* R, char* RA, char* trash, hipStream_t st) const {
+                         char* R, char* RA, char* trash, bool act_out, hipStream_t st) const {
   const int nk = (int)rb_kernels.size();
   const bf16* zero = (const bf16*)(P + zero_off);
   int rc;
@@ -215,6 +277,10 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
         b.y = (bf16*)XS;
         if (j > 0) ef |= VE_ACCUM;
         if (j == nk - 1) ef |= VE_DIV;
+        if (j == nk - 1 && act_out) {  // lrelu(xs) for the next upsampler, in RA (this pair's conv1 read it)
+          b.y2 = (bf16*)RA;
+          ef |= VE_DUAL;
+        }
       }
       if ((rc = launch_vconv(ef, b, st))) return rc;
     }
@@ -240,7 +306,15 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     ConvArgs a = gemm_args(pre, P, B, T);
     a.x0 = xm;
     a.y = XS;
-    if ((rc = launch_conv<E, 0, 0>(a, st))) return rc;
+    bool dual = false;
+    if constexpr (std::is_same<E, bf16>::value) dual = ups_vc(0);
+    if (dual) {  // + lrelu(xs) in RA, the first upsampler's vconv input
+      a.y2 = RA;
+      a.slope = 0.1f;
+      if ((rc = launch_conv<E, 0, EF_DUAL>(a, st))) return rc;
+    } else if ((rc = launch_conv<E, 0, 0>(a, st))) {
+      return rc;
+    }
   }
   int L = T;
   const int nk = (int)rb_kernels.size();
@@ -250,17 +324,26 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     u.y = X;
     u.slope = 0.1f;
     const int C = ups[i].cout;
+    bool done_up = false;
     if constexpr (std::is_same<E, bf16>::value) {
-      if (stage_vc((int)i)) {
+      const bool svc = stage_vc((int)i);
+      if (ups_vc((int)i)) {  // polyphase vconv from lrelu(xs) (RA); + XA = lrelu(X) for a vconv stage
+        if ((rc = ups_vconv(P, (int)i, B, L, RA, X, XA, svc, trash, st))) return rc;
+        done_up = true;
+      }
+      if (svc) {
         // X and XA = lrelu(X): the three resblocks' first convs read XA, their residual X
-        u.y2 = XA;
-        if ((rc = launch_conv<E, PF_LRELU, EF_DUAL>(u, st))) return rc;
+        if (!done_up) {
+          u.y2 = XA;
+          if ((rc = launch_conv<E, PF_LRELU, EF_DUAL>(u, st))) return rc;
+        }
         L = u.Tout;
-        if ((rc = stage_vconv(P, (int)i, B, L, X, XA, XS, Tb, R, RA, trash, st))) return rc;
+        const bool act_out = i + 1 < ups.size() && ups_vc((int)i + 1);
+        if ((rc = stage_vconv(P, (int)i, B, L, X, XA, XS, Tb, R, RA, trash, act_out, st))) return rc;
         continue;
       }
     }
-    if ((rc = launch_conv<E, PF_LRELU, 0>(u, st))) return rc;
+    if (!done_up && (rc = launch_conv<E, PF_LRELU, 0>(u, st))) return rc;
     L = u.Tout;
     bool uniform = true;
     for (const auto& dl : rb_dils) uniform = uniform && dl.size() == rb_dils[0].size();
