@@ -384,6 +384,7 @@ size_t Decoder::workspace_bytes(int B, int T, int S) const {
   n += align256((size_t)S * n_res * C * 4);           // tb
   n += 4096;                                          // trash (vconv stores past the last frame)
   n += align256(attention_part_bytes(B, T, heads));   // attention key-split slots
+  n += align256(BT * (C / 64) * 2 * 4);               // lnp
   return n;
 }
 
@@ -421,6 +422,7 @@ Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
   w.tb = (float*)take((size_t)S * n_res * C * 4);
   w.trash = take(4096);
   w.apart = (float*)take(attention_part_bytes(B, T, heads));
+  w.lnp = (float*)take(BT * (C / 64) * 2 * 4);
   w.m0 = nullptr;
   return w;
 }
@@ -461,6 +463,7 @@ VConvArgs Decoder::vargs(const GemmW& g, const char* P, const Work& w, const voi
   a.zero = (const bf16*)(P + zero_off);
   a.trash = (bf16*)w.trash;
   a.ln_stats = w.lns;
+  a.ln_eps = 1e-5f;
   a.probe = PROBE_VCONV_DEC;
   return a;
 }
@@ -473,8 +476,9 @@ VConvArgs Decoder::vargs(const GemmW& g, const char* P, const Work& w, const voi
 template <class E>
 int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, const void* x1, int c0,
                     int cin, bool x_masked, void* out, const float* mask, int B, int Tl, const float* tb,
-                    hipStream_t st) const {
+                    bool* row_stats, hipStream_t st) const {
   int rc, nt1 = 0, nt2 = 0;
+  *row_stats = false;
   const float* g1 = (const float*)(P + R.gn1_off);
   const float* g2 = (const float*)(P + R.gn2_off);
   // block 1 -> y1 + gn1
@@ -528,7 +532,9 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
     c.c0 = c0;
     c.cin = cin;
     c.resid = (const bf16*)w.y2;
-    return launch_vconv(VE_RESID, c, st);
+    c.row_out = w.lnp;  // the LayerNorm partials of the transformer block that reads `out`
+    *row_stats = true;
+    return launch_vconv(VE_RESID | VE_ROWSTATS, c, st);
   }
   ConvArgs c = gemm_args(R.res, P, B, Tl);
   c.x0 = x0;
@@ -548,27 +554,35 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
 }
 
 template <class E>
-int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, bool mask_out, int B,
-                    int Tl, hipStream_t st) const {
+int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, bool mask_out,
+                    bool row_stats, int B, int Tl, hipStream_t st) const {
   int rc;
   if constexpr (std::is_same<E, bf16>::value) {
     if (t.qkv.vc && t.out.vc && t.ff1.vc && t.ff2.vc) {
       // bf16: the four GEMMs on mt_vconv's 1x1 pipeline; LayerNorm folded into the QKV / FF1 epilogues
       auto vargs = [&](const GemmW& g, const void* xin, void* y) { return this->vargs(g, P, w, xin, B, Tl, y); };
-      if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
+      // LayerNorm statistics: per-slab partials from the producing conv's epilogue (VE_ROWSTATS) when it
+      // wrote them, else a row-statistics pass
       VConvArgs q = vargs(t.qkv, x, w.qkv);
       q.wsum = (const float*)(P + t.wsq_off);
-      if ((rc = launch_vconv(VE_LN, q, st))) return rc;
+      if (row_stats) {
+        q.ln_stats = w.lnp;
+        if ((rc = launch_vconv(VE_LN | VE_LNP, q, st))) return rc;
+      } else {
+        if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
+        if ((rc = launch_vconv(VE_LN, q, st))) return rc;
+      }
       if ((rc = launch_attention(dtype, w.qkv, mask, w.ob, B, Tl, heads, st, w.apart))) return rc;
       VConvArgs o = vargs(t.out, w.ob, x);
       o.resid = (const bf16*)x;
-      if ((rc = launch_vconv(VE_RESID, o, st))) return rc;
-      if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
+      o.row_out = w.lnp;
+      if ((rc = launch_vconv(VE_RESID | VE_ROWSTATS, o, st))) return rc;
       VConvArgs f1 = vargs(t.ff1, x, w.ff);
+      f1.ln_stats = w.lnp;
       f1.wsum = (const float*)(P + t.wsf_off);
       f1.snake_alpha = (const float*)(P + t.snake_off);
       f1.snake_ibeta = (const float*)(P + t.snake_off) + TE;
-      if ((rc = launch_vconv(VE_LN | VE_SNAKE, f1, st))) return rc;
+      if ((rc = launch_vconv(VE_LN | VE_LNP | VE_SNAKE, f1, st))) return rc;
       VConvArgs f2 = vargs(t.ff2, w.ff, x);
       f2.resid = (const bf16*)x;
       // the chain's last block hands its consumers (convs reading x * mask) a masked copy in place
@@ -616,10 +630,11 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   // bf16 + vconv: every tensor a conv reads as x * mask is stored masked by its producer (the last
   // transformer block of a chain, the down/up convs), so mt_vconv needs no input prologue
   const bool mio = vconv && std::is_same<E, bf16>::value;
+  bool rs = false;  // the last resnet's output conv wrote the LayerNorm partials of its output
   auto tblocks = [&](int r, void* x, const float* m, int Tl) -> int {
     const int nb = (int)tbs[r].size();
     for (int j = 0; j < nb; ++j) {
-      int e = tblock<E>(P, w, tbs[r][j], x, m, mio && j == nb - 1, B, Tl, st);
+      int e = tblock<E>(P, w, tbs[r][j], x, m, mio && j == nb - 1, rs && j == 0, B, Tl, st);
       if (e) return e;
     }
     return 0;
@@ -642,19 +657,19 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
     return launch_conv<E, PF_MASK, 0>(a, st);
   };
   // down 0 @T
-  if ((rc = resnet<E>(P, w, res[0], w.xin, nullptr, c_cond, c_cond, false, w.H0, m0, B, T, tbp(0), st)))
+  if ((rc = resnet<E>(P, w, res[0], w.xin, nullptr, c_cond, c_cond, false, w.H0, m0, B, T, tbp(0), &rs, st)))
     return rc;
   if ((rc = tblocks(0, w.H0, m0, T))) return rc;
   if ((rc = plain(down0, w.H0, m0, m1, T, w.XA))) return rc;
   // down 1 @T/2
-  if ((rc = resnet<E>(P, w, res[1], w.XA, nullptr, C, C, mio, w.H1, m1, B, T1, tbp(1), st))) return rc;
+  if ((rc = resnet<E>(P, w, res[1], w.XA, nullptr, C, C, mio, w.H1, m1, B, T1, tbp(1), &rs, st))) return rc;
   if ((rc = tblocks(1, w.H1, m1, T1))) return rc;
   if ((rc = plain(down1, w.H1, m1, m1, T1, w.XB))) return rc;
   char* half[3] = {w.XA, w.XB, w.XC};
   int cur = 1;
   for (int i = 0; i < n_mid; ++i) {
     const int nx = (cur + 1) % 3;
-    if ((rc = resnet<E>(P, w, res[2 + i], half[cur], nullptr, C, C, mio, half[nx], m1, B, T1, tbp(2 + i), st)))
+    if ((rc = resnet<E>(P, w, res[2 + i], half[cur], nullptr, C, C, mio, half[nx], m1, B, T1, tbp(2 + i), &rs, st)))
       return rc;
     if ((rc = tblocks(2 + i, half[nx], m1, T1))) return rc;
     cur = nx;
@@ -663,7 +678,7 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   {
     const int nx = (cur + 1) % 3;
     const int r = 2 + n_mid;
-    if ((rc = resnet<E>(P, w, res[r], half[cur], w.H1, C, 2 * C, mio, half[nx], m1, B, T1, tbp(r), st)))
+    if ((rc = resnet<E>(P, w, res[r], half[cur], w.H1, C, 2 * C, mio, half[nx], m1, B, T1, tbp(r), &rs, st)))
       return rc;
     if ((rc = tblocks(r, half[nx], m1, T1))) return rc;
     if ((rc = plain(up0, half[nx], m1, m0, T1, w.U))) return rc;  // ConvTranspose1d k4 s2 p1 -> T
@@ -671,7 +686,7 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   // up 1 @T: cat(U, skip=H0)
   {
     const int r = 3 + n_mid;
-    if ((rc = resnet<E>(P, w, res[r], w.U, w.H0, C, 2 * C, mio, w.XF, m0, B, T, tbp(r), st))) return rc;
+    if ((rc = resnet<E>(P, w, res[r], w.U, w.H0, C, 2 * C, mio, w.XF, m0, B, T, tbp(r), &rs, st))) return rc;
     if ((rc = tblocks(r, w.XF, m0, T))) return rc;
     if ((rc = plain(up1, w.XF, m0, m0, T, w.U))) return rc;
   }

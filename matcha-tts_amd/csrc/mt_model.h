@@ -97,6 +97,7 @@ struct Decoder {
     float *zm, *m1, *emb, *h1, *h2, *tb, *lns;
     double *gn1, *gn2;
     float* apart;  // attention key-split slots
+    float* lnp;    // per frame, per 64-channel slab (sum, sum of squares): LayerNorm partials (vconv VE_ROWSTATS)
     const float* m0;
   };
   Work carve(void* ws, int B, int T, int S) const;
@@ -110,10 +111,12 @@ struct Decoder {
   int eval(const char* P, const Work& w, int B, int T, int ev, const Euler& eu, hipStream_t st) const;
   template <class E>
   int resnet(const char* P, const Work& w, const Res& R, const void* x0, const void* x1, int c0, int cin,
-             bool x_masked, void* out, const float* mask, int B, int Tl, const float* tb, hipStream_t st) const;
+             bool x_masked, void* out, const float* mask, int B, int Tl, const float* tb, bool* row_stats,
+             hipStream_t st) const;
+  // row_stats: w.lnp already holds the LayerNorm partials of x (written by the producing conv)
   template <class E>
-  int tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, bool mask_out, int B,
-             int Tl, hipStream_t st) const;
+  int tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, bool mask_out, bool row_stats,
+             int B, int Tl, hipStream_t st) const;
   bool vc(const GemmW& g) const { return vconv && g.vc; }
   VConvArgs vargs(const GemmW& g, const char* P, const Work& w, const void* x, int B, int Tl, void* y) const;
 

@@ -227,6 +227,39 @@ __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[jj][x][r] + bias[x][r];
+        if constexpr (std::is_same<E, bf16>::value) {
+          // 4 consecutive channels of one frame per lane: one 8-byte LDS access instead of four 2-byte ones
+          if (half == 0) {
+            uint32_t w[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const bf16 t0 = (bf16)v[2 * h], t1 = (bf16)v[2 * h + 1];
+              const bf16 a0 = (bf16)(inseq ? lrelu_f((float)t0, a.slope) : 0.f);
+              const bf16 a1 = (bf16)(inseq ? lrelu_f((float)t1, a.slope) : 0.f);
+              w[h] = (uint32_t)__builtin_bit_cast(uint16_t, a0) | ((uint32_t)__builtin_bit_cast(uint16_t, a1) << 16);
+            }
+            *reinterpret_cast<uint2*>(T + row * ROW + ch * 2) = make_uint2(w[0], w[1]);
+            continue;
+          }
+          const uint2 sr = *reinterpret_cast<const uint2*>(S + row * ROW + ch * 2);
+          v[0] += __uint_as_float(sr.x << 16);
+          v[1] += __uint_as_float(sr.x & 0xffff0000u);
+          v[2] += __uint_as_float(sr.y << 16);
+          v[3] += __uint_as_float(sr.y & 0xffff0000u);
+          if (!last) {
+            uint32_t ws_[2], wl_[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const bf16 s0 = (bf16)(inseq ? v[2 * h] : 0.f), s1 = (bf16)(inseq ? v[2 * h + 1] : 0.f);
+              const bf16 l0 = (bf16)lrelu_f((float)s0, a.slope), l1 = (bf16)lrelu_f((float)s1, a.slope);
+              ws_[h] = (uint32_t)__builtin_bit_cast(uint16_t, s0) | ((uint32_t)__builtin_bit_cast(uint16_t, s1) << 16);
+              wl_[h] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+            }
+            *reinterpret_cast<uint2*>(S + row * ROW + ch * 2) = make_uint2(ws_[0], ws_[1]);
+            *reinterpret_cast<uint2*>(SL + row * ROW + ch * 2) = make_uint2(wl_[0], wl_[1]);
+            continue;
+          }
+        } else {
         if (half == 0) {
           E* tp = reinterpret_cast<E*>(T + row * ROW) + ch;
 #pragma unroll
@@ -234,20 +267,25 @@ __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {
             const float tv = to_f(from_f<E>(v[r]));
             tp[r] = from_f<E>(inseq ? lrelu_f(tv, a.slope) : 0.f);
           }
-        } else {
-          const E* sp = reinterpret_cast<const E*>(S + row * ROW) + ch;
+          continue;
+        }
+        const E* sp = reinterpret_cast<const E*>(S + row * ROW) + ch;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = v[r] + to_f(sp[r]);
-          if (!last) {
-            E* sw = reinterpret_cast<E*>(S + row * ROW) + ch;
-            E* lw = reinterpret_cast<E*>(SL + row * ROW) + ch;
+        for (int r = 0; r < 4; ++r) v[r] = v[r] + to_f(sp[r]);
+        if (!last) {
+          E* sw = reinterpret_cast<E*>(S + row * ROW) + ch;
+          E* lw = reinterpret_cast<E*>(SL + row * ROW) + ch;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float sv = inseq ? to_f(from_f<E>(v[r])) : 0.f;
-              sw[r] = from_f<E>(sv);
-              lw[r] = from_f<E>(lrelu_f(sv, a.slope));
-            }
-          } else if (jj < OJ) {
+          for (int r = 0; r < 4; ++r) {
+            const float sv = inseq ? to_f(from_f<E>(v[r])) : 0.f;
+            sw[r] = from_f<E>(sv);
+            lw[r] = from_f<E>(lrelu_f(sv, a.slope));
+          }
+          continue;
+        }
+        }
+        {
+          if (jj < OJ) {
             // xs = rb_0; xs += rb_j (rounded to E after every add, as the per-layer path
             // stores xs); the last add is followed by / nk before rounding
 #pragma unroll

@@ -20,6 +20,9 @@ enum : int {
   VE_SNAKE = 64, // v + ibeta[m] * sin(v * alpha[m])^2 after the bias (SnakeBeta, model.py:580-609)
   VE_MASK = 128, // v * mask[frame] as the last step (a masked copy for consumers that read x * mask)
   VE_GNSTATS = 256,  // per-(utterance, 32-channel group) partial sum / sum of squares of v (fp64) -> gn_out
+  VE_ROWSTATS = 512, // per frame and 64-channel slab: (sum, sum of squares) of the stored values -> row_out
+                     // (the next LayerNorm's statistics, consumed with VE_LNP)
+  VE_LNP = 1024,     // with VE_LN: ln_stats holds VE_ROWSTATS partials [frames][cin/64] instead of (mean, rstd)
 };
 
 struct VConvArgs {
@@ -41,6 +44,8 @@ struct VConvArgs {
   const float* snake_ibeta;  // [M] 1 / (exp(beta) + 1e-9)
   const float* emask;        // [B*L] frame mask (VE_MASK)
   double* gn_out;            // [B][M/32][vconv_gn_parts(L, M)][2] (VE_GNSTATS)
+  float* row_out;            // [B*L][M/64][2] (VE_ROWSTATS)
+  float ln_eps;              // VE_LNP
   int probe;                 // launch-probe site of k >= 2 launches (0: PROBE_VCONV, < 0: none)
   // Output placement (all 0 = the plain [B][L][M] layout). ConvTranspose1d as a polyphase conv
   // (rows = phase x C_out) writes column n, row m to element n * ldy + m - yshift of its utterance,

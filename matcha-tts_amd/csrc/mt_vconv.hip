@@ -63,6 +63,9 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
 // waiting for fewer outstanding operations than allowed is always correct (only stricter), and a
 // three-level branch tree keeps the scalar cost per step small (a 64-way switch was ~40 SALU + branches)
 __device__ __forceinline__ void wait_vmcnt(int n) {
+#if defined(VCONV_EXP) && VCONV_EXP == 1  // timing experiment only: no DMA waits (wrong results)
+  return;
+#endif
   if (n < 7) {
     if (n < 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if (n < 4) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -78,6 +81,9 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 }
 
 __device__ __forceinline__ void raw_barrier() {
+#if defined(VCONV_EXP) && VCONV_EXP == 2  // timing experiment only: no step barrier (wrong results)
+  return;
+#endif
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -189,6 +195,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   // step, consumed after its MFMAs
   u32x4 rv[2][FN], yv[2][FN];
   float2 lns[FN];  // (mean, rstd) of each fragment column's frame (VE_LN)
+  f32x4 lnr[FN][2];  // VE_LNP: raw per-slab partials (s0, q0, s1, q1), (s2, q2, s3, q3)
   float mk[FN];    // frame mask of each fragment column (VE_MASK)
   auto epi_loads = [&](int ti) {
     int b, n0, m0;
@@ -202,8 +209,14 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
         const size_t o = (rowbase + n) * a.M + m0 + ch16 + fp * 32;
         if constexpr ((EF & VE_RESID) != 0) rv[fp][fn] = *reinterpret_cast<const u32x4*>(a.resid + o);
         if constexpr ((EF & VE_ACCUM) != 0) yv[fp][fn] = *reinterpret_cast<const u32x4*>(a.y + o);
-        if constexpr ((EF & VE_LN) != 0)
+        if constexpr ((EF & VE_LN) != 0 && (EF & VE_LNP) == 0)
           if (fp == 0) lns[fn] = *reinterpret_cast<const float2*>(a.ln_stats + 2 * (rowbase + n));
+        if constexpr ((EF & VE_LNP) != 0)
+          if (fp == 0) {  // the producer's 4 per-slab (sum, sum of squares) of this frame; merged after the MFMAs
+            const f32x4* pp = reinterpret_cast<const f32x4*>(a.ln_stats + 8 * (rowbase + n));
+            lnr[fn][0] = pp[0];
+            lnr[fn][1] = pp[1];
+          }
         if constexpr ((EF & VE_MASK) != 0)
           if (fp == 0) mk[fn] = a.emask[rowbase + n];
       }
@@ -219,6 +232,19 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
     double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};  // VE_GNSTATS: this lane's sums per 32-channel group
+    float rsum[FN], rsq[FN];                         // VE_ROWSTATS: this lane's 16 channels of frame fn
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) rsum[fn] = rsq[fn] = 0.f;
+    if constexpr ((EF & VE_LNP) != 0) {
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const float s = (lnr[fn][0][0] + lnr[fn][0][2]) + (lnr[fn][1][0] + lnr[fn][1][2]);
+        const float q = (lnr[fn][0][1] + lnr[fn][0][3]) + (lnr[fn][1][1] + lnr[fn][1][3]);
+        const float mean = s * (1.f / 256.f);
+        const float var = fmaxf(q * (1.f / 256.f) - mean * mean, 0.f);
+        lns[fn] = float2{mean, rsqrtf(var + a.ln_eps)};
+      }
+    }
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -270,6 +296,11 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
             }
             if constexpr ((EF & VE_MASK) != 0) v = v * mk[fn];
             const bf16 rb = (bf16)v;
+            if constexpr ((EF & VE_ROWSTATS) != 0) {
+              const float fr = (float)rb;
+              rsum[fn] += fr;
+              rsq[fn] += fr * fr;
+            }
             const bf16 av = (bf16)lrelu_f((float)rb, a.slope);
             ob[r] = (EF & VE_ACT) ? av : rb;
             ab[r] = av;
@@ -292,6 +323,21 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
           *reinterpret_cast<u32x4*>(ok ? a.y2 + o : a.trash + 8 * lane) = u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]};
         }
       }
+    if constexpr ((EF & VE_ROWSTATS) != 0) {
+      // lanes l16 + 16*g4 hold the wave's 64-channel slab of one frame: reduce over g4, lanes 0-15 store
+      const int ns = a.M >> 6, slab = (m0 >> 6) + wm;
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        float s = rsum[fn], q = rsq[fn];
+        s += __shfl_xor(s, 16, 64);
+        q += __shfl_xor(q, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        q += __shfl_xor(q, 32, 64);
+        const int n = n0 + wn * WNC + fn * 16 + l16;
+        if (g4 == 0 && n < L)
+          *reinterpret_cast<float2*>(a.row_out + 2 * (((size_t)b * L + n) * ns + slab)) = float2{s, q};
+      }
+    }
     if constexpr ((EF & VE_GNSTATS) != 0) {
       // fm pair fp covers channels m0 + wm*64 + 32*fp .. +31: one GroupNorm(8) group of the 256 channels
       const int nparts = ntn * TT::WAVES_N, part = (n0 / BN) * TT::WAVES_N + wn;
@@ -441,6 +487,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       }
     }
   }
+#if defined(VCONV_EXP)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -525,6 +574,9 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(!(ef & VE_RESID) || a0.resid, "vconv: resid");
   MT_REQUIRE(!(ef & VE_DUAL) || a0.y2, "vconv: y2");
   MT_REQUIRE(!(ef & VE_LN) || (a0.ln_stats && a0.wsum), "vconv: LN stats / weight sums");
+  MT_REQUIRE(!(ef & VE_LNP) || ((ef & VE_LN) && a0.ln_eps > 0.f && a0.cin == 256),
+             "vconv: LN partials need VE_LN, eps and 256 input channels (4 slabs)");
+  MT_REQUIRE(!(ef & VE_ROWSTATS) || a0.row_out, "vconv: row statistics output");
   MT_REQUIRE(!(ef & VE_SNAKE) || (a0.snake_alpha && a0.snake_ibeta), "vconv: snake params");
   MT_REQUIRE(!(ef & VE_MASK) || a0.emask, "vconv: mask");
   MT_REQUIRE(!(ef & VE_GNSTATS) || (a0.gn_out && a0.taps > 1 && a0.M % 32 == 0), "vconv: GN statistics");
@@ -600,6 +652,9 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE1(VE_LN | VE_SNAKE)
       MT_VCASE1(VE_RESID)
       MT_VCASE1(VE_RESID | VE_MASK)
+      MT_VCASE1(VE_RESID | VE_ROWSTATS)
+      MT_VCASE1(VE_LN | VE_LNP)
+      MT_VCASE1(VE_LN | VE_LNP | VE_SNAKE)
       MT_VCASE1(0)
       default: set_error("vconv: 1x1 epilogue %d not compiled in", ef); return -1;
     }
