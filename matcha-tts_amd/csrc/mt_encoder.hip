@@ -132,9 +132,21 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const E* __restrict__ qkv
     }
   }
   const float mq = tq < Tx ? xmask[(size_t)b * Tx + tq] : 0.f;
+  // A tile of padded queries only: their rows are zeroed downstream (the FFN and LayerNorm outputs are
+  // masked) and never read unmasked, so they are written as 0.
+  if (!__syncthreads_or(mq != 0.f)) {
+    if (tq < Tx) {
+      E* dst = out + ((size_t)b * Tx + tq) * W + h * DK + p * DP;
+#pragma unroll
+      for (int i = 0; i < DP; ++i) dst[i] = from_f<E>(0.f);
+    }
+    return;
+  }
   float mrun = -INFINITY, lrun = 0.f;
   for (int k0 = 0; k0 < Tx; k0 += 64) {
-    __syncthreads();
+    // a tile of padded keys only adds exp(-1e4 - m) == 0 for every valid query: skipped (exact)
+    const bool kval = tid < 64 && k0 + tid < Tx && xmask[(size_t)b * Tx + k0 + tid] != 0.f;
+    if (!__syncthreads_or(kval)) continue;
     for (int e = tid; e < 64 * DK; e += 256) {
       const int r = e / DK, d = e - r * DK;
       const int t = k0 + r;

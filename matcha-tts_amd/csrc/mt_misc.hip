@@ -468,6 +468,25 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ 
   __shared__ float ga[256], gs[256], gm[8], gr[8];
   const int b = blockIdx.y, tid = threadIdx.x;
   const int G = C >> 5;
+  const int cpr = C >> 3;  // 16-byte groups per row
+  const int rows_per = 256 / cpr;
+  const int q = tid % cpr, c = 8 * q;
+  // this thread's rows are loaded first (independent of the GroupNorm coefficients), so their latency
+  // overlaps the partial-sum merge below
+  constexpr int NR = GN_FR / 8;  // rows per thread at C = 256 (fewer used at smaller C)
+  u32x4 v[NR];
+  float mk[NR];
+  const int t0 = blockIdx.x * GN_FR + tid / cpr;
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int t = min(t0 + j * rows_per, T - 1);
+    const size_t row = (size_t)b * T + t;
+    v[j] = *reinterpret_cast<const u32x4*>(y + row * C + c);
+    mk[j] = mask[row];
+  }
+  float tbv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) tbv[k] = tb ? tb[c + k] : 0.f;
   if (tid < G) {  // same merge order and formulas as the conv kernel's PF_GN pre-phase (mt_conv.hip)
     const double* p = part + (size_t)(b * G + tid) * nparts * 2;
     double s1 = 0.0, s2 = 0.0;
@@ -483,30 +502,12 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ 
     gr[tid] = (float)(1.0 / sqrt(var + (double)eps));
   }
   __syncthreads();
-  for (int c = tid; c < C; c += 256) {
-    const float sc = gr[c >> 5] * gamma[c];
-    ga[c] = sc;
-    gs[c] = -sc * gm[c >> 5] + beta[c];
+  for (int cc = tid; cc < C; cc += 256) {
+    const float sc = gr[cc >> 5] * gamma[cc];
+    ga[cc] = sc;
+    gs[cc] = -sc * gm[cc >> 5] + beta[cc];
   }
   __syncthreads();
-  const int cpr = C >> 3;  // 16-byte groups per row
-  const int rows_per = 256 / cpr;
-  const int q = tid % cpr, c = 8 * q;
-  float tbv[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) tbv[k] = tb ? tb[c + k] : 0.f;
-  // all of this thread's rows loaded before any math: GN_FR / rows_per 16-byte loads in flight
-  constexpr int NR = GN_FR / 8;  // rows per thread at C = 256 (fewer used at smaller C)
-  u32x4 v[NR];
-  float mk[NR];
-  const int t0 = blockIdx.x * GN_FR + tid / cpr;
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const int t = min(t0 + j * rows_per, T - 1);
-    const size_t row = (size_t)b * T + t;
-    v[j] = *reinterpret_cast<const u32x4*>(y + row * C + c);
-    mk[j] = mask[row];
-  }
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int t = t0 + j * rows_per;
