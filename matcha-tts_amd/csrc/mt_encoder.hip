@@ -147,17 +147,22 @@ __global__ __launch_bounds__(256) void enc_attn_kernel(const E* __restrict__ qkv
     // a tile of padded keys only adds exp(-1e4 - m) == 0 for every valid query: skipped (exact)
     const bool kval = tid < 64 && k0 + tid < Tx && xmask[(size_t)b * Tx + k0 + tid] != 0.f;
     if (!__syncthreads_or(kval)) continue;
-    for (int e = tid; e < 64 * DK; e += 256) {
-      const int r = e / DK, d = e - r * DK;
+    // 16-byte loads of K and V rows, widened to fp32 in LDS
+    constexpr int VN = Vec16<E>::N, VPR = DK / VN;
+    for (int e = tid; e < 64 * VPR; e += 256) {
+      const int r = e / VPR, c = e - r * VPR;
       const int t = k0 + r;
-      float kv = 0.f, vv = 0.f;
+      Vec16<E> kv = zero16<E>(), vv = zero16<E>();
       if (t < Tx) {
-        const E* src = base + (size_t)t * ld + d;
-        kv = to_f(src[W]);
-        vv = to_f(src[2 * W]);
+        const E* src = base + (size_t)t * ld + c * VN;
+        kv = load16(src + W);
+        vv = load16(src + 2 * W);
       }
-      Ks[r * KS + d] = kv;
-      Vs[r * KS + d] = vv;
+#pragma unroll
+      for (int i = 0; i < VN; i += 4) {
+        *reinterpret_cast<f32x4*>(Ks + r * KS + c * VN + i) = f32x4{kv.get(i), kv.get(i + 1), kv.get(i + 2), kv.get(i + 3)};
+        *reinterpret_cast<f32x4*>(Vs + r * KS + c * VN + i) = f32x4{vv.get(i), vv.get(i + 1), vv.get(i + 2), vv.get(i + 3)};
+      }
     }
     if (tid < 64) km[tid] = k0 + tid < Tx ? xmask[(size_t)b * Tx + k0 + tid] : 0.f;
     __syncthreads();

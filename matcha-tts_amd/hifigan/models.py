@@ -106,6 +106,7 @@ class Generator(nn.Module):
                 m.weight_v.normal_(0.0, 0.01)
         self.precision = precision
         self._engines = {}
+        self._pk = rt.PackCache()
 
     # ---- HIP plumbing ----
     def set_precision(self, precision: str):
@@ -127,8 +128,12 @@ class Generator(nn.Module):
         return out
 
     def packed(self, device):
-        src = list(self.state_dict(keep_vars=True).values())
-        return self.engine().pack(self.folded_state, src, device)
+        key = (self.precision, str(device))
+        packed = self._pk.get(key)
+        if packed is None:
+            src = list(self.state_dict(keep_vars=True).values())
+            packed = self._pk.put(key, src, self.engine().pack(self.folded_state, src, device))
+        return packed
 
     def forward(self, x):
         rt.require_gpu(x, what="Generator.forward")

@@ -72,6 +72,58 @@ def _param_list(h, num_fn, name_fn, shape_fn) -> List[Tuple[str, Tuple[int, ...]
     return out
 
 
+# Every parameter / buffer / submodule (re)registration anywhere bumps this counter (torch's global
+# module registration hooks), so PackCache reuses a packed buffer only while no registration happened
+# and the module's state tensors are the same tensors at the same addresses and version counters.
+_REG = [0]
+
+
+def _bump_registration(*_args):
+    _REG[0] += 1
+
+
+for _hook in (torch.nn.modules.module.register_module_parameter_registration_hook,
+              torch.nn.modules.module.register_module_buffer_registration_hook,
+              torch.nn.modules.module.register_module_module_registration_hook):
+    _hook(_bump_registration)
+
+
+class PackCache:
+    """Per-module cache of packed weight buffers, keyed by (precision, device).
+
+    A hit costs one pass over the module's state tensors (address + version counter); a miss (first call,
+    in-place weight update, `param.data = ...`, a registration such as remove_weight_norm, .to()) makes
+    the caller rebuild state_dict() and repack. `trust_next` lets one internal call sequence (synthesize)
+    validate early, while the GPU is still busy, and skip the check at the point of use."""
+
+    def __init__(self):
+        self.entries = {}
+        self.trusted = set()
+
+    def get(self, key):
+        e = self.entries.get(key)
+        if e is None:
+            return None
+        if key in self.trusted:
+            self.trusted.discard(key)
+            return e[3]
+        reg, tensors, state, packed = e
+        if reg != _REG[0] or [(t.data_ptr(), t._version) for t in tensors] != state:
+            return None
+        return packed
+
+    def put(self, key, tensors, packed):
+        self.entries[key] = (_REG[0], tensors, [(t.data_ptr(), t._version) for t in tensors], packed)
+        return packed
+
+    def trust_next(self, key):
+        if key in self.entries:
+            self.trusted.add(key)
+
+    def untrust(self):
+        self.trusted.clear()
+
+
 def fingerprint(tensors: List[torch.Tensor]) -> Tuple:
     return tuple((t.data_ptr(), t._version, tuple(t.shape), str(t.device)) for t in tensors)
 

@@ -232,6 +232,7 @@ class TextEncoder(nn.Module):
         super().__init__()
         self.precision = precision
         self._engines = {}
+        self._pk = rt.PackCache()
         self.encoder_type = encoder_type
         self.n_vocab = n_vocab
         self.n_feats = _get(encoder_params, "n_feats")
@@ -275,7 +276,11 @@ class TextEncoder(nn.Module):
         if self.n_spks > 1 and spks is None:
             raise ValueError("multi-speaker TextEncoder needs spks [B, spk_emb_dim]")
         eng = self.engine()
-        packed = eng.pack({k: v for k, v in self.state_dict(keep_vars=True).items()}, x.device)
+        key = (self.precision, str(x.device))
+        packed = self._pk.get(key)
+        if packed is None:
+            sd = self.state_dict(keep_vars=True)
+            packed = self._pk.put(key, list(sd.values()), eng.pack(dict(sd), x.device))
         return eng.forward(packed, x, x_lengths, rt.f32c(spks))
 
 
@@ -427,6 +432,7 @@ class Decoder(nn.Module):
         self.final_proj = nn.Conv1d(256, out_channels, 1)
         self.precision = precision
         self._engines = {}
+        self._pk = rt.PackCache()
 
     # ---- HIP plumbing ----
     def set_precision(self, precision: str):
@@ -442,8 +448,12 @@ class Decoder(nn.Module):
         return self._engines[key]
 
     def packed(self, device):
-        sd = {k: v for k, v in self.state_dict(keep_vars=True).items()}
-        return self.engine().pack(sd, device)
+        key = (self.precision, str(device))
+        packed = self._pk.get(key)
+        if packed is None:
+            sd = self.state_dict(keep_vars=True)
+            packed = self._pk.put(key, list(sd.values()), self.engine().pack(dict(sd), device))
+        return packed
 
     def forward(self, x, mask, mu, t, spks=None, cond=None):
         """model.py:964-1048 — x, mu [B,80,T], mask [B,1,T], t [B] (or scalar) -> [B,80,T]."""
@@ -536,10 +546,18 @@ class MatchaTTS(nn.Module):
         rt.require_gpu(x, x_lengths, spks, what="MatchaTTS.synthesize")
         mu, logw, x_mask = self.encoder(x, x_lengths, spks)
         w_ceil, cum, y_lengths = rt.durations(logw, x_mask, length_scale)
-        y_max = int(y_lengths.max())                 # the reference's host sync (model.py:1278-1281)
-        t_pad = fix_len_compatibility(y_max)
-        attn, mu_y, y_mask = rt.alignment(cum, y_lengths, t_pad, mu)
-        z = self.decoder(mu_y, y_mask, n_timesteps, temperature, spks, cond=None)
+        # validate the estimator's packed weights now, while the GPU runs the encoder, instead of after the
+        # host sync below (nothing between here and the solve can change them)
+        est = self.decoder.estimator
+        est.packed(x.device)
+        est._pk.trust_next((est.precision, str(x.device)))
+        try:
+            y_max = int(y_lengths.max())                 # the reference's host sync (model.py:1278-1281)
+            t_pad = fix_len_compatibility(y_max)
+            attn, mu_y, y_mask = rt.alignment(cum, y_lengths, t_pad, mu)
+            z = self.decoder(mu_y, y_mask, n_timesteps, temperature, spks, cond=None)
+        finally:
+            est._pk.untrust()
         mel = rt.denorm_crop(z, self.mel_mean, self.mel_std, y_max)
         return mel, y_lengths, attn
 

@@ -170,6 +170,23 @@ def test_vconv_stages_match_generic_per_layer(T):
     eng.set_vconv(2)
 
 
+def test_packed_weights_follow_weight_updates():
+    """The cached packed buffer follows in-place updates and parameter re-registration (PackCache)."""
+    from torch import nn
+    g, gen = _gen("bf16", True)
+    mel = t(g["mel"], DEV)
+    a = gen(mel)
+    with torch.no_grad():
+        gen.conv_post.weight.mul_(2.0)
+    b = gen(mel)
+    assert not torch.equal(a, b)
+    with torch.no_grad():
+        gen.conv_post.weight.div_(2.0)   # exact inverse in fp32
+    assert torch.equal(gen(mel), a)
+    gen.conv_post.weight = nn.Parameter(gen.conv_post.weight.detach() * 2.0)
+    assert torch.equal(gen(mel), b)
+
+
 def test_denoiser_fp32():
     from hifigan.denoiser import Denoiser
     from oracle import matcha_oracle as O
