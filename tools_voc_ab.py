@@ -13,6 +13,10 @@ from hifigan.config import v1  # noqa: E402
 from hifigan.env import AttrDict  # noqa: E402
 from hifigan.models import Generator  # noqa: E402
 from matcha_hip import synthetic  # noqa: E402
+if os.environ.get("MT_LIB"):  # timing experiments: another build of the library
+    import matcha_hip._lib as _L  # noqa: E402
+    _L.LIB_PATH = os.environ["MT_LIB"]
+MODES = tuple(int(c) for c in os.environ.get("MODES", "210"))
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 728
@@ -24,7 +28,6 @@ g = g.cuda().eval()
 g.remove_weight_norm()
 mel = (torch.randn(B, 80, T) * 2 - 5).cuda()
 eng = g.engine()
-MODES = (2, 1, 0)
 res = {m: [] for m in MODES}
 for r in range(R + 1):
     for on in MODES:
