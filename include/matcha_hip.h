@@ -13,6 +13,7 @@
  *   mt_denorm_crop               <- denormalize + crop  model.py:106-125, 1295-1298
  *   mt_vocoder_forward           <- hifigan.models.Generator.forward  hifigan/models.py:181-197
  *   mt_denoise                   <- hifigan.denoiser.Denoiser.forward hifigan/denoiser.py:62-68
+ *   mt_maximum_path              <- train_standalone.maximum_path train_standalone.py:280-325 (MAS)
  *
  * Conventions
  *  - Every pointer argument is DEVICE memory owned by the caller (PyTorch), except the
@@ -160,6 +161,17 @@ int mt_denoise(const float* audio, int B, int L, const float* bias_spec, float s
                void* ws, size_t ws_bytes, void* stream);
 /* |STFT| (same framing) of every frame: mag [B][1+L/256][513] (bias spectrum, denoiser.py:57-60) */
 int mt_stft_magnitude(const float* audio, int B, int L, float* mag, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Training-side (§8f rank 3): Monotonic Alignment Search, replacing train_standalone.py:280-325
+ * `maximum_path(neg_cent, mask)` (a device->host copy + CPU numba/Python DP in the reference) with
+ * its exact recurrence as a GPU anti-diagonal wavefront. neg_cent [B][Tx][Ty] fp32, t_xs / t_ys [B]
+ * int32 (the mask's token / frame counts) -> paths [B][Tx][Ty] fp32 one-hot per frame column inside
+ * [0,t_x) x [0,t_y), zero elsewhere. Tx <= 1024.
+ * ------------------------------------------------------------------------------------- */
+size_t mt_maximum_path_workspace_bytes(int B, int Tx, int Ty);
+int mt_maximum_path(const float* neg_cent, const int32_t* t_xs, const int32_t* t_ys, int B, int Tx, int Ty,
+                    float* paths, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Op-level entry points (per-kernel parity tests)

@@ -222,6 +222,13 @@ int mt_denoise(const float* audio, int B, int L, const float* bias_spec, float s
   return mt::denoise(audio, B, L, bias_spec, strength, out, ws, ws_bytes, (hipStream_t)stream);
 }
 
+size_t mt_maximum_path_workspace_bytes(int B, int Tx, int Ty) { return mt::mas_workspace_bytes(B, Tx, Ty); }
+int mt_maximum_path(const float* neg_cent, const int32_t* t_xs, const int32_t* t_ys, int B, int Tx, int Ty,
+                    float* paths, void* ws, size_t ws_bytes, void* stream) {
+  MT_REQUIRE(neg_cent && t_xs && t_ys && paths, "maximum_path: null argument");
+  return mt::maximum_path(neg_cent, t_xs, t_ys, B, Tx, Ty, paths, ws, ws_bytes, (hipStream_t)stream);
+}
+
 int mt_stft_magnitude(const float* audio, int B, int L, float* mag, void* stream) {
   MT_REQUIRE(audio && mag, "stft_magnitude: null argument");
   return mt::stft_magnitude(audio, B, L, mag, (hipStream_t)stream);

@@ -45,6 +45,11 @@ int denorm_crop(const float* z, const float* mean, const float* stdv, int B, int
 
 // part (optional): key-split slots (attention_part_bytes, sized for the largest T launched on it);
 // with it an unpadded utterance's keys are split over several workgroups + a merge launch
+// Monotonic Alignment Search (mt_mas.hip, train_standalone.py:280-325)
+size_t mas_workspace_bytes(int B, int Tx, int Ty);
+int maximum_path(const float* value, const int* t_xs, const int* t_ys, int B, int Tx, int Ty, float* out,
+                 void* ws, size_t ws_bytes, hipStream_t st);
+
 int launch_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                      hipStream_t stream, float* part = nullptr);
 size_t attention_part_bytes(int B, int T, int heads);

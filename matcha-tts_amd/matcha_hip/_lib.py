@@ -63,6 +63,8 @@ SIGNATURES = {
     "mt_denorm_crop": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P]),
     "mt_denoise_workspace_bytes": (c_size_t, [c_int, c_int]),
     "mt_denoise": (c_int, [P, c_int, c_int, P, c_float, P, P, c_size_t, P]),
+    "mt_maximum_path_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mt_maximum_path": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_size_t, P]),
     "mt_stft_magnitude": (c_int, [P, c_int, c_int, P, P]),
     "mt_op_conv1d_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "mt_op_conv1d": (c_int, [c_int, P, c_int, c_int, c_int, P, P, c_int, c_int, c_int, c_int, c_int,

@@ -415,6 +415,23 @@ def denoise(audio: torch.Tensor, bias_spec: torch.Tensor, strength: float) -> to
     return out
 
 
+def maximum_path(neg_cent: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """train_standalone.py:280-325 on the GPU: neg_cent [B,Tx,Ty], attention mask [B,Tx,Ty] (x_mask x
+    y_mask) -> one-hot monotonic path [B,Tx,Ty] in neg_cent's dtype. The lengths are the mask's row /
+    column counts at index 0, as the reference takes them."""
+    require_gpu(neg_cent, mask, what="maximum_path")
+    B, Tx, Ty = neg_cent.shape
+    value = f32c(neg_cent.detach())
+    t_xs = mask.detach().sum(dim=1)[:, 0].to(torch.int32).contiguous()
+    t_ys = mask.detach().sum(dim=2)[:, 0].to(torch.int32).contiguous()
+    out = torch.empty((B, Tx, Ty), dtype=torch.float32, device=neg_cent.device)
+    L_ = lib()
+    ws = _Workspace.get(L_.mt_maximum_path_workspace_bytes(B, Tx, Ty), neg_cent.device)
+    check(L_.mt_maximum_path(ptr(value), ptr(t_xs), ptr(t_ys), B, Tx, Ty, ptr(out), ws.data_ptr(), ws.numel(),
+                             stream_handle(neg_cent.device)), "maximum_path")
+    return out.to(neg_cent.dtype)
+
+
 def op_conv1d(x_btc: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor], stride=1, pad=0, dil=1,
               transposed=False, slope: Optional[float] = None, precision="fp32", variant: int = -1,
               out: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -464,3 +464,38 @@ def denoise(audio: Tensor, bias_spec: Tensor, strength: float = 0.0005,
     w = torch.hann_window(win, dtype=audio.dtype)
     return torch.istft(torch.complex(mag * torch.cos(ang), mag * torch.sin(ang)),
                        n_fft=n_fft, hop_length=hop, win_length=win, window=w)
+
+
+# ---------------------------------------------------------------------------------------------------
+# Training side (§8f rank 3): Monotonic Alignment Search, train_standalone.py:280-325 (its pure-Python
+# branch, the reference's recurrence with the same-column predecessor path[x-1, y]; float32 numpy
+# scalars as the reference runs it). Pinned by tests/golden/g7_mas.npz (make_golden_mas.py ran the
+# reference function itself).
+# ---------------------------------------------------------------------------------------------------
+def maximum_path(neg_cent: Tensor, mask: Tensor) -> Tensor:
+    import numpy as np
+    value = neg_cent.detach().cpu().numpy().astype(np.float32)
+    m = mask.detach().cpu().numpy()
+    b, tx_max, ty_max = value.shape
+    t_xs = m.sum(axis=1)[:, 0].astype(np.int32)  # train_standalone.py:291-292
+    t_ys = m.sum(axis=2)[:, 0].astype(np.int32)
+    paths = np.zeros((b, tx_max, ty_max), dtype=np.float32)
+    for i in range(b):
+        tx, ty = int(t_xs[i]), int(t_ys[i])
+        p = np.zeros((tx, ty), dtype=np.float32)  # DP table; unvisited cells stay 0
+        v = value[i, :tx, :ty]
+        for y in range(ty):  # :306-318
+            for x in range(max(0, tx + y - ty), min(tx, y + 1)):
+                if x == 0:
+                    vp = np.float32(0.0) if y == 0 else p[0, y - 1]
+                elif y == 0:
+                    vp = p[x - 1, 0]
+                else:
+                    vp = max(p[x - 1, y], p[x, y - 1])
+                p[x, y] = vp + v[x, y]
+        index = tx - 1  # backtrack :320-325 (the y = 0 comparison reads a rewritten column: no effect)
+        for y in range(ty - 1, -1, -1):
+            paths[i, index, y] = 1.0
+            if y > 0 and index > 0 and p[index - 1, y - 1] > p[index, y - 1]:
+                index -= 1
+    return torch.from_numpy(paths)
