@@ -211,7 +211,9 @@ __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {
 #pragma unroll
         for (int x = 0; x < FMJ; ++x) Acur[t][x] = Anext[t][x];
     }
-    __syncthreads();  // every wave is done reading src before S / T are rewritten
+    // No barrier here: this conv's epilogue writes T (conv1) or S / SL (conv2), none of which its own MFMA
+    // phase reads (src is SL for conv1, T for conv2); the writes only race with the NEXT conv's reads,
+    // which the barrier after the epilogue orders.
 
     // ---- epilogue ----
 #pragma unroll
