@@ -45,10 +45,12 @@ struct VT {
   static constexpr int WSLOT = BM * 128;          // BM rows x 64 bf16 channels
   static constexpr int NWW = BM / 64;             // W wave-instructions per wave per step
   static constexpr int NWSLOT = K1_ ? 3 : 4;      // weight ring (NWSLOT - 1 steps in flight)
-  static constexpr int XROWS = K1_ ? TBN : 320;   // >= BN + (taps - 1) * dil
+  static constexpr int XROWS = K1_ ? TBN : TBN + 64;  // >= BN + (taps - 1) * dil (halo <= 64 rows)
   static constexpr int XBUF = XROWS * 128;
   static constexpr int NXW = XROWS / 64;          // X wave-instructions per wave per chunk
-  static constexpr int NXB = (K1_ || BM == 64) ? 3 : 2;  // row buffers: chunks staged NXB-1 ahead
+  // row buffers: chunks staged NXB-1 ahead (the 64-row tiles with 256 frames have one chunk per tile
+  // and stage two tiles ahead; with 384 frames the buffers only fit twice)
+  static constexpr int NXB = K1_ ? 3 : (BM == 64 && TBN <= 256) ? 3 : 2;
   static constexpr int PAR_OFF = NWSLOT * WSLOT + NXB * XBUF;  // per-channel tables: bias, wsum, alpha, ibeta
   static constexpr int LDS_BYTES = PAR_OFF + NPAR_ * MMAX * 4;
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -605,8 +607,15 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   long ntiles = (long)a.B * ((a.Lout + BN - 1) / BN) * (a.Mpad / BM);
   // 1x1 GEMMs whose 256-frame tiles would leave CUs idle (the decoder's half-resolution blocks):
   // 128-frame tiles double the parallelism
-  const bool small = k1 && ntiles < (long)cu_count();
+#ifndef VCONV_SMALL_MULT
+#define VCONV_SMALL_MULT 1
+#endif
+  const bool small = k1 && ntiles < (long)VCONV_SMALL_MULT * cu_count();
   if (small) ntiles = (long)((a.L + 127) / 128) * (a.Mpad / BM);
+  // k >= 2 convs with 64-row tiles take 384 frames per tile: 1.5x the MFMAs per step barrier
+  constexpr int BN64 = 384;
+  if (!k1 && BM == 64) ntiles = (long)a.B * ((a.Lout + BN64 - 1) / BN64) * (a.Mpad / BM);
+  MT_REQUIRE(!(ef & VE_GNSTATS) || BM == 128, "vconv: GroupNorm partials need 128-row tiles");
   const int G = (int)std::min<long>(ntiles, cu_count());
   const double flops = 2.0 * a.M * a.cin * a.taps * (double)a.B * a.Lout;
   const int touts = 1 + ((ef & VE_RESID) ? 1 : 0) + ((ef & VE_ACCUM) ? 1 : 0) + ((ef & VE_DUAL) ? 1 : 0);
@@ -618,7 +627,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
 #define MT_VCASE(E)                                                                                \
   case E:                                                                                          \
     if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false>), dim3(G), dim3(NT), 0, st, a); \
-    else hipLaunchKernelGGL((vconv_kernel<E, 64, false>), dim3(G), dim3(NT), 0, st, a);           \
+    else hipLaunchKernelGGL((vconv_kernel<E, 64, false, BN64>), dim3(G), dim3(NT), 0, st, a);     \
     break;
 #define MT_VCASE1(E)                                                                                    \
   case E:                                                                                               \

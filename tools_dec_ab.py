@@ -13,6 +13,9 @@ import torch  # noqa: E402
 
 from conftest import make_decoder  # noqa: E402
 from matcha_hip import synthetic  # noqa: E402
+if os.environ.get("MT_LIB"):  # timing experiments: another build of the library
+    import matcha_hip._lib as _L  # noqa: E402
+    _L.LIB_PATH = os.environ["MT_LIB"]
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 728
