@@ -106,6 +106,12 @@ size_t mt_decoder_step_workspace_bytes(const mt_decoder* d, int B, int T);
 int mt_decoder_step(const mt_decoder* d, const void* packed, const float* x, const float* mu_y,
                     const float* mask, const float* spks, float t, int B, int T, float* out, void* ws,
                     size_t ws_bytes, void* stream);
+/* the same with one time per utterance, t [B] fp32 in device memory (Decoder.forward with a [B] t as
+ * CFM.compute_loss calls it, model.py:1147-1162) */
+size_t mt_decoder_step_times_workspace_bytes(const mt_decoder* d, int B, int T);
+int mt_decoder_step_times(const mt_decoder* d, const void* packed, const float* x, const float* mu_y,
+                          const float* mask, const float* spks, const float* t, int B, int T, float* out,
+                          void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * HiFi-GAN Generator (hifigan/models.py:148-206). Parameters are the folded weights

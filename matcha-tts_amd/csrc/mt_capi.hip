@@ -140,6 +140,16 @@ int mt_decoder_step(const mt_decoder* d, const void* packed, const float* x, con
   return d->d.step(packed, x, mu_y, mask, spks, t, B, T, out, ws, ws_bytes, (hipStream_t)stream);
 }
 
+size_t mt_decoder_step_times_workspace_bytes(const mt_decoder* d, int B, int T) {
+  return d ? d->d.workspace_bytes(B, T, B) : 0;
+}
+int mt_decoder_step_times(const mt_decoder* d, const void* packed, const float* x, const float* mu_y,
+                          const float* mask, const float* spks, const float* t, int B, int T, float* out, void* ws,
+                          size_t ws_bytes, void* stream) {
+  MT_REQUIRE(d && packed && x && mu_y && mask && t && out && ws, "decoder_step_times: null argument");
+  return d->d.step_times(packed, x, mu_y, mask, spks, t, B, T, out, ws, ws_bytes, (hipStream_t)stream);
+}
+
 // ---- vocoder ----
 int mt_vocoder_create(int resblock, int n_ups, const int* up_rates, const int* up_kernels, int up_init,
                       int n_kernels, const int* rb_kernels, int n_dils, const int* rb_dils, int dtype,

@@ -63,7 +63,8 @@ struct ConvArgs {
   const float* gn_g;
   const float* gn_b;
   float gn_eps;
-  const float* tb;      // [cin]
+  const float* tb;      // [cin] (+ b * tb_ld for utterance b)
+  int tb_ld;            // 0: one time bias for the batch
   // epilogue params
   const float* emask;   // [B][Tout]
   const void* resid;

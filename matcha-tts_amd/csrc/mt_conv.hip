@@ -83,7 +83,7 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
   float* tbs = lnr + BN;                                           // [256] time-embedding bias
 
   if constexpr ((PF & PF_TB) != 0) {
-    for (int c = tid; c < a.cin; c += NT) tbs[c] = a.tb[c];
+    for (int c = tid; c < a.cin; c += NT) tbs[c] = a.tb[(size_t)b * a.tb_ld + c];
     __syncthreads();
   }
 

@@ -421,15 +421,17 @@ Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
   w.h2 = (float*)take((size_t)S * TE * 4);
   w.tb = (float*)take((size_t)S * n_res * C * 4);
   w.trash = take(4096);
+  w.tb_ld = 0;
   w.apart = (float*)take(attention_part_bytes(B, T, heads));
   w.lnp = (float*)take(BT * (C / 64) * 2 * 4);
   w.m0 = nullptr;
   return w;
 }
 
-int Decoder::time_embed(const char* P, const Work& w, const TimeSched& ts, int S, hipStream_t st) const {
+int Decoder::time_embed(const char* P, const Work& w, const TimeSched& ts, int S, hipStream_t st,
+                        const float* t_dev) const {
   int rc;
-  if ((rc = sinus_embed(ts, S, (const float*)(P + freq_off), c_cond / 2, w.emb, st))) return rc;
+  if ((rc = sinus_embed(ts, S, (const float*)(P + freq_off), c_cond / 2, w.emb, st, t_dev))) return rc;
   if ((rc = rowdot(w.emb, c_cond, (const float*)(P + t1w_off), (const float*)(P + t1b_off), w.h1, TE, 0, S,
                    TE, c_cond, 0, 1, st)))
     return rc;
@@ -504,7 +506,7 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
   // block 2 -> y2 + gn2 (generic) or y1 + gn2 (vconv, its input h1 in y2)
   const void* yb2 = w.y2;
   if (vc(R.c2)) {
-    if ((rc = gn_apply(w.y1, B, Tl, C, w.gn1, nt1, g1, g1 + C, 1e-5f, tb, mask, w.y2, st))) return rc;
+    if ((rc = gn_apply(w.y1, B, Tl, C, w.gn1, nt1, g1, g1 + C, 1e-5f, tb, w.tb_ld, mask, w.y2, st))) return rc;
     VConvArgs b = vargs(R.c2, P, w, w.y2, B, Tl, w.y1);
     b.gn_out = w.gn2;
     if ((rc = launch_vconv(VE_GNSTATS, b, st))) return rc;
@@ -521,12 +523,13 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
     b.gn_g = g1;
     b.gn_b = g1 + C;
     b.tb = tb;
+    b.tb_ld = w.tb_ld;
     b.gn_out = w.gn2;
     if ((rc = launch_conv<E, PF_GN | PF_TB | PF_MASK, EF_GNSTATS>(b, st, &nt2))) return rc;
   }
   // residual 1x1 + block output
   if (x_masked && vc(R.res)) {
-    if ((rc = gn_apply(yb2, B, Tl, C, w.gn2, nt2, g2, g2 + C, 1e-5f, nullptr, mask, w.y2, st))) return rc;
+    if ((rc = gn_apply(yb2, B, Tl, C, w.gn2, nt2, g2, g2 + C, 1e-5f, nullptr, 0, mask, w.y2, st))) return rc;
     VConvArgs c = vargs(R.res, P, w, x0, B, Tl, out);
     c.x1 = (const bf16*)x1;
     c.c0 = c0;
@@ -626,7 +629,8 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   const int T1 = T / 2;
   const float* m0 = w.m0;
   const float* m1 = w.m1;
-  auto tbp = [&](int r) { return w.tb + ((size_t)ev * n_res + r) * C; };
+  // time bias of resnet r: one vector per evaluation, or (tb_ld != 0) one per utterance
+  auto tbp = [&](int r) { return w.tb_ld ? w.tb + (size_t)r * C : w.tb + ((size_t)ev * n_res + r) * C; };
   // bf16 + vconv: every tensor a conv reads as x * mask is stored masked by its producer (the last
   // transformer block of a chain, the down/up convs), so mt_vconv needs no input prologue
   const bool mio = vconv && std::is_same<E, bf16>::value;
@@ -802,6 +806,30 @@ int Decoder::step(const void* packed, const float* x, const float* mu_y, const f
   if ((rc = init_inputs(w, x, 1.f, mu_y, spks, B, T, st))) return rc;
   MT_CHECK_HIP(hipMemsetAsync(w.zm, 0, (size_t)B * T * NF * 4, st));
   Euler eu{1.f, 0, 1};  // z = 0 + pred * 1  ==  pred exactly
+  rc = dtype == BF16 ? eval<bf16>(P, w, B, T, 0, eu, st) : eval<float>(P, w, B, T, 0, eu, st);
+  if (rc) return rc;
+  return btc_to_bct(F32, w.zm, NF, 0, B, NF, T, out, st);
+}
+
+// One estimator evaluation with a time per utterance (CFM.compute_loss draws t ~ U(0,1) per sample,
+// model.py:1147-1162): the time MLPs run once per utterance and every ResnetBlock adds its utterance's
+// time bias. t: [B] fp32 in device memory.
+int Decoder::step_times(const void* packed, const float* x, const float* mu_y, const float* mask,
+                        const float* spks, const float* t_dev, int B, int T, float* out, void* ws, size_t ws_bytes,
+                        hipStream_t st) const {
+  int rc;
+  if ((rc = check_geom(B, T))) return rc;
+  MT_REQUIRE(t_dev, "decoder: per-utterance times missing");
+  MT_REQUIRE(ws_bytes >= workspace_bytes(B, T, B), "decoder: workspace too small");
+  const char* P = (const char*)packed;
+  Work w = carve(ws, B, T, B);
+  w.m0 = mask;
+  w.tb_ld = n_res * C;
+  TimeSched ts{};
+  if ((rc = time_embed(P, w, ts, B, st, t_dev))) return rc;
+  if ((rc = init_inputs(w, x, 1.f, mu_y, spks, B, T, st))) return rc;
+  MT_CHECK_HIP(hipMemsetAsync(w.zm, 0, (size_t)B * T * NF * 4, st));
+  Euler eu{1.f, 0, 1};
   rc = dtype == BF16 ? eval<bf16>(P, w, B, T, 0, eu, st) : eval<float>(P, w, B, T, 0, eu, st);
   if (rc) return rc;
   return btc_to_bct(F32, w.zm, NF, 0, B, NF, T, out, st);

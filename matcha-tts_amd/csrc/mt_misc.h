@@ -29,10 +29,13 @@ int mask_rows(int dtype, void* x, int rows, int C, const float* mask, hipStream_
 // ResnetBlock1D block tail (GroupNorm(8) -> Mish [-> + time bias] -> * mask, model.py Block1D/ResnetBlock1D)
 // for bf16 rows y[b][t][C] whose GroupNorm partial sums (fp64 (sum, sumsq) per (b, 32-channel group,
 // part), nparts per group) a conv epilogue produced: h = (mish(y * ga[b,c] + gs[b,c]) + tb[c]) * mask[b,t]
+// tb_ld: elements between utterances' time biases (0: one shared vector)
 int gn_apply(const void* y, int B, int T, int C, const double* part, int nparts, const float* gamma,
-             const float* beta, float eps, const float* tb, const float* mask, void* h, hipStream_t st);
+             const float* beta, float eps, const float* tb, int tb_ld, const float* mask, void* h, hipStream_t st);
 
-int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* emb, hipStream_t st);
+// t_dev (optional): the S times in device memory instead of ts
+int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* emb, hipStream_t st,
+                const float* t_dev = nullptr);
 int rowdot(const float* x, int ldx, const float* W, const float* bias, float* y, int ldy, int yoff, int S,
            int O, int I, int pre, int post, hipStream_t st);
 

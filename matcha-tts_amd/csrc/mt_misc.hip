@@ -246,19 +246,20 @@ int mask_half(const float* m0, int B, int T0, float* m1, hipStream_t st) {
 // time embedding (model.py:747-762, 819-832, 780): per solver evaluation s
 //   emb[s] = [sin(1000 t_s f_k), cos(1000 t_s f_k)]  (f_k = exp(-k ln(1e4)/(half-1)), host table)
 // ------------------------------------------------------------------------------------
-__global__ void sinus_kernel(TimeSched ts, const float* __restrict__ freq, int half,
-                             float* __restrict__ emb) {
+__global__ void sinus_kernel(TimeSched ts, const float* __restrict__ t_dev, const float* __restrict__ freq,
+                             int half, float* __restrict__ emb) {
   const int s = blockIdx.x;
-  const float st = 1000.f * ts.t[s];
+  const float st = 1000.f * (t_dev ? t_dev[s] : ts.t[s]);
   for (int k = threadIdx.x; k < 2 * half; k += blockDim.x) {
     const float a = st * freq[k % half];
     emb[(size_t)s * 2 * half + k] = k < half ? sinf(a) : cosf(a);
   }
 }
 
-int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* emb, hipStream_t st) {
-  MT_REQUIRE(S > 0 && S <= TimeSched::MAX, "time schedule length %d", S);
-  hipLaunchKernelGGL(sinus_kernel, dim3(S), dim3(256), 0, st, ts, freq, half, emb);
+int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* emb, hipStream_t st,
+                const float* t_dev) {
+  MT_REQUIRE(S > 0 && (t_dev || S <= TimeSched::MAX), "time schedule length %d", S);
+  hipLaunchKernelGGL(sinus_kernel, dim3(S), dim3(256), 0, st, ts, t_dev, freq, half, emb);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -463,7 +464,7 @@ constexpr int GN_FR = 32;
 __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ y, int T, int C,
                                                        const double* __restrict__ part, int nparts,
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                       float eps, const float* __restrict__ tb,
+                                                       float eps, const float* __restrict__ tb, int tb_ld,
                                                        const float* __restrict__ mask, bf16* __restrict__ h) {
   __shared__ float ga[256], gs[256], gm[8], gr[8];
   const int b = blockIdx.y, tid = threadIdx.x;
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ 
   }
   float tbv[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) tbv[k] = tb ? tb[c + k] : 0.f;
+  for (int k = 0; k < 8; ++k) tbv[k] = tb ? tb[(size_t)b * tb_ld + c + k] : 0.f;
   if (tid < G) {  // same merge order and formulas as the conv kernel's PF_GN pre-phase (mt_conv.hip)
     const double* p = part + (size_t)(b * G + tid) * nparts * 2;
     double s1 = 0.0, s2 = 0.0;
@@ -528,10 +529,10 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ 
 }
 
 int gn_apply(const void* y, int B, int T, int C, const double* part, int nparts, const float* gamma,
-             const float* beta, float eps, const float* tb, const float* mask, void* h, hipStream_t st) {
+             const float* beta, float eps, const float* tb, int tb_ld, const float* mask, void* h, hipStream_t st) {
   MT_REQUIRE(C % 32 == 0 && C <= 256 && C >= 64 && 256 % (C / 8) == 0 && nparts > 0, "gn_apply: C %d", C);
   hipLaunchKernelGGL(gn_apply_kernel, dim3((T + GN_FR - 1) / GN_FR, B), dim3(256), 0, st, (const bf16*)y, T, C, part, nparts,
-                     gamma, beta, eps, tb, mask, (bf16*)h);
+                     gamma, beta, eps, tb, tb_ld, mask, (bf16*)h);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -98,10 +98,12 @@ struct Decoder {
     double *gn1, *gn2;
     float* apart;  // attention key-split slots
     float* lnp;    // per frame, per 64-channel slab (sum, sum of squares): LayerNorm partials (vconv VE_ROWSTATS)
+    int tb_ld;     // 0: one time bias per evaluation; n_res * C: one per utterance (step_times)
     const float* m0;
   };
   Work carve(void* ws, int B, int T, int S) const;
-  int time_embed(const char* P, const Work& w, const TimeSched& ts, int S, hipStream_t st) const;
+  int time_embed(const char* P, const Work& w, const TimeSched& ts, int S, hipStream_t st,
+                 const float* t_dev = nullptr) const;
 
   struct Euler {
     float dt;
@@ -127,6 +129,8 @@ struct Decoder {
             void* ws, size_t ws_bytes, hipStream_t st) const;
   int step(const void* packed, const float* x, const float* mu_y, const float* mask, const float* spks,
            float t, int B, int T, float* out, void* ws, size_t ws_bytes, hipStream_t st) const;
+  int step_times(const void* packed, const float* x, const float* mu_y, const float* mask, const float* spks,
+                 const float* t_dev, int B, int T, float* out, void* ws, size_t ws_bytes, hipStream_t st) const;
 };
 
 // -------------------------------------------------------------------------------------

@@ -64,6 +64,8 @@ SIGNATURES = {
     "mt_denoise_workspace_bytes": (c_size_t, [c_int, c_int]),
     "mt_denoise": (c_int, [P, c_int, c_int, P, c_float, P, P, c_size_t, P]),
     "mt_maximum_path_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mt_decoder_step_times_workspace_bytes": (c_size_t, [P, c_int, c_int]),
+    "mt_decoder_step_times": (c_int, [P, P, P, P, P, P, P, c_int, c_int, P, P, c_size_t, P]),
     "mt_maximum_path": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_size_t, P]),
     "mt_stft_magnitude": (c_int, [P, c_int, c_int, P, P]),
     "mt_op_conv1d_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),

@@ -281,6 +281,21 @@ class DecoderEngine:
         return out
 
 
+    def step_times(self, packed, x, mu_y, mask, spks, t: torch.Tensor, out=None):
+        """One evaluation with a time per utterance: t [B] (device)."""
+        B, C, T = mu_y.shape
+        out = torch.empty_like(mu_y) if out is None else out
+        tt = f32c(t.reshape(-1).to(mu_y.device))
+        if tt.numel() != B:
+            raise ValueError(f"t has {tt.numel()} values for a batch of {B}")
+        L = lib()
+        ws = _Workspace.get(L.mt_decoder_step_times_workspace_bytes(self.h, B, T), mu_y.device)
+        check(L.mt_decoder_step_times(self.h, packed.data_ptr(), ptr(x), ptr(mu_y), ptr(mask), ptr(spks), ptr(tt),
+                                      B, T, ptr(out), ws.data_ptr(), ws.numel(), stream_handle(mu_y.device)),
+              "decoder_step_times")
+        return out
+
+
 class VocoderEngine:
     """mt_vocoder handle: HiFi-GAN Generator for one config and dtype."""
 

@@ -461,13 +461,10 @@ class Decoder(nn.Module):
         x, mu, mask, spks = rt.f32c(x), rt.f32c(mu), rt.f32c(mask), rt.f32c(spks)
         t = torch.as_tensor(t, dtype=torch.float32).reshape(-1)
         eng, packed = self.engine(), self.packed(x.device)
-        tv = t.detach().cpu()
-        if tv.numel() == 1 or bool((tv == tv[0]).all()):
-            return eng.step(packed, x, mu, mask, spks, float(tv[0]))
-        # per-utterance times: rows are independent (per-sample GroupNorm / attention / masks)
-        outs = [eng.step(packed, x[i:i + 1], mu[i:i + 1], mask[i:i + 1], None if spks is None else spks[i:i + 1],
-                         float(tv[i])) for i in range(x.shape[0])]
-        return torch.cat(outs, 0)
+        if t.numel() == 1:
+            return eng.step(packed, x, mu, mask, spks, float(t[0]))
+        # one time per utterance (CFM.compute_loss): one batched call, the times stay on the device
+        return eng.step_times(packed, x, mu, mask, spks, t.to(x.device))
 
 
 # ======================================================================================
@@ -493,8 +490,18 @@ class BASECFM(nn.Module):
                                   self.solver, out=z)
 
     def compute_loss(self, x1, mask, mu, spks=None, cond=None):
-        raise NotImplementedError("CFM training (model.py:1147-1162) is outside this round's hot path "
-                                  "(SURVEY.md §8f row 3)")
+        """model.py:1147-1162 -> (loss, y_t, pred, u_t): t ~ U(0,1) and z ~ N(0,1) per utterance on the
+        device, one batched estimator evaluation with a time per utterance (mt_decoder_step_times).
+        Forward only: the estimator has no backward kernels yet, so the loss carries no gradient
+        (validation-loss use; training is the rest of SURVEY.md §8f row 3)."""
+        b = mu.shape[0]
+        t = torch.rand([b, 1, 1], device=mu.device, dtype=mu.dtype)
+        z = torch.randn_like(x1)
+        y_t = (1 - (1 - self.sigma_min) * t) * z + t * x1
+        u_t = x1 - (1 - self.sigma_min) * z
+        pred = self.estimator(y_t, mask, mu, t.squeeze(), spks, cond)
+        loss = F.mse_loss(pred, u_t, reduction="sum") / (torch.sum(mask) * u_t.shape[1])
+        return loss, y_t, pred, u_t
 
 
 class CFM(BASECFM):

@@ -250,6 +250,59 @@ def test_decoder_mid_size_vs_oracle_and_determinism():
     assert (one - out1[1:2]).abs().max() < 1e-4
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_decoder_per_utterance_times(precision):
+    """Decoder.forward with one time per utterance (as CFM.compute_loss calls it) runs as ONE batched
+    evaluation (mt_decoder_step_times) and matches the oracle; a uniform [B] time equals the scalar call."""
+    from oracle import matcha_oracle as O
+    from matcha_hip import synthetic
+    dec = make_decoder(160, precision)
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(
+        [(k, tuple(v.shape)) for k, v in dec.state_dict().items()], 31).items()}
+    dec = _load(dec, sd)
+    B, T = 3, 200
+    g = torch.Generator().manual_seed(2)
+    x, mu = torch.randn(B, 80, T, generator=g), torch.randn(B, 80, T, generator=g)
+    mask = (torch.arange(T)[None] < torch.tensor([200, 151, 98])[:, None]).float()[:, None]
+    tt = torch.tensor([0.1, 0.55, 0.93])
+    out = dec(x.cuda(), mask.cuda(), (mu * mask).cuda(), tt.cuda()).cpu()
+    ref = O.decoder_forward(sd, x, mask, mu * mask, tt)
+    if precision == "fp32":
+        assert (out - ref).abs().max() < 2e-4
+    else:
+        assert rel_rms(out, ref) < 2e-2
+    same = torch.full((B,), 0.4)
+    a = dec(x.cuda(), mask.cuda(), (mu * mask).cuda(), same.cuda())
+    b = dec(x.cuda(), mask.cuda(), (mu * mask).cuda(), 0.4)
+    assert torch.equal(a, b)
+
+
+def test_cfm_compute_loss_forward():
+    """CFM.compute_loss (model.py:1147-1162), forward only: same t / z draws as the reference code on
+    the device, the estimator's batched per-utterance evaluation, the loss against the oracle."""
+    from model import CFM
+    from oracle import matcha_oracle as O
+    g = golden("g3_cfm_lj")
+    sd = weights_from(g)
+    dec = _load(make_decoder(160, "fp32"), sd)
+    cfm = CFM(80, {"solver": "euler", "sigma_min": 1e-4}, estimator=dec)
+    mu, mask = t(g["mu"], DEV), t(g["mask"], DEV)
+    x1 = torch.randn(mu.shape, generator=torch.Generator().manual_seed(4)).to(DEV) * mask
+    torch.manual_seed(11)
+    loss, y_t, pred, u_t = cfm.compute_loss(x1, mask, mu)
+    torch.manual_seed(11)
+    tr = torch.rand([mu.shape[0], 1, 1], device=DEV)
+    z = torch.randn_like(x1)
+    y_ref = (1 - (1 - 1e-4) * tr) * z + tr * x1
+    assert torch.equal(y_t, y_ref)
+    pred_ref = O.decoder_forward({k: v.cpu() for k, v in sd.items()}, y_ref.cpu(), mask.cpu(), mu.cpu(),
+                                 tr.squeeze().cpu())
+    assert (pred.cpu() - pred_ref).abs().max() < 2e-4
+    u_ref = x1 - (1 - 1e-4) * z
+    loss_ref = torch.nn.functional.mse_loss(pred_ref, u_ref.cpu(), reduction="sum") / (mask.sum().cpu() * 80)
+    assert abs(loss.item() - loss_ref.item()) <= 1e-5 * abs(loss_ref.item())
+
+
 @pytest.mark.parametrize("T,lens", [(200, [200, 151, 98]), (600, [600, 411, 130])])
 def test_decoder_bf16_vconv_path_vs_generic_and_oracle(T, lens):
     """bf16 decoder with its k=3 / ResnetBlock convs on mt_vconv (producer-masked inputs, GroupNorm
