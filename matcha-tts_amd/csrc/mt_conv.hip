@@ -380,7 +380,7 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
           if (a.half_step) inc = inc * 0.5f;
           const float zn = zp[r] + inc;
           if (a.update_master) zp[r] = zn;
-          xz[r] = from_f<E>(zn);
+          xz[r] = from_f<E>(zn * em);  // the estimator-input slot is read as x * mask only
         }
       } else if constexpr ((EF & EF_OUTF32) != 0) {
         float* yp = reinterpret_cast<float*>(a.y) + orow * a.ldy + ch;

@@ -180,10 +180,14 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
   freq_off = pk.take(Cc / 2 * 4);
 
   // bf16 convs mt_vconv serves (stride 1, C_in % 64 == 0) get its [cin/64][taps][M][64] image too
+  // (the first ResnetBlock reads x ‖ mu ‖ spk, c_cond channels: its image takes the input zero-padded to a
+  // multiple of 64, which is how the vconv path stores that input)
   auto vcify = [&](GemmW& g) {
-    if (dtype == BF16 && g.kind == 0 && vconv_supported(g.cin, g.cout, g.k, g.dil, g.s)) {
+    const int ci = (g.cin + 63) / 64 * 64;
+    if (dtype == BF16 && g.kind == 0 && vconv_supported(ci, g.cout, g.k, g.dil, g.s)) {
       g.vc = true;
-      g.v_off = pk.take(vconv_packed_bytes(g.cin, g.cout, g.k));
+      g.vcin = ci != g.cin ? ci : 0;
+      g.v_off = pk.take(vconv_packed_bytes(ci, g.cout, g.k));
     }
   };
   auto add_res = [&](const std::string& p, int dim_in) {
@@ -325,7 +329,9 @@ int Decoder::pack(const float* const* p, void* packed, hipStream_t st) const {
     PK(pack_gemm(R.c2, dtype, p, P, st));
     PK(pack_gemm(R.res, dtype, p, P, st));
     for (const GemmW* g : {&R.c1, &R.c2, &R.res})
-      if (g->vc) PK(vconv_repack(P + g->w_off, g->Mpad, g->taps, g->cin_pad, g->cin, g->cout, P + g->v_off, st));
+      if (g->vc)
+        PK(vconv_repack(P + g->w_off, g->Mpad, g->taps, g->cin_pad, g->vcin ? g->vcin : g->cin, g->cout,
+                        P + g->v_off, st, g->cin));
     PK(pack_vec(p[R.gn1g], C, C, 0, (float*)(P + R.gn1_off), st));
     PK(pack_vec(p[R.gn1b], C, C, 0, (float*)(P + R.gn1_off) + C, st));
     PK(pack_vec(p[R.gn2g], C, C, 0, (float*)(P + R.gn2_off), st));
@@ -369,7 +375,7 @@ size_t Decoder::workspace_bytes(int B, int T, int S) const {
   // GroupNorm partial slots: generic conv tiles of 64 frames or vconv tiles x waves, whichever is more
   const size_t ntl = (size_t)std::max((T + 63) / 64, vconv_gn_parts(T, C));
   size_t n = 0;
-  n += align256(BT * c_cond * esize);                 // xin
+  n += align256(BT * ((c_cond + 63) / 64 * 64) * esize);  // xin (row stride xld())
   n += 8 * align256(BT * C * esize);                  // H0 H1 XA XB XC U XF + y1
   n += align256(BT * C * esize);                      // y2
   n += align256(BT * 3 * inner * esize);              // qkv
@@ -398,7 +404,7 @@ Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
     return r;
   };
   Work w;
-  w.xin = take(BT * c_cond * esize);
+  w.xin = take(BT * ((c_cond + 63) / 64 * 64) * esize);
   w.H0 = take(BT * C * esize);
   w.H1 = take(BT * C * esize);
   w.XA = take(BT * C * esize);
@@ -452,7 +458,7 @@ VConvArgs Decoder::vargs(const GemmW& g, const char* P, const Work& w, const voi
   a.x = (const bf16*)x;
   a.B = B;
   a.L = Tl;
-  a.cin = g.cin;
+  a.cin = g.vcin ? g.vcin : g.cin;
   a.w = (const bf16*)(P + g.v_off);
   a.bias = (const float*)(P + g.b_off);
   a.M = a.Mpad = g.cout;
@@ -661,8 +667,8 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
     return launch_conv<E, PF_MASK, 0>(a, st);
   };
   // down 0 @T
-  if ((rc = resnet<E>(P, w, res[0], w.xin, nullptr, c_cond, c_cond, false, w.H0, m0, B, T, tbp(0), &rs, st)))
-    return rc;
+  const int xc = mio ? xld() : c_cond;  // input channels of the first ResnetBlock as stored
+  if ((rc = resnet<E>(P, w, res[0], w.xin, nullptr, xc, xc, mio, w.H0, m0, B, T, tbp(0), &rs, st))) return rc;
   if ((rc = tblocks(0, w.H0, m0, T))) return rc;
   if ((rc = plain(down0, w.H0, m0, m1, T, w.XA))) return rc;
   // down 1 @T/2
@@ -721,7 +727,7 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   f.gn_b = (const float*)(P + fgn_off) + C;
   f.zmaster = w.zm;
   f.xin_z = w.xin;
-  f.ld_xin = c_cond;
+  f.ld_xin = xld();
   f.dt = eu.dt;
   f.half_step = eu.half_step;
   f.update_master = eu.update_master;
@@ -731,13 +737,18 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
 int Decoder::init_inputs(const Work& w, const float* z, float temperature, const float* mu_y,
                          const float* spks, int B, int T, hipStream_t st) const {
   int rc;
+  const int ld = xld();
+  if (ld != c_cond) MT_CHECK_HIP(hipMemsetAsync(w.xin, 0, (size_t)B * T * ld * esize, st));  // zero pad channels
   if ((rc = bct_to_btc(F32, z, B, NF, T, temperature, w.zm, NF, 0, st))) return rc;
-  if ((rc = bct_to_btc(dtype, z, B, NF, T, temperature, w.xin, c_cond, 0, st))) return rc;
-  if ((rc = bct_to_btc(dtype, mu_y, B, NF, T, 1.f, w.xin, c_cond, NF, st))) return rc;
+  if ((rc = bct_to_btc(dtype, z, B, NF, T, temperature, w.xin, ld, 0, st))) return rc;
+  if ((rc = bct_to_btc(dtype, mu_y, B, NF, T, 1.f, w.xin, ld, NF, st))) return rc;
   if (c_cond > 2 * NF) {
     MT_REQUIRE(spks != nullptr, "decoder: c_cond %d needs speaker embeddings", c_cond);
-    if ((rc = spk_fill(dtype, spks, B, c_cond - 2 * NF, T, w.xin, c_cond, 2 * NF, st))) return rc;
+    if ((rc = spk_fill(dtype, spks, B, c_cond - 2 * NF, T, w.xin, ld, 2 * NF, st))) return rc;
   }
+  // the vconv path reads x ‖ mu ‖ spk as x * mask straight from HBM: store it masked (the generic path masks
+  // in its prologue, so both read the same values; the Euler epilogue keeps the z slot masked)
+  if (vconv && dtype == BF16 && (rc = mask_rows(dtype, w.xin, B * T, ld, w.m0, st))) return rc;
   return mask_half(w.m0, B, T, w.m1, st);
 }
 

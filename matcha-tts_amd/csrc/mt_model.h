@@ -44,6 +44,7 @@ struct GemmW {
   size_t v_off = 0;  // vconv image [cin/64][taps][Mpad128][64] (bf16 HiFi-GAN convs, mt_vconv.h)
   bool vc = false;
   int vrows = 0;     // ConvTranspose on vconv: polyphase rows per image (M / vrows images back to back)
+  int vcin = 0;      // vconv image input channels when cin is zero-padded to a multiple of 64 (0: cin)
 };
 
 GemmW make_conv(int cout, int cin, int k, int stride, int pad, int dil, std::vector<int> w, int b,
@@ -120,6 +121,8 @@ struct Decoder {
   int tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, bool mask_out, bool row_stats,
              int B, int Tl, hipStream_t st) const;
   bool vc(const GemmW& g) const { return vconv && g.vc; }
+  // decoder input row stride: zero-padded to a multiple of 64 channels (and stored masked) on the vconv path
+  int xld() const { return (vconv && dtype == BF16) ? (c_cond + 63) / 64 * 64 : c_cond; }
   VConvArgs vargs(const GemmW& g, const char* P, const Work& w, const void* x, int B, int Tl, void* y) const;
 
   int init_inputs(const Work& w, const float* z, float temperature, const float* mu_y, const float* spks,

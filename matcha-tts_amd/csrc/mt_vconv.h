@@ -64,7 +64,9 @@ bool vconv_supported(int cin, int cout, int k, int dil, int stride);
 // packed bytes of the [cin/64][taps][Mpad][64] image
 size_t vconv_packed_bytes(int cin, int cout, int k);
 // [Mpad0][taps][cin_pad] (pack_conv layout, bf16) -> [cin/64][taps][Mpad][64]
-int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st);
+// cin_src < cin: the image's channels [cin_src, cin) are zero (an input zero-padded to a multiple of 64)
+int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st,
+                 int cin_src = -1);
 int launch_vconv(int ef, const VConvArgs& a, hipStream_t st);
 // wsum[m] = sum over (chunk, tap, channel) of the packed bf16 image (VE_LN)
 int vconv_wsum(const void* img, int cin, int taps, int cout, float* wsum, hipStream_t st);

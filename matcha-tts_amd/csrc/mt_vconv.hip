@@ -497,8 +497,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
 // ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
-__global__ void vconv_repack_kernel(const bf16* __restrict__ src, int Mpad0, int taps, int cin_pad, int cout,
-                                    int Mpad, size_t total, bf16* __restrict__ dst) {
+__global__ void vconv_repack_kernel(const bf16* __restrict__ src, int Mpad0, int taps, int cin_pad, int cin_src,
+                                    int cout, int Mpad, size_t total, bf16* __restrict__ dst) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int cl = (int)(i & 63);
     size_t r = i >> 6;
@@ -507,7 +507,7 @@ __global__ void vconv_repack_kernel(const bf16* __restrict__ src, int Mpad0, int
     const int t = (int)(r % taps);
     const int c = (int)(r / taps);
     const int ci = c * 64 + cl;
-    dst[i] = m < cout && m < Mpad0 ? src[((size_t)m * taps + t) * cin_pad + ci] : (bf16)0.f;
+    dst[i] = m < cout && m < Mpad0 && ci < cin_src ? src[((size_t)m * taps + t) * cin_pad + ci] : (bf16)0.f;
   }
 }
 
@@ -522,13 +522,15 @@ size_t vconv_packed_bytes(int cin, int cout, int k) {
   return (size_t)(cin / 64) * k * Mpad * 64 * sizeof(bf16);
 }
 
-int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st) {
-  MT_REQUIRE(cin % 64 == 0 && cin_pad >= cin, "vconv_repack: cin %d", cin);
+int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st,
+                 int cin_src) {
+  if (cin_src < 0) cin_src = cin;
+  MT_REQUIRE(cin % 64 == 0 && cin_pad >= cin_src && cin_src <= cin, "vconv_repack: cin %d (source %d)", cin, cin_src);
   const int Mpad = (cout + BMP - 1) / BMP * BMP;
   const size_t total = (size_t)(cin / 64) * taps * Mpad * 64;
   const int blocks = (int)std::min<size_t>((total + 255) / 256, 65535);
   hipLaunchKernelGGL(vconv_repack_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)src, Mpad0, taps, cin_pad,
-                     cout, Mpad, total, (bf16*)dst);
+                     cin_src, cout, Mpad, total, (bf16*)dst);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }
