@@ -16,6 +16,55 @@
 
 namespace mt {
 
+// conv_post (hifigan/models.py:194-196) for bf16 C = 32: tanh(conv_k7(lrelu(x, 0.01)) + b), one output channel.
+// A memory-bound dot product of 7 x 32 inputs per sample: 256 samples per workgroup, their 262 input
+// rows staged once in LDS as lrelu'd fp32 (rounded to bf16 first, as the generic kernel stages them),
+// 144-byte rows so each lane's 16-byte reads of rows t..t+6 hit distinct bank slots.
+constexpr int PC_N = 256, PC_ROW = 36;
+__global__ __launch_bounds__(256) void post_conv_kernel(const bf16* __restrict__ x, int L,
+                                                        const bf16* __restrict__ w, const float* __restrict__ bias,
+                                                        float slope, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float xs[(PC_N + 6) * PC_ROW];
+  __shared__ __attribute__((aligned(16))) float wsm[7 * 32];
+  const int b = blockIdx.y, f0 = blockIdx.x * PC_N, tid = threadIdx.x;
+  const bf16* xb = x + (size_t)b * L * 32;
+  for (int e = tid; e < (PC_N + 6) * 4; e += 256) {
+    const int r = e >> 2, q = e & 3;
+    const int f = f0 - 3 + r;
+    float v[8];
+    if (f >= 0 && f < L) {
+      const u32x4 u = *reinterpret_cast<const u32x4*>(xb + (size_t)f * 32 + q * 8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[2 * j] = (float)(bf16)lrelu_f(__uint_as_float(u[j] << 16), slope);
+        v[2 * j + 1] = (float)(bf16)lrelu_f(__uint_as_float(u[j] & 0xffff0000u), slope);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    }
+    float* d = xs + r * PC_ROW + q * 8;
+    *reinterpret_cast<f32x4*>(d) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(d + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+  if (tid < 7 * 32) wsm[tid] = (float)w[tid];
+  __syncthreads();
+  const int f = f0 + tid;
+  if (f >= L) return;
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const float* row = xs + (tid + k) * PC_ROW;
+#pragma unroll
+    for (int c = 0; c < 32; c += 4) {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(row + c);
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(wsm + k * 32 + c);
+      acc += xv[0] * wv[0] + xv[1] * wv[1] + xv[2] * wv[2] + xv[3] * wv[3];
+    }
+  }
+  out[(size_t)b * L + f] = tanhf(acc + bias[0]);
+}
+
 int Vocoder::init(int resblock_, const std::vector<int>& ur, const std::vector<int>& uk, int up_init_,
                   const std::vector<int>& rk, const std::vector<std::vector<int>>& rd, int dtype_) {
   MT_REQUIRE(resblock_ == 1 || resblock_ == 2, "vocoder: resblock must be 1 or 2");
@@ -430,6 +479,14 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
         }
         if (rc) return rc;
       }
+    }
+  }
+  if constexpr (std::is_same<E, bf16>::value) {
+    if (post.cin == 32 && post.k == 7 && post.cout == 1) {
+      hipLaunchKernelGGL(post_conv_kernel, dim3((L + PC_N - 1) / PC_N, B), dim3(256), 0, st, (const bf16*)XS, L,
+                         (const bf16*)(P + post.w_off), (const float*)(P + post.b_off), 0.01f, wav);
+      MT_CHECK_HIP(hipGetLastError());
+      return 0;
     }
   }
   ConvArgs c = gemm_args(post, P, B, L);
