@@ -441,12 +441,13 @@ int Decoder::time_embed(const char* P, const Work& w, const TimeSched& ts, int S
   if ((rc = rowdot(w.emb, c_cond, (const float*)(P + t1w_off), (const float*)(P + t1b_off), w.h1, TE, 0, S,
                    TE, c_cond, 0, 1, st)))
     return rc;
+  // h2 is only ever read through the ResnetBlocks' Mish (model.py mlp = Mish -> Linear): store mish(h2)
   if ((rc = rowdot(w.h1, TE, (const float*)(P + t2w_off), (const float*)(P + t2b_off), w.h2, TE, 0, S, TE, TE,
-                   0, 0, st)))
+                   0, 2, st)))
     return rc;
   for (int r = 0; r < n_res; ++r) {
     if ((rc = rowdot(w.h2, TE, (const float*)(P + res[r].mlp_w_off), (const float*)(P + res[r].mlp_b_off),
-                     w.tb, n_res * C, r * C, S, C, TE, 1, 0, st)))
+                     w.tb, n_res * C, r * C, S, C, TE, 0, 0, st)))
       return rc;
   }
   return 0;

@@ -265,7 +265,7 @@ int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* 
 }
 
 // y[s][yoff + o] = post( sum_i W[o][i] * pre(x[s][i]) + bias[o] ); one wave per output o.
-// pre: 0 none, 1 mish ; post: 0 none, 1 silu
+// pre: 0 none, 1 mish ; post: 0 none, 1 silu, 2 mish
 // The time-embedding MLPs (model.py TimestepEmbedding, ResnetBlock1D.mlp): S <= 128 rows, I <= 1024.
 // pre(x) of RD_S rows is staged once per block in LDS, each wave keeps its output's weight row in
 // registers across all rows; per (s, o) the lane-strided sum + wave reduction order is fixed.
@@ -308,6 +308,7 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* __restrict__ x
         if (lane == 0 && o < O) {
           float v = acc + (bias ? bias[o] : 0.f);
           if (post == 1) v = v / (1.f + expf(-v));
+          if (post == 2) v = v * tanhf(log1pf(expf(v)));
           y[(size_t)(s0 + r) * ldy + yoff + o] = v;
         }
       }
