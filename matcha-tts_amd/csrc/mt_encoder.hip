@@ -13,6 +13,7 @@
 #include <algorithm>
 
 #include "mt_model.h"
+#include "mt_vconv.h"
 
 namespace mt {
 
@@ -245,6 +246,7 @@ int Encoder::init(int n_vocab_, int n_ch, int filt, int heads_, int layers_, int
   L = ParamList();
   lay.clear();
   pre.clear();
+  ezero_off = 0;
   const long long Cl = C, Wl = W;
   emb = L.add("emb.weight", {n_vocab, Cl});
   emb_off = pk.take((size_t)n_vocab * C * 4);
@@ -289,6 +291,14 @@ int Encoder::init(int n_vocab_, int n_ch, int filt, int heads_, int layers_, int
     l.o = make_conv(W, W, 1, 1, 0, 1, {wo}, bo, esize, pk);
     l.f1 = make_conv(F, W, k, 1, k / 2, 1, {w1}, b1, esize, pk);
     l.f2 = make_conv(W, F, k, 1, k / 2, 1, {w2}, b2, esize, pk);
+    if (dtype == BF16 && vconv_supported(W, F, k, 1, 1) && vconv_supported(F, W, k, 1, 1)) {
+      // the FFN convs on mt_vconv: their inputs are stored masked by their producers (LN1, FFN conv 1)
+      for (GemmW* g : {&l.f1, &l.f2}) {
+        g->vc = true;
+        g->v_off = pk.take(vconv_packed_bytes(g->cin, g->cout, g->k));
+      }
+      if (!ezero_off) ezero_off = pk.take(256);
+    }
     l.n1_off = pk.take(2 * W * 4);
     l.n2_off = pk.take(2 * W * 4);
     lay.push_back(l);
@@ -339,6 +349,8 @@ int Encoder::pack(const float* const* p, void* packed, hipStream_t st) const {
     PK(pack_gemm(l.o, dtype, p, P, st));
     PK(pack_gemm(l.f1, dtype, p, P, st));
     PK(pack_gemm(l.f2, dtype, p, P, st));
+    for (const GemmW* g : {&l.f1, &l.f2})
+      if (g->vc) PK(vconv_repack(P + g->w_off, g->Mpad, g->taps, g->cin_pad, g->cin, g->cout, P + g->v_off, st));
     PK(pack_vec(p[l.n1g], W, W, 0, (float*)(P + l.n1_off), st));
     PK(pack_vec(p[l.n1b], W, W, 0, (float*)(P + l.n1_off) + W, st));
     PK(pack_vec(p[l.n2g], W, W, 0, (float*)(P + l.n2_off), st));
@@ -353,6 +365,7 @@ int Encoder::pack(const float* const* p, void* packed, hipStream_t st) const {
   PK(pack_vec(p[dn2g], DF, DF, 0, (float*)(P + dn2_off), st));
   PK(pack_vec(p[dn2b], DF, DF, 0, (float*)(P + dn2_off) + DF, st));
   PK(pack_vec(p[theta], dk / 4, dk / 4, 0, (float*)(P + theta_off), st));
+  if (ezero_off) PK(pack_vec(nullptr, 1, 64, 0, (float*)(P + ezero_off), st));
 #undef PK
   return 0;
 }
@@ -360,7 +373,7 @@ int Encoder::pack(const float* const* p, void* packed, hipStream_t st) const {
 size_t Encoder::workspace_bytes(int B, int Tx) const {
   const size_t n = (size_t)B * Tx;
   const int wmax = std::max(std::max(W, 3 * W), std::max(F, DF));
-  return 5 * align256(n * wmax * esize) + align256(n * 80 * esize) + align256(n * 4);
+  return 5 * align256(n * wmax * esize) + align256(n * 80 * esize) + align256(n * 4) + 4096;  // + vconv trash
 }
 
 template <class E>
@@ -458,6 +471,42 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
     o.resid = X;
     o.ldr = W;
     if ((rc = launch_conv<E, 0, EF_RESID>(o, st))) return rc;
+    if constexpr (std::is_same<E, bf16>::value) {
+      if (l.f1.vc && l.f2.vc) {
+        // FFN on vconv (model.py:119-130): LN1 stores A masked, conv 1 stores relu(.) masked, conv 2 adds the
+        // residual and masks (its padded frames differ from the generic order v*m + A, and LN2 masks them)
+        char* trash = MU + align256(n * 80 * esize) + align256(n * 4);
+        if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n1_off), eps, xmask, 0, (E*)A, st)))
+          return rc;
+        auto vargs = [&](const GemmW& g, const void* x, void* y) {
+          VConvArgs a{};
+          a.x = (const bf16*)x;
+          a.B = B;
+          a.L = Tx;
+          a.cin = g.cin;
+          a.w = (const bf16*)(P + g.v_off);
+          a.bias = (const float*)(P + g.b_off);
+          a.M = a.Mpad = g.cout;
+          a.taps = g.k;
+          a.dil = 1;
+          a.pad = g.pad;
+          a.y = (bf16*)y;
+          a.div = 1.f;
+          a.zero = (const bf16*)(P + ezero_off);
+          a.trash = (bf16*)trash;
+          a.emask = xmask;
+          a.probe = -1;
+          return a;
+        };
+        if ((rc = launch_vconv(VE_RELU | VE_MASK, vargs(l.f1, A, Hh), st))) return rc;
+        VConvArgs f2 = vargs(l.f2, Hh, Bb);
+        f2.resid = (const bf16*)A;
+        if ((rc = launch_vconv(VE_RESID | VE_MASK, f2, st))) return rc;
+        if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n2_off), eps, xmask, 0, (E*)X, st)))
+          return rc;
+        continue;
+      }
+    }
     if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n1_off), eps, nullptr, 0, (E*)A, st))) return rc;
     ConvArgs f1 = gemm_args(l.f1, P, B, Tx);
     f1.x0 = A;

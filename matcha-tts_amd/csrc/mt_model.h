@@ -159,6 +159,7 @@ struct Encoder {
     size_t n1_off, n2_off;
   };
   std::vector<Layer> lay;
+  size_t ezero_off = 0;  // 256 zero bytes (vconv padding rows) when the FFN convs run on vconv (bf16)
   GemmW proj_m, dp1, dp2, dpp;
   int dn1g, dn1b, dn2g, dn2b, theta;
   size_t dn1_off, dn2_off, theta_off;

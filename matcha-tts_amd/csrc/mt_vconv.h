@@ -23,6 +23,7 @@ enum : int {
   VE_ROWSTATS = 512, // per frame and 64-channel slab: (sum, sum of squares) of the stored values -> row_out
                      // (the next LayerNorm's statistics, consumed with VE_LNP)
   VE_LNP = 1024,     // with VE_LN: ln_stats holds VE_ROWSTATS partials [frames][cin/64] instead of (mean, rstd)
+  VE_RELU = 2048,    // max(v, 0) after the bias (text-encoder FFN, model.py:119-130)
 };
 
 struct VConvArgs {

@@ -287,6 +287,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
               const float sn = __sinf(v * al4[r]);
               v = v + ib4[r] * (sn * sn);
             }
+            if constexpr ((EF & VE_RELU) != 0) v = fmaxf(v, 0.f);
             if constexpr ((EF & VE_RESID) != 0) v = v + bf2(rr[r >> 1], r & 1);
             if constexpr ((EF & VE_ACCUM) != 0) v = bf2(yy[r >> 1], r & 1) + v;
             if constexpr ((EF & VE_DIV) != 0) v = v / a.div;
@@ -652,6 +653,8 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE(VE_GNSTATS)
       MT_VCASE(VE_MASK)
       MT_VCASE(VE_DUAL)
+      MT_VCASE(VE_RELU | VE_MASK)
+      MT_VCASE(VE_RESID | VE_MASK)
       MT_VCASE(VE_RESID | VE_DIV | VE_DUAL)
       MT_VCASE(VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL)
       MT_VCASE(0)
