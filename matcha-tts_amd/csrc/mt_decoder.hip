@@ -268,6 +268,11 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
     int w = L.add("down_blocks.0.2.conv.weight", {C, C, 3});
     int b = L.add("down_blocks.0.2.conv.bias", {C});
     down0 = make_conv(C, C, 3, 2, 1, 1, {w}, b, esize, pk);
+    if (dtype == BF16 && vconv_supported(2 * C, C, 2, 1, 1)) {  // stride 2 as a 2-tap conv over frame pairs
+      down0.vc = true;
+      down0.vcin = 2 * C;
+      down0.v_off = pk.take(vconv_packed_bytes(2 * C, C, 2));
+    }
   }
   add_res("down_blocks.1.0", C);
   add_tbs("down_blocks.1.1");
@@ -287,6 +292,11 @@ int Decoder::init(int c_cond_, int n_mid_, int n_blocks_, int heads_, int dtype_
     int w = L.add("up_blocks.0.2.conv.weight", {C, C, 4});
     int b = L.add("up_blocks.0.2.conv.bias", {C});
     up0 = make_convT(C, C, 4, 2, 1, w, b, esize, pk);
+    if (dtype == BF16 && up0.M <= 1024 && vconv_supported(C, up0.M, up0.taps, 1, 1)) {  // polyphase, placed output
+      up0.vc = true;
+      up0.vrows = up0.M;
+      up0.v_off = pk.take(vconv_packed_bytes(C, up0.M, up0.taps));
+    }
   }
   add_res("up_blocks.1.0", 2 * C);
   add_tbs("up_blocks.1.1");
@@ -357,8 +367,10 @@ int Decoder::pack(const float* const* p, void* packed, hipStream_t st) const {
   }
   PK(pack_vec(nullptr, 1, 64, 0, (float*)(P + zero_off), st));
   PK(pack_gemm(down0, dtype, p, P, st));
+  if (down0.vc) PK(vconv_repack_s2(P + down0.w_off, down0.cin_pad, C, C, P + down0.v_off, st));
   PK(pack_gemm(down1, dtype, p, P, st));
   PK(pack_gemm(up0, dtype, p, P, st));
+  if (up0.vc) PK(vconv_repack(P + up0.w_off, up0.vrows, up0.taps, up0.cin_pad, up0.cin, up0.vrows, P + up0.v_off, st));
   PK(pack_gemm(up1, dtype, p, P, st));
   PK(pack_gemm(fconv, dtype, p, P, st));
   PK(pack_vec(p[fgn_g], C, C, 0, (float*)(P + fgn_off), st));
@@ -671,7 +683,15 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   const int xc = mio ? xld() : c_cond;  // input channels of the first ResnetBlock as stored
   if ((rc = resnet<E>(P, w, res[0], w.xin, nullptr, xc, xc, mio, w.H0, m0, B, T, tbp(0), &rs, st))) return rc;
   if ((rc = tblocks(0, w.H0, m0, T))) return rc;
-  if ((rc = plain(down0, w.H0, m0, m1, T, w.XA))) return rc;
+  if (mio && vc(down0)) {  // frame pairs: [T][C] rows read as [T/2][2C]
+    VConvArgs a = vargs(down0, P, w, w.H0, B, T1, w.XA);
+    a.taps = 2;
+    a.pad = 1;
+    a.emask = m1;
+    if ((rc = launch_vconv(VE_MASK, a, st))) return rc;
+  } else if ((rc = plain(down0, w.H0, m0, m1, T, w.XA))) {
+    return rc;
+  }
   // down 1 @T/2
   if ((rc = resnet<E>(P, w, res[1], w.XA, nullptr, C, C, mio, w.H1, m1, B, T1, tbp(1), &rs, st))) return rc;
   if ((rc = tblocks(1, w.H1, m1, T1))) return rc;
@@ -692,7 +712,25 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
     if ((rc = resnet<E>(P, w, res[r], half[cur], w.H1, C, 2 * C, mio, half[nx], m1, B, T1, tbp(r), &rs, st)))
       return rc;
     if ((rc = tblocks(r, half[nx], m1, T1))) return rc;
-    if ((rc = plain(up0, half[nx], m1, m0, T1, w.U))) return rc;  // ConvTranspose1d k4 s2 p1 -> T
+    if (mio && vc(up0)) {  // ConvTranspose1d k4 s2 p1 -> T as a polyphase conv with a placed, masked output
+      int Tout = 0, Ncols = 0;
+      gemm_geom(up0, T1, &Tout, &Ncols);
+      VConvArgs a = vargs(up0, P, w, half[nx], B, T1, w.U);
+      a.M = a.Mpad = up0.vrows;
+      a.taps = up0.taps;
+      a.pad = up0.gpad;
+      a.Lout = Ncols;
+      a.ldy = up0.M;
+      a.yshift = up0.opad * up0.cout;
+      a.ylim = Tout * up0.cout;
+      a.ystride = (long long)Tout * up0.cout;
+      a.mask_div = up0.cout;
+      a.emask = m0;
+      a.probe = -1;
+      if ((rc = launch_vconv(VE_PMASK, a, st))) return rc;
+    } else if ((rc = plain(up0, half[nx], m1, m0, T1, w.U))) {  // ConvTranspose1d k4 s2 p1 -> T
+      return rc;
+    }
   }
   // up 1 @T: cat(U, skip=H0)
   {

@@ -24,6 +24,7 @@ enum : int {
                      // (the next LayerNorm's statistics, consumed with VE_LNP)
   VE_LNP = 1024,     // with VE_LN: ln_stats holds VE_ROWSTATS partials [frames][cin/64] instead of (mean, rstd)
   VE_RELU = 2048,    // max(v, 0) after the bias (text-encoder FFN, model.py:119-130)
+  VE_PMASK = 4096,   // placed output: v * emask[output frame], frame = element / mask_div
 };
 
 struct VConvArgs {
@@ -56,6 +57,7 @@ struct VConvArgs {
   int yshift;
   int ylim;
   long long ystride;   // elements per utterance of y
+  int mask_div;        // VE_PMASK: output elements per frame
 };
 
 // partial-sum slots per (utterance, group) that VE_GNSTATS writes: column tiles x waves across columns
@@ -69,6 +71,9 @@ size_t vconv_packed_bytes(int cin, int cout, int k);
 int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st,
                  int cin_src = -1);
 int launch_vconv(int ef, const VConvArgs& a, hipStream_t st);
+// image of a k = 3, stride 2, pad 1 conv (generic [Mpad0][3][cin_pad] source) as a 2-tap stride-1 conv over
+// frame pairs (2C input channels): run it with L = T/2, cin = 2C, taps = 2, pad = 1 on the same [T][C] rows
+int vconv_repack_s2(const void* src, int cin_pad, int C, int cout, void* dst, hipStream_t st);
 // wsum[m] = sum over (chunk, tap, channel) of the packed bf16 image (VE_LN)
 int vconv_wsum(const void* img, int cin, int taps, int cout, float* wsum, hipStream_t st);
 

@@ -264,6 +264,13 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
           swap16(yx1, yy1);
         }
         uint32_t o1[2][2], o2[2][2];  // [X|Y][dword]
+        float pmk = 1.f;  // VE_PMASK: the mask of the output frame this lane's 32-row group lands in
+        if constexpr ((EF & VE_PMASK) != 0) {
+          const int n = n0 + wn * WNC + fn * 16 + l16;
+          const int e = n * a.ldy + m0 + wm * 64 + fp * 32 - a.yshift;
+          const bool ok = n < a.Lout && e >= 0 && e < a.ylim;
+          pmk = ok ? a.emask[(size_t)b * (a.ylim / a.mask_div) + e / a.mask_div] : 0.f;
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int fm = 2 * fp + h;
@@ -298,6 +305,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
               }
             }
             if constexpr ((EF & VE_MASK) != 0) v = v * mk[fn];
+            if constexpr ((EF & VE_PMASK) != 0) v = v * pmk;
             const bf16 rb = (bf16)v;
             if constexpr ((EF & VE_ROWSTATS) != 0) {
               const float fr = (float)rb;
@@ -512,6 +520,35 @@ __global__ void vconv_repack_kernel(const bf16* __restrict__ src, int Mpad0, int
   }
 }
 
+// k = 3, stride 2, pad 1 conv as a stride-1 conv over frame PAIRS ([T][C] == [T/2][2C] in memory): output j
+// = W0 x[2j-1] + W1 x[2j] + W2 x[2j+1] = W'_0 . pair[j-1] + W'_1 . pair[j] with W'_0 = (0 | W0) and
+// W'_1 = (W1 | W2) over the pair's (even | odd) channel halves. Source: the generic [Mpad0][3][cin_pad] image.
+__global__ void vconv_repack_s2_kernel(const bf16* __restrict__ src, int cin_pad, int C, int cout, int Mpad,
+                                       size_t total, bf16* __restrict__ dst) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int cl = (int)(i & 63);
+    size_t r = i >> 6;
+    const int m = (int)(r % Mpad);
+    r /= Mpad;
+    const int t = (int)(r % 2);
+    const int cp = (int)(r / 2) * 64 + cl;  // channel of the pair
+    const int odd = cp >= C, ci = odd ? cp - C : cp;
+    const int k = t == 0 ? (odd ? 0 : -1) : (odd ? 2 : 1);
+    dst[i] = (m < cout && k >= 0) ? src[((size_t)m * 3 + k) * cin_pad + ci] : (bf16)0.f;
+  }
+}
+
+int vconv_repack_s2(const void* src, int cin_pad, int C, int cout, void* dst, hipStream_t st) {
+  MT_REQUIRE(C % 32 == 0 && cin_pad >= C, "vconv_repack_s2: C %d", C);
+  const int Mpad = (cout + BMP - 1) / BMP * BMP;
+  const size_t total = (size_t)(2 * C / 64) * 2 * Mpad * 64;
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 65535);
+  hipLaunchKernelGGL(vconv_repack_s2_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)src, cin_pad, C, cout, Mpad,
+                     total, (bf16*)dst);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 bool vconv_supported(int cin, int cout, int k, int dil, int stride) {
   // k >= 2 convs stage a chunk's rows during its predecessor's first step and read them a step later;
   // 1x1 convs use the K1 pipeline (rows staged two chunks ahead)
@@ -591,7 +628,9 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
              a.c0, a.cin);
   const bool k1 = a0.taps == 1;
   const bool placed = a0.Lout || a0.ldy || a0.yshift || a0.ylim || a0.ystride;
-  MT_REQUIRE(!placed || (!k1 && (ef & ~VE_DUAL) == 0 && a0.Lout > 0 && a0.ldy >= a0.M && a0.ylim > 0 &&
+  MT_REQUIRE(!(ef & VE_PMASK) || (a0.emask && a0.mask_div > 0 && a0.ylim % a0.mask_div == 0 && a0.mask_div % 32 == 0),
+             "vconv: placed-output mask");
+  MT_REQUIRE(!placed || (!k1 && (ef & ~(VE_DUAL | VE_PMASK)) == 0 && a0.Lout > 0 && a0.ldy >= a0.M && a0.ylim > 0 &&
                          a0.ystride >= a0.ylim && a0.yshift % 8 == 0 && a0.ldy % 8 == 0),
              "vconv: placed output (ConvTranspose) geometry / epilogue %d", ef);
   if (k1) {  // no halo: the utterances' frames are one contiguous sequence of B*L columns
@@ -654,6 +693,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE(VE_MASK)
       MT_VCASE(VE_DUAL)
       MT_VCASE(VE_RELU | VE_MASK)
+      MT_VCASE(VE_PMASK)
       MT_VCASE(VE_RESID | VE_MASK)
       MT_VCASE(VE_RESID | VE_DIV | VE_DUAL)
       MT_VCASE(VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL)
