@@ -107,6 +107,21 @@ __device__ __forceinline__ void rb_chunk_dispatch(int nj, int ng, const char* bs
   }
 }
 
+// bf16 epilogue helpers: pairs of frames' channels as packed fp32 math (v_pk_add / v_pk_mul), one
+// v_cvt_pk_bf16_f32 per pair, lrelu as max(x, slope * x) (equal to x > 0 ? x : slope * x for 0 < slope < 1)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t rb_pack(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+__device__ __forceinline__ f32x2 rb_unpack(uint32_t w) {
+  return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+__device__ __forceinline__ f32x2 rb_lrelu(f32x2 t, float slope) {
+  const f32x2 m = t * slope;
+  return f32x2{__builtin_fmaxf(t.x, m.x), __builtin_fmaxf(t.y, m.y)};
+}
+
 template <class E, int C, int N>
 __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {
   using TL = RBTile<E, C, N>;
@@ -138,16 +153,42 @@ __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {
     return reinterpret_cast<const E*>(cv.w) + ((size_t)(cbk * 32 + (lane & 15)) * a.k[j]) * C + (lane >> 4) * VN;
   };
 
-  float out[OJ][FMJ][4];  // running resblock sum of this wave's output blocks (E-rounded values)
+  // running resblock sum of this wave's output blocks (E-rounded values; bf16: packed pairs)
+  constexpr bool BF = std::is_same<E, bf16>::value;
+  float out[BF ? 1 : OJ][FMJ][4];
+  uint32_t outp[BF ? OJ : 1][FMJ][2];
 #pragma unroll
-  for (int o = 0; o < OJ; ++o)
+  for (int o = 0; o < (BF ? OJ : 1); ++o)
+#pragma unroll
+    for (int x = 0; x < FMJ; ++x) outp[o][x][0] = outp[o][x][1] = 0u;
+#pragma unroll
+  for (int o = 0; o < (BF ? 1 : OJ); ++o)
 #pragma unroll
     for (int x = 0; x < FMJ; ++x)
 #pragma unroll
       for (int r = 0; r < 4; ++r) out[o][x][r] = 0.f;
 
-  Vec16<E> Acur[4][FMJ], Anext[4][FMJ];
-  rb_load_chunk<E, C, FMJ>(wlane(0), a.k[0], 0, 0, Acur);
+  // The stage input tile (+ halo) stays in registers for the whole kernel: every resblock restarts its
+  // chain from it without another trip to L2 / HBM (and without a load stall behind a barrier).
+  // (C = 32 only: at C = 64 the tile would push the kernel past its register budget)
+  constexpr bool XREG = C == 32;
+  constexpr int XV = XREG ? (TL::W0 * TL::VPR + TL::NT - 1) / TL::NT : 1;
+  Vec16<E> xr[XV];
+  if constexpr (XREG) {
+#pragma unroll
+    for (int k = 0; k < XV; ++k) {
+      const int v = tid + k * TL::NT;
+      const int r = v / TL::VPR, sl = v % TL::VPR;
+      const int f = fbase + r;
+      xr[k] = zero16<E>();
+      if (r < W0 && f >= 0 && f < a.L) xr[k] = load16(X + (size_t)f * C + sl * VN);
+    }
+  }
+
+  // A fragments ping-pong between A0 / A1 (no register copies); A0 holds the next conv's first chunk
+  Vec16<E> A0[4][FMJ], A1[4][FMJ];
+  rb_load_chunk<E, C, FMJ>(wlane(0), a.k[0], 0, 0, A0);
+  const bool interior = fbase >= 0 && fbase + W0 <= a.L;  // no tile row outside the sequence
 
   for (int c = 0; c < ncv; ++c) {
     const int j = c / np2, i = (c % np2) >> 1, half = c & 1;
@@ -167,19 +208,34 @@ __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {
       for (int r = 0; r < 4; ++r) bias[x][r] = cv.bias[cbk * 32 + x * 16 + 4 * (lane >> 4) + r];
 
     if (half == 0 && (c % np2) == 0) {
-      // ---- new resblock: S = x, SL = lrelu(x) over tile + halo (0 outside [0, L)); x is L2-resident
-      __syncthreads();
-      for (int v = tid; v < W0 * TL::VPR; v += TL::NT) {
-        const int r = v / TL::VPR, sl = v % TL::VPR;
-        const int f = fbase + r;
-        Vec16<E> raw = zero16<E>(), act = zero16<E>();
-        if (f >= 0 && f < a.L) {
-          raw = load16(X + (size_t)f * C + sl * VN);
+      // ---- new resblock: S = x, SL = lrelu(x) over tile + halo (0 outside [0, L)). The previous conv's
+      // closing barrier already ordered every read of S / SL before these writes.
+      if constexpr (XREG) {
 #pragma unroll
-          for (int k = 0; k < VN; ++k) act.set(k, lrelu_f(raw.get(k), a.slope));
+        for (int k = 0; k < XV; ++k) {
+          const int v = tid + k * TL::NT;
+          const int r = v / TL::VPR, sl = v % TL::VPR;
+          if (r >= W0) break;
+          Vec16<E> act;
+#pragma unroll
+          for (int e = 0; e < VN; ++e) act.set(e, lrelu_f(xr[k].get(e), a.slope));
+          store16(reinterpret_cast<E*>(S + r * ROW + sl * 16), xr[k]);
+          store16(reinterpret_cast<E*>(SL + r * ROW + sl * 16), act);
         }
-        store16(reinterpret_cast<E*>(S + r * ROW + sl * 16), raw);
-        store16(reinterpret_cast<E*>(SL + r * ROW + sl * 16), act);
+      } else {
+        // x is L2-resident: re-read it per resblock
+        for (int v = tid; v < W0 * TL::VPR; v += TL::NT) {
+          const int r = v / TL::VPR, sl = v % TL::VPR;
+          const int f = fbase + r;
+          Vec16<E> raw = zero16<E>(), act = zero16<E>();
+          if (f >= 0 && f < a.L) {
+            raw = load16(X + (size_t)f * C + sl * VN);
+#pragma unroll
+            for (int e = 0; e < VN; ++e) act.set(e, lrelu_f(raw.get(e), a.slope));
+          }
+          store16(reinterpret_cast<E*>(S + r * ROW + sl * 16), raw);
+          store16(reinterpret_cast<E*>(SL + r * ROW + sl * 16), act);
+        }
       }
       __syncthreads();
     }
@@ -195,22 +251,20 @@ __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {
     const E* wl = wlane(c);
     const int ngroups = (kk + 3) / 4, nchunks = ngroups * KC;
     const int cn = c + 1 < ncv ? c + 1 : c;
-    const E* wl_next = wlane(cn);
-    const int kk_next = a.k[cn / np2];
     const int row0 = ra + fw * 16 + (lane & 15) - qd;
-    for (int ch = 0; ch < nchunks; ++ch) {
-      const int g = ch / KC, kc = ch % KC;
-      if (ch + 1 < nchunks)
-        rb_load_chunk<E, C, FMJ>(wl, kk, (ch + 1) / KC, (ch + 1) % KC, Anext);
-      else
-        rb_load_chunk<E, C, FMJ>(wl_next, kk_next, 0, 0, Anext);
-      rb_chunk_dispatch<E, JPW, FMJ, ROW, WPC>(nj, min(4, kk - 4 * g), src + kc * 64 + (lane >> 4) * 16, row0, g,
-                                               d, Acur, acc);
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int x = 0; x < FMJ; ++x) Acur[t][x] = Anext[t][x];
+    const char* bsrc = src + (lane >> 4) * 16;
+    for (int ch = 0;;) {
+      if (ch + 1 < nchunks) rb_load_chunk<E, C, FMJ>(wl, kk, (ch + 1) / KC, (ch + 1) % KC, A1);
+      rb_chunk_dispatch<E, JPW, FMJ, ROW, WPC>(nj, min(4, kk - 4 * (ch / KC)), bsrc + (ch % KC) * 64, row0, ch / KC,
+                                               d, A0, acc);
+      if (++ch == nchunks) break;
+      if (ch + 1 < nchunks) rb_load_chunk<E, C, FMJ>(wl, kk, (ch + 1) / KC, (ch + 1) % KC, A0);
+      rb_chunk_dispatch<E, JPW, FMJ, ROW, WPC>(nj, min(4, kk - 4 * (ch / KC)), bsrc + (ch % KC) * 64, row0, ch / KC,
+                                               d, A1, acc);
+      if (++ch == nchunks) break;
     }
+    // the next conv's first chunk is in flight during this conv's epilogue
+    rb_load_chunk<E, C, FMJ>(wlane(cn), a.k[cn / np2], 0, 0, A0);
     // No barrier here: this conv's epilogue writes T (conv1) or S / SL (conv2), none of which its own MFMA
     // phase reads (src is SL for conv1, T for conv2); the writes only race with the NEXT conv's reads,
     // which the barrier after the epilogue orders.
@@ -222,46 +276,51 @@ __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {
       const int row = ra + (fw + jj * WPC) * 16 + (lane & 15);
       if (row >= rb) continue;
       const int f = fbase + row;
-      const bool inseq = f >= 0 && f < a.L;
+      const bool inseq = interior || (f >= 0 && f < a.L);
 #pragma unroll
       for (int x = 0; x < FMJ; ++x) {
         const int ch = cbk * 32 + x * 16 + 4 * (lane >> 4);
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[jj][x][r] + bias[x][r];
-        if constexpr (std::is_same<E, bf16>::value) {
+        if constexpr (BF) {
           // 4 consecutive channels of one frame per lane: one 8-byte LDS access instead of four 2-byte ones
+          f32x2 v01 = f32x2{acc[jj][x][0], acc[jj][x][1]} + f32x2{bias[x][0], bias[x][1]};
+          f32x2 v23 = f32x2{acc[jj][x][2], acc[jj][x][3]} + f32x2{bias[x][2], bias[x][3]};
           if (half == 0) {
-            uint32_t w[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const bf16 t0 = (bf16)v[2 * h], t1 = (bf16)v[2 * h + 1];
-              const bf16 a0 = (bf16)(inseq ? lrelu_f((float)t0, a.slope) : 0.f);
-              const bf16 a1 = (bf16)(inseq ? lrelu_f((float)t1, a.slope) : 0.f);
-              w[h] = (uint32_t)__builtin_bit_cast(uint16_t, a0) | ((uint32_t)__builtin_bit_cast(uint16_t, a1) << 16);
-            }
-            *reinterpret_cast<uint2*>(T + row * ROW + ch * 2) = make_uint2(w[0], w[1]);
+            uint2 w = make_uint2(rb_pack(rb_lrelu(rb_unpack(rb_pack(v01)), a.slope)),
+                                 rb_pack(rb_lrelu(rb_unpack(rb_pack(v23)), a.slope)));
+            if (!inseq) w = make_uint2(0u, 0u);
+            *reinterpret_cast<uint2*>(T + row * ROW + ch * 2) = w;
             continue;
           }
           const uint2 sr = *reinterpret_cast<const uint2*>(S + row * ROW + ch * 2);
-          v[0] += __uint_as_float(sr.x << 16);
-          v[1] += __uint_as_float(sr.x & 0xffff0000u);
-          v[2] += __uint_as_float(sr.y << 16);
-          v[3] += __uint_as_float(sr.y & 0xffff0000u);
+          v01 += rb_unpack(sr.x);
+          v23 += rb_unpack(sr.y);
           if (!last) {
-            uint32_t ws_[2], wl_[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const bf16 s0 = (bf16)(inseq ? v[2 * h] : 0.f), s1 = (bf16)(inseq ? v[2 * h + 1] : 0.f);
-              const bf16 l0 = (bf16)lrelu_f((float)s0, a.slope), l1 = (bf16)lrelu_f((float)s1, a.slope);
-              ws_[h] = (uint32_t)__builtin_bit_cast(uint16_t, s0) | ((uint32_t)__builtin_bit_cast(uint16_t, s1) << 16);
-              wl_[h] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
-            }
-            *reinterpret_cast<uint2*>(S + row * ROW + ch * 2) = make_uint2(ws_[0], ws_[1]);
-            *reinterpret_cast<uint2*>(SL + row * ROW + ch * 2) = make_uint2(wl_[0], wl_[1]);
+            uint2 ws = make_uint2(rb_pack(v01), rb_pack(v23));
+            if (!inseq) ws = make_uint2(0u, 0u);
+            *reinterpret_cast<uint2*>(S + row * ROW + ch * 2) = ws;
+            *reinterpret_cast<uint2*>(SL + row * ROW + ch * 2) =
+                make_uint2(rb_pack(rb_lrelu(rb_unpack(ws.x), a.slope)), rb_pack(rb_lrelu(rb_unpack(ws.y), a.slope)));
             continue;
           }
+          if (jj < OJ) {
+            // xs = rb_0; xs += rb_j (rounded to bf16 after every add, as the per-layer path stores xs);
+            // the last add is followed by / nk before rounding
+            if (j != 0) {
+              v01 += rb_unpack(outp[jj][x][0]);
+              v23 += rb_unpack(outp[jj][x][1]);
+            }
+            if (j == a.nk - 1) {
+              v01 = f32x2{v01.x / a.div, v01.y / a.div};
+              v23 = f32x2{v23.x / a.div, v23.y / a.div};
+            }
+            outp[jj][x][0] = rb_pack(v01);
+            outp[jj][x][1] = rb_pack(v23);
+          }
+          continue;
         } else {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[jj][x][r] + bias[x][r];
         if (half == 0) {
           E* tp = reinterpret_cast<E*>(T + row * ROW) + ch;
 #pragma unroll
@@ -285,18 +344,16 @@ __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {
           }
           continue;
         }
-        }
-        {
-          if (jj < OJ) {
-            // xs = rb_0; xs += rb_j (rounded to E after every add, as the per-layer path
-            // stores xs); the last add is followed by / nk before rounding
+        if (jj < OJ) {
+          // xs = rb_0; xs += rb_j (rounded to E after every add, as the per-layer path
+          // stores xs); the last add is followed by / nk before rounding
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float o = j == 0 ? v[r] : out[jj][x][r] + v[r];
-              if (j == a.nk - 1) o = o / a.div;
-              out[jj][x][r] = to_f(from_f<E>(o));
-            }
+          for (int r = 0; r < 4; ++r) {
+            float o = j == 0 ? v[r] : out[jj][x][r] + v[r];
+            if (j == a.nk - 1) o = o / a.div;
+            out[jj][x][r] = to_f(from_f<E>(o));
           }
+        }
         }
       }
     }
@@ -311,8 +368,12 @@ __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {
 #pragma unroll
     for (int x = 0; x < FMJ; ++x) {
       E* yp = Y + (size_t)f * C + cbk * 32 + x * 16 + 4 * (lane >> 4);
+      if constexpr (BF) {
+        *reinterpret_cast<uint2*>(yp) = make_uint2(outp[o][x][0], outp[o][x][1]);
+      } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) yp[r] = from_f<E>(out[o][x][r]);
+        for (int r = 0; r < 4; ++r) yp[r] = from_f<E>(out[o][x][r]);
+      }
     }
   }
 }
