@@ -489,19 +489,28 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ 
   float tbv[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) tbv[k] = tb ? tb[(size_t)b * tb_ld + c + k] : 0.f;
-  if (tid < G) {  // same merge order and formulas as the conv kernel's PF_GN pre-phase (mt_conv.hip)
-    const double* p = part + (size_t)(b * G + tid) * nparts * 2;
+  if (tid < 64) {
+    // first wave: 64 / G lanes per group each sum a strided subset of the group's partials (all loads in
+    // flight at once), then a butterfly inside the lane segment
+    const int lpg = 64 / G, g = tid / lpg, sub = tid % lpg;
+    const double* p = part + (size_t)(b * G + g) * nparts * 2;
     double s1 = 0.0, s2 = 0.0;
-    for (int i = 0; i < nparts; ++i) {
+    for (int i = sub; i < nparts; i += lpg) {
       s1 += p[2 * i];
       s2 += p[2 * i + 1];
     }
-    const double n = 32.0 * (double)T;
-    const double mean = s1 / n;
-    double var = s2 / n - mean * mean;
-    var = var < 0.0 ? 0.0 : var;
-    gm[tid] = (float)mean;
-    gr[tid] = (float)(1.0 / sqrt(var + (double)eps));
+    for (int o = lpg >> 1; o > 0; o >>= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    if (sub == 0) {
+      const double n = 32.0 * (double)T;
+      const double mean = s1 / n;
+      double var = s2 / n - mean * mean;
+      var = var < 0.0 ? 0.0 : var;
+      gm[g] = (float)mean;
+      gr[g] = (float)(1.0 / sqrt(var + (double)eps));
+    }
   }
   __syncthreads();
   for (int cc = tid; cc < C; cc += 256) {
