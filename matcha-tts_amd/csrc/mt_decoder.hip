@@ -385,7 +385,7 @@ int Decoder::pack(const float* const* p, void* packed, hipStream_t st) const {
 size_t Decoder::workspace_bytes(int B, int T, int S) const {
   const size_t BT = (size_t)B * T;
   // GroupNorm partial slots: generic conv tiles of 64 frames or vconv tiles x waves, whichever is more
-  const size_t ntl = (size_t)std::max((T + 63) / 64, vconv_gn_parts(T, C));
+  const size_t ntl = (size_t)std::max((T + 63) / 64, vconv_gn_parts_max(T));
   size_t n = 0;
   n += align256(BT * ((c_cond + 63) / 64 * 64) * esize);  // xin (row stride xld())
   n += 8 * align256(BT * C * esize);                  // H0 H1 XA XB XC U XF + y1
@@ -408,7 +408,7 @@ size_t Decoder::workspace_bytes(int B, int T, int S) const {
 
 Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
   const size_t BT = (size_t)B * T;
-  const size_t ntl = (size_t)std::max((T + 63) / 64, vconv_gn_parts(T, C));
+  const size_t ntl = (size_t)std::max((T + 63) / 64, vconv_gn_parts_max(T));
   char* p = (char*)ws;
   auto take = [&](size_t bytes) {
     char* r = p;
@@ -510,7 +510,7 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
     a.cin = cin;
     a.gn_out = w.gn1;
     if ((rc = launch_vconv(VE_GNSTATS, a, st))) return rc;
-    nt1 = vconv_gn_parts(Tl, C);
+    nt1 = vconv_gn_parts(B, Tl, C);
   } else {
     ConvArgs a = gemm_args(R.c1, P, B, Tl);
     a.x0 = x0;
@@ -529,7 +529,7 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
     VConvArgs b = vargs(R.c2, P, w, w.y2, B, Tl, w.y1);
     b.gn_out = w.gn2;
     if ((rc = launch_vconv(VE_GNSTATS, b, st))) return rc;
-    nt2 = vconv_gn_parts(Tl, C);
+    nt2 = vconv_gn_parts(B, Tl, C);
     yb2 = w.y1;
   } else {
     ConvArgs b = gemm_args(R.c2, P, B, Tl);
@@ -745,7 +745,7 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
     VConvArgs a = vargs(fconv, P, w, w.U, B, T, w.y1);
     a.gn_out = w.gn1;
     if ((rc = launch_vconv(VE_GNSTATS, a, st))) return rc;
-    ntf = vconv_gn_parts(T, C);
+    ntf = vconv_gn_parts(B, T, C);
   } else {
     ConvArgs a = gemm_args(fconv, P, B, T);
     a.x0 = w.U;

@@ -45,7 +45,7 @@ struct VConvArgs {
   const float* snake_alpha;  // [M] exp(alpha) (VE_SNAKE)
   const float* snake_ibeta;  // [M] 1 / (exp(beta) + 1e-9)
   const float* emask;        // [B*L] frame mask (VE_MASK)
-  double* gn_out;            // [B][M/32][vconv_gn_parts(L, M)][2] (VE_GNSTATS)
+  double* gn_out;            // [B][M/32][vconv_gn_parts(B, L, M)][2] (VE_GNSTATS)
   float* row_out;            // [B*L][M/64][2] (VE_ROWSTATS)
   float ln_eps;              // VE_LNP
   int probe;                 // launch-probe site of k >= 2 launches (0: PROBE_VCONV, < 0: none)
@@ -61,7 +61,9 @@ struct VConvArgs {
 };
 
 // partial-sum slots per (utterance, group) that VE_GNSTATS writes: column tiles x waves across columns
-int vconv_gn_parts(int L, int M);
+int vconv_gn_parts(int B, int L, int M);
+// an upper bound of vconv_gn_parts over B (workspace sizing)
+int vconv_gn_parts_max(int L);
 
 bool vconv_supported(int cin, int cout, int k, int dil, int stride);
 // packed bytes of the [cin/64][taps][Mpad][64] image

@@ -602,10 +602,25 @@ int vconv_wsum(const void* img, int cin, int taps, int cout, float* wsum, hipStr
   return 0;
 }
 
-int vconv_gn_parts(int L, int M) {
-  const int BM = M % 128 == 0 ? 128 : 64;
-  return (L + BN - 1) / BN * (8 / (BM / 64));
+// Frames per tile of a k >= 2 conv with 128-row tiles: 256, or 128 when the 256-frame grid leaves CUs idle
+// and the finer grid finishes sooner (the decoder's half-resolution blocks: B = 32, L = 364 gives 128 tiles
+// of 256 frames (40 % of them padding) but 192 tiles of 128). A 128-frame tile carries the same per-step
+// barrier and staging overhead for half the MFMAs, priced as 1.25x its frames.
+static int vconv_tile_frames(int B, int L, int Mpad, int ef) {
+  if (Mpad % 128 != 0 || (ef & ~(VE_GNSTATS | VE_MASK)) != 0) return BN;
+  const long cu = cu_count(), ntm = Mpad / 128;
+  const long t256 = (long)B * ((L + 255) / 256) * ntm, t128 = (long)B * ((L + 127) / 128) * ntm;
+  const long c256 = (t256 + cu - 1) / cu * 256 * 4, c128 = (t128 + cu - 1) / cu * 128 * 5;
+  return c128 < c256 ? 128 : BN;
 }
+
+int vconv_gn_parts(int B, int L, int M) {
+  const int BM = M % 128 == 0 ? 128 : 64;
+  const int bn = vconv_tile_frames(B, L, M, VE_GNSTATS);
+  return (L + bn - 1) / bn * (8 / (BM / 64));
+}
+
+int vconv_gn_parts_max(int L) { return (L + 127) / 128 * 4; }
 
 int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(a0.x && a0.w && a0.bias && a0.y && a0.zero && a0.trash, "vconv: null pointer");
@@ -658,6 +673,8 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   constexpr int BN64 = 384;
   if (!k1 && BM == 64) ntiles = (long)a.B * ((a.Lout + BN64 - 1) / BN64) * (a.Mpad / BM);
   MT_REQUIRE(!(ef & VE_GNSTATS) || BM == 128, "vconv: GroupNorm partials need 128-row tiles");
+  const bool half = !k1 && !placed && vconv_tile_frames(a.B, a.L, a.Mpad, ef) == 128;
+  if (half) ntiles = (long)a.B * ((a.L + 127) / 128) * (a.Mpad / BM);
   const int G = (int)std::min<long>(ntiles, cu_count());
   const double flops = 2.0 * a.M * a.cin * a.taps * (double)a.B * a.Lout;
   const int touts = 1 + ((ef & VE_RESID) ? 1 : 0) + ((ef & VE_ACCUM) ? 1 : 0) + ((ef & VE_DUAL) ? 1 : 0);
@@ -670,6 +687,12 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   case E:                                                                                          \
     if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false>), dim3(G), dim3(NT), 0, st, a); \
     else hipLaunchKernelGGL((vconv_kernel<E, 64, false, BN64>), dim3(G), dim3(NT), 0, st, a);     \
+    break;
+#define MT_VCASE_H(E)                                                                                  \
+  case E:                                                                                              \
+    if (half) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 128>), dim3(G), dim3(NT), 0, st, a);     \
+    else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false>), dim3(G), dim3(NT), 0, st, a); \
+    else hipLaunchKernelGGL((vconv_kernel<E, 64, false, BN64>), dim3(G), dim3(NT), 0, st, a);          \
     break;
 #define MT_VCASE1(E)                                                                                    \
   case E:                                                                                               \
@@ -689,8 +712,8 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE(VE_RESID | VE_ACCUM)
       MT_VCASE(VE_RESID | VE_DIV)
       MT_VCASE(VE_RESID | VE_ACCUM | VE_DIV)
-      MT_VCASE(VE_GNSTATS)
-      MT_VCASE(VE_MASK)
+      MT_VCASE_H(VE_GNSTATS)
+      MT_VCASE_H(VE_MASK)
       MT_VCASE(VE_DUAL)
       MT_VCASE(VE_RELU | VE_MASK)
       MT_VCASE(VE_PMASK)
@@ -714,6 +737,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
     }
   }
 #undef MT_VCASE
+#undef MT_VCASE_H
 #undef MT_VCASE1
   MT_CHECK_HIP(hipGetLastError());
   if (probed) probe_end(site, st, flops, bytes);
