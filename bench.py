@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-denoise", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--cpu-utterances", type=int, default=3, help="CPU baseline sample size (batch 1)")
+    p.add_argument("--no-north-star", action="store_true", help="skip the B=256 single-GPU record")
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()
 
@@ -108,20 +109,61 @@ def step(m, g, den, x, xl, n_ts, denoise):
     return mel, yl, wav
 
 
-def roofline(probe, precision, default_workload=True):
+# SURVEY.md §8d per-frame algorithmic cost of the hot path (one padded mel frame of one utterance):
+# layer-boundary bytes (bf16) and FLOPs. Decoder per ODE step: 27,536 elements moved (25,488 GEMM-layer +
+# 2,048 attention core) and 10,985,472 + 1,536*T + 6,619,136/T FLOPs; vocoder: 1,013,072 elements and
+# 614,105,088 FLOPs per mel frame (exact).
+DEC_BYTES_PER_FRAME_STEP = 27_536 * 2
+VOC_BYTES_PER_FRAME = 1_013_072 * 2
+VOC_FLOPS_PER_FRAME = 614_105_088
+PEAK_FLOPS, PEAK_BW = 2.5e15, 8.0e12  # MI355X dense bf16 MFMA, HBM3E (MI355X_MICROARCH.md)
+
+
+def dec_flops_per_frame_step(t_pad):
+    return 10_985_472 + 1_536 * t_pad + 6_619_136 / t_pad
+
+
+def path_roofline(sec_per_step, y_lengths, t_pad, n_ts):
+    """Whole hot path (mu_y, mask, z -> wav): the roofline time of one step's work =
+    max(FLOPs / MFMA peak, layer-boundary bytes / HBM peak), the decoder on B*T_pad frames x n_ts steps
+    and the vocoder on B*T_y frames, over the measured step time. Also the verdict's useful-frames form:
+    useful mel-frames/s over the bf16 HBM ceiling at T=576 (8e12 / 2,576,864 B = 3.10 M frames/s)."""
+    B, t_y = len(y_lengths), max(y_lengths)
+    dec_frames, voc_frames = B * t_pad, B * t_y
+    flops = dec_frames * n_ts * dec_flops_per_frame_step(t_pad) + voc_frames * VOC_FLOPS_PER_FRAME
+    nbytes = dec_frames * n_ts * DEC_BYTES_PER_FRAME_STEP + voc_frames * VOC_BYTES_PER_FRAME
+    t_roof = max(flops / PEAK_FLOPS, nbytes / PEAK_BW)
+    useful = sum(y_lengths) / sec_per_step
+    ceiling = PEAK_BW / (10 * DEC_BYTES_PER_FRAME_STEP + VOC_BYTES_PER_FRAME)
+    return {"bound": "hbm" if nbytes / PEAK_BW >= flops / PEAK_FLOPS else "mfma",
+            "roof_ms_per_step": round(t_roof * 1e3, 3), "frac": round(t_roof / sec_per_step, 4),
+            "tflops": round(flops / sec_per_step / 1e12, 1), "hbm_gbs": round(nbytes / sec_per_step / 1e9, 1),
+            "padded_frames_per_s": round(voc_frames / sec_per_step, 1),
+            "useful_frames_per_s": round(useful, 1), "ceiling_frames_per_s_T576": round(ceiling, 1),
+            "useful_frac_of_ceiling": round(useful / ceiling, 4), "padding_efficiency": round(sum(y_lengths) / dec_frames, 4),
+            "scope": "hot path (decoder n_ts steps + vocoder); encoder and denoiser excluded as in SURVEY §8d"}
+
+
+def _latest_profile(name):
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", f"r*_{name}")))
+    return files[-1] if files else None
+
+
+def roofline(probe, default_workload=True):
     """Dominant kernel of the step: mt_vconv, the LDS-DMA persistent implicit-GEMM conv that runs every
     ResBlock conv of HiFi-GAN stages 1-3 (54 launches per step: 3 stages x 3 resblocks x 3 pairs x
     2 convs; C = 256/128/64 on B x 8/64/128 * T_y frames, k = 3/7/11). Timed by HIP events recorded on
     its launch stream around each of its launches INSIDE the timed region (mt_probe_*, site
-    PROBE_VCONV). Per launch: algorithmic FLOPs = 2 * C_out * C_in * k * B * L; algorithmic bytes =
-    input + output (+ residual, + accumulator, + activated copy) activations of B * L frames x C
-    channels in bf16, + weights (mt_vconv.hip launch_vconv). The family's intensity decides the bound:
-    below the bf16 ridge (2.5 PFLOP/s / 8 TB/s = 312.5 FLOP/B) it is HBM-bound and `achieved` is
-    algorithmic GB/s, above it MFMA-bound and `achieved` is TFLOP/s. `traffic` = HBM bytes per launch
-    from rocprofv3 FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE on this same bench command
-    (profiles/r01_pmc_vconv.json, tools_round_profile.sh)."""
+    PROBE_VCONV). Per launch (SURVEY.md §8d): algorithmic FLOPs = 2 * C_out * C_in * k * B * L;
+    algorithmic bytes = layer-boundary bytes 2 * B * L * (C_in + C_out) (bf16 input read once, output
+    written once) + weights. The family's intensity decides the bound against the bf16 ridge (2.5 PFLOP/s /
+    8 TB/s = 312.5 FLOP/B). `roof_frac` = the summed per-launch roofline time max(F/P_mfma, B/P_hbm) over
+    the measured time. `traffic` = HBM bytes per launch from rocprofv3 FETCH_SIZE (x2, gfx950 correction)
+    + WRITE_SIZE on this same bench command (profiles/rNN_pmc_vconv.json), `traffic_ratio` = traffic /
+    algorithmic bytes (> 1: bytes this implementation moves beyond the layer boundaries)."""
     if probe is None or probe["launches"] == 0:
-        return {"bound": "hbm", "achieved": None, "peak": 8000.0, "unit": "GB/s", "frac": None,
+        return {"bound": "mfma", "achieved": None, "peak": 2500.0, "unit": "TFLOP/s", "frac": None,
                 "traffic": None, "kernel": "vconv_kernel (bf16 path only)"}
     n = probe["launches"]
     ms = probe["ms"] / n
@@ -130,13 +172,12 @@ def roofline(probe, precision, default_workload=True):
     intensity = flops / nbytes
     tflops = flops / (ms * 1e-3) / 1e12
     gbs = nbytes / (ms * 1e-3) / 1e9
-    peak_f, peak_b = 2500.0, 8000.0  # dense bf16 MFMA TFLOP/s, HBM GB/s (MI355X_MICROARCH.md)
-    ridge = peak_f * 1e12 / (peak_b * 1e9)
-    traffic = None
-    pmc = os.path.join(HERE, "profiles", "r01_pmc_vconv.json")
-    if os.path.exists(pmc) and default_workload:  # the PMC passes ran the default bench workload only
+    peak_f, peak_b = PEAK_FLOPS / 1e12, PEAK_BW / 1e9
+    ridge = PEAK_FLOPS / PEAK_BW
+    traffic, pmc_file = None, _latest_profile("pmc_vconv.json")
+    if pmc_file and default_workload:  # the PMC passes ran the default bench workload only
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            traffic = json.load(open(pmc_file)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     if intensity >= ridge:
@@ -145,38 +186,100 @@ def roofline(probe, precision, default_workload=True):
         bound, achieved, peak, unit = "hbm", gbs, peak_b, "GB/s"
     return {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": traffic,
+            "traffic_ratio": round(traffic / nbytes, 3) if traffic else None,
+            "traffic_source": os.path.relpath(pmc_file, HERE) if traffic else None,
             "kernel": "vconv_kernel<bf16> LDS-DMA implicit-GEMM conv, HiFi-GAN stage 1-3 ResBlock convs",
             "launches": n, "launch_ms": round(ms, 4), "flops_per_launch": flops,
             "algo_bytes_per_launch": nbytes, "intensity_flop_per_byte": round(intensity, 1),
             "tflops": round(tflops, 2), "mfma_frac": round(tflops / peak_f, 4),
-            "gbs": round(gbs, 1), "hbm_frac": round(gbs / peak_b, 4)}
+            "gbs": round(gbs, 1), "hbm_frac": round(gbs / peak_b, 4),
+            "roof_frac": round(probe["roof_ms"] / probe["ms"], 4)}
 
 
-def cpu_baseline(m_sd, g_sd, x, xl, n_ts, seconds):
-    """Oracle (torch CPU restatement, fp32) on a bounded sample of the same workload."""
+def _cpu_info():
+    model, phys = "unknown", set()
+    try:
+        cur = {}
+        vis = os.sched_getaffinity(0)
+        for line in open("/proc/cpuinfo"):
+            if ":" not in line:
+                if cur.get("processor") is not None and int(cur["processor"]) in vis:
+                    phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+                continue
+            k, v = (s.strip() for s in line.split(":", 1))
+            cur[k] = v
+            if k == "model name":
+                model = v
+    except Exception:
+        vis = set(range(os.cpu_count() or 1))
+    return model, len(vis), len(phys) or len(vis)
+
+
+def cpu_baseline(m_sd, g_sd, x, xl, n_ts, n_utt=3):
+    """SURVEY.md §8d CPU baseline: the oracle (fp32 torch CPU restatement of the reference, "port") on a
+    fixed sample of the same workload at batch 1, threads = the physical cores visible to this process
+    (capped by OMP_NUM_THREADS, the box's CPU share), one warm-up pass, then the median of 3 timed passes.
+    Two figures: BASELINE configs[0] exactly (B=1, 4 ODE steps, synthesise + Generator) and the bench's
+    text->wav at n_ts steps with the denoiser."""
     from oracle import matcha_oracle as O
     from hifigan.config import v1
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    model, visible, physical = _cpu_info()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(physical, omp) if omp > 0 else physical
     torch.set_num_threads(threads)
     hp = dict(n_channels=192, n_layers=6, n_heads=2, kernel_size=3, dp_kernel_size=3, n_spks=1)
     sd = {k: v.detach().cpu() for k, v in m_sd.items()}
     gs = {k: v.detach().cpu() for k, v in g_sd.items()}
     bias = O.denoiser_bias_spec(gs, v1)
-    frames, n, t0 = 0, 0, time.perf_counter()
-    with torch.inference_mode():
-        while n < x.shape[0]:
-            xi, li = x[n:n + 1, : int(xl[n])], xl[n:n + 1]
-            mel, yl, _ = O.synthesize(sd, xi, li, n_ts, lambda mu: torch.randn_like(mu) * 0.667, hp)
-            wav = O.generator_forward(gs, mel, v1).clamp(-1, 1)
-            O.denoise(wav.squeeze(1), bias, 0.00025)
-            frames += int(yl.sum())
-            n += 1
-            if time.perf_counter() - t0 > seconds:
-                break
-    dt = time.perf_counter() - t0
-    return {"value": round(frames / dt, 2), "unit": "mel-frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} utterance(s) x {n_ts} ODE steps text->wav (+denoiser), batch 1, fp32, "
-                      f"{frames} frames in {dt:.1f}s"}
+    g = torch.Generator().manual_seed(0)
+
+    def run(steps, denoise):
+        frames, t0 = 0, time.perf_counter()
+        with torch.inference_mode():
+            for n in range(n_utt):
+                xi, li = x[n:n + 1, : int(xl[n])], xl[n:n + 1]
+                mel, yl, _ = O.synthesize(sd, xi, li, steps, lambda mu: torch.randn(mu.shape, generator=g) * 0.667, hp)
+                wav = O.generator_forward(gs, mel, v1).clamp(-1, 1)
+                if denoise:
+                    O.denoise(wav.squeeze(1), bias, 0.00025)
+                frames += int(yl.sum())
+        return frames, time.perf_counter() - t0
+
+    out = {"unit": "mel-frames/s", "cores": threads, "kind": "port", "cpu_model": model,
+           "visible_cpus": visible, "physical_cores_visible": physical}
+    for key, steps, den in (("config1", 4, False), ("bench", n_ts, True)):
+        run(steps, den)  # warm-up
+        res = sorted((run(steps, den) for _ in range(3)), key=lambda r: r[1])
+        frames, dt = res[1]
+        out[key] = {"value": round(frames / dt, 2), "n_timesteps": steps, "denoiser": den,
+                    "median_s": round(dt, 3), "runs_s": [round(r[1], 3) for r in res]}
+    out["value"] = out["bench"]["value"]
+    out["sample"] = (f"{n_utt} utterances of the bench shard at batch 1, fp32, {threads} threads; warm-up + median "
+                     f"of 3. config1 = BASELINE configs[0] (B=1, 4 ODE steps, synthesise + Generator); bench = "
+                     f"{n_ts} ODE steps text->wav + denoiser (the `value`)")
+    return out
+
+
+def north_star(m, g, den, batch, seed, n_ts, denoise, steps=3, warmup=1):
+    """BASELINE north_star target point: B=256 utterances on ONE MI355X, 10-step text->wav, timed in this
+    same run (its own warm-up; barrier-free single GPU)."""
+    x_cpu, xl_cpu = shard_inputs(0, 1, batch, seed)
+    x, xl = x_cpu.to(m.mel_mean.device), xl_cpu.to(m.mel_mean.device)
+    for _ in range(warmup):
+        step(m, g, den, x, xl, n_ts, denoise)
+    _, yl, _ = step(m, g, den, x, xl, n_ts, denoise)
+    yls = [int(v) for v in yl.cpu()]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(m, g, den, x, xl, n_ts, denoise)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    t_pad = 4 * math.ceil(max(yls) / 4)
+    return {"batch": batch, "steps": steps, "warmup": warmup, "ms_per_step": round(el * 1e3, 3),
+            "value": round(sum(yls) / el, 2), "unit": "mel-frames/s", "seq_len": t_pad,
+            "rtf": round(el / (sum(yls) * HOP / SR), 6), "path_roofline": path_roofline(el, yls, t_pad, n_ts)}
 
 
 def main():
@@ -204,6 +307,7 @@ def main():
 
     # useful frames per step on this rank (deterministic durations), outside the timed region
     _, yl, wav = step(m, g, den, x, xl, a.n_timesteps, denoise)
+    yls = [int(v) for v in yl.cpu()]
     frames = int(yl.sum())
     t_y = int(yl.max())
     t_pad = 4 * math.ceil(t_y / 4)
@@ -243,9 +347,12 @@ def main():
     if rank == 0:
         if world == 1:
             default = (a.batch, a.n_timesteps, a.seed, a.no_denoise, a.precision) == (32, 10, 1234, False, "bf16")
-            out["roofline"] = roofline(probe, a.precision, default_workload=default)
+            out["roofline"] = roofline(probe, default_workload=default)
+            out["path_roofline"] = path_roofline(el / a.steps, yls, t_pad, a.n_timesteps)
+            if not a.no_north_star and a.batch != 256 and a.precision == "bf16":
+                out["north_star"] = north_star(m, g, den, 256, a.seed, a.n_timesteps, denoise)
             if not a.no_cpu_baseline:
-                out["cpu_baseline"] = cpu_baseline(msd, gsd, x_cpu, xl_cpu, a.n_timesteps, a.cpu_seconds)
+                out["cpu_baseline"] = cpu_baseline(msd, gsd, x_cpu, xl_cpu, a.n_timesteps, a.cpu_utterances)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

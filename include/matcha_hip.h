@@ -209,15 +209,27 @@ int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, in
  * Launch probe (measurement only; no reference counterpart). Arms HIP events around every
  * launch of one kernel site, on the stream the kernel is launched on, so a benchmark can time
  * that kernel inside its own timed region. Sites: 1 = fused 64-channel HiFi-GAN ResBlock stage,
- * 2 = fused 32-channel stage, 3 = every mt_vconv launch (ResBlock convs of the wide stages). mt_probe_stop synchronizes the recorded events and returns the
- * number of launches, their summed duration and the algorithmic FLOPs / bytes they did.
+ * 2 = fused 32-channel stage, 3 = every mt_vconv launch of the HiFi-GAN ResBlock convs, 4 = the
+ * decoder's k >= 2 mt_vconv launches. mt_probe_stop synchronizes the recorded events and returns the
+ * number of launches, their summed duration, the algorithmic FLOPs and layer-boundary bytes they did
+ * (every conv reads its input once and writes its output once, + its weights), and
+ * roof_ms = sum over launches of max(FLOPs / peak_flops, bytes / peak_bw) (peaks in FLOP/s, B/s).
  * ------------------------------------------------------------------------------------- */
 #define MT_PROBE_RBFUSE_C64 1
 #define MT_PROBE_RBFUSE_C32 2
 #define MT_PROBE_VCONV 3
 #define MT_PROBE_VCONV_DEC 4
 int mt_probe_start(int site, int max_launches);
-int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes);
+int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes, double peak_flops, double peak_bw,
+                  double* roof_ms);
+
+/* Launch log of the persistent LDS-DMA conv (test coverage only; no reference counterpart). While
+ * armed, every mt_vconv launch appends 11 int32: epilogue flags, rows per tile (BM), frames per tile
+ * (BN), 1x1 pipeline flag, output tiles, grid size (tiles > grid: workgroups walk several tiles), taps,
+ * output channels, input channels, utterances, frames per utterance. stop returns the record count. */
+#define MT_VCONV_LOG_FIELDS 11
+int mt_vconv_log_start(int capacity);
+int mt_vconv_log_stop(int32_t* records, int capacity);
 
 #ifdef __cplusplus
 }

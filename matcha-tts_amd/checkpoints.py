@@ -8,20 +8,22 @@
 - HiFi-GAN (main.py:142-150): `{"generator": state_dict}` with weight-norm `weight_g` / `weight_v`
   keys, loaded into the Generator before `remove_weight_norm()`.
 
-Files are read with `torch.load(weights_only=True)` (tensors, containers and primitives only; nothing
+Files are read ONLY with `torch.load(weights_only=True)` (tensors, containers and primitives; nothing
 in the file is executed). A Lightning checkpoint that pickles other objects (callback or
-hyper-parameter classes) is refused by that loader; pass `trusted=True` only for files you trust, to
-load them the way the reference does (`weights_only=False`).
+hyper-parameter classes) is refused by that loader; name those classes in `safe_globals` to allowlist
+them (torch.serialization.safe_globals) — there is deliberately no `weights_only=False` path.
 """
-from typing import Dict
+from typing import Dict, Iterable, Optional
 
 import torch
 
 
-def _load(path_or_obj, map_location, trusted: bool):
+def _load(path_or_obj, map_location, safe_globals: Optional[Iterable] = None):
     if isinstance(path_or_obj, dict):
         return path_or_obj
-    return torch.load(path_or_obj, map_location=map_location, weights_only=not trusted)
+    allow = list(safe_globals or [])
+    with torch.serialization.safe_globals(allow):
+        return torch.load(path_or_obj, map_location=map_location, weights_only=True)
 
 
 def matcha_state_dict(ckpt) -> Dict[str, torch.Tensor]:
@@ -33,16 +35,16 @@ def matcha_state_dict(ckpt) -> Dict[str, torch.Tensor]:
     return out
 
 
-def load_matcha(model: torch.nn.Module, path_or_obj, map_location="cpu", trusted: bool = False):
+def load_matcha(model: torch.nn.Module, path_or_obj, map_location="cpu", safe_globals: Optional[Iterable] = None):
     """Load a Matcha Lightning checkpoint (or bare state dict) into `model` (strict), return the model."""
-    model.load_state_dict(matcha_state_dict(_load(path_or_obj, map_location, trusted)))
+    model.load_state_dict(matcha_state_dict(_load(path_or_obj, map_location, safe_globals)))
     return model
 
 
-def load_hifigan(generator: torch.nn.Module, path_or_obj, map_location="cpu", trusted: bool = False,
-                 remove_weight_norm: bool = True):
+def load_hifigan(generator: torch.nn.Module, path_or_obj, map_location="cpu",
+                 safe_globals: Optional[Iterable] = None, remove_weight_norm: bool = True):
     """main.py:146-149: state["generator"] into the Generator, then fold weight norm (as main.py does)."""
-    state = _load(path_or_obj, map_location, trusted)
+    state = _load(path_or_obj, map_location, safe_globals)
     generator.load_state_dict(state["generator"] if "generator" in state else state)
     if remove_weight_norm:
         generator.remove_weight_norm()

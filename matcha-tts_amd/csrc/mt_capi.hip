@@ -341,8 +341,12 @@ int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, in
 
 int mt_probe_start(int site, int max_launches) { return mt::probe_start(site, max_launches); }
 
-int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes) {
-  return mt::probe_stop(launches, total_ms, flops, bytes);
+int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes, double peak_flops, double peak_bw,
+                  double* roof_ms) {
+  return mt::probe_stop(launches, total_ms, flops, bytes, peak_flops, peak_bw, roof_ms);
 }
+
+int mt_vconv_log_start(int capacity) { return mt::vclog_start(capacity); }
+int mt_vconv_log_stop(int32_t* records, int capacity) { return mt::vclog_stop(records, capacity); }
 
 }  // extern "C"

@@ -509,8 +509,8 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
     a.c0 = c0;
     a.cin = cin;
     a.gn_out = w.gn1;
+    nt1 = a.gn_parts = vconv_gn_parts(B, Tl, C);
     if ((rc = launch_vconv(VE_GNSTATS, a, st))) return rc;
-    nt1 = vconv_gn_parts(B, Tl, C);
   } else {
     ConvArgs a = gemm_args(R.c1, P, B, Tl);
     a.x0 = x0;
@@ -528,8 +528,8 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
     if ((rc = gn_apply(w.y1, B, Tl, C, w.gn1, nt1, g1, g1 + C, 1e-5f, tb, w.tb_ld, mask, w.y2, st))) return rc;
     VConvArgs b = vargs(R.c2, P, w, w.y2, B, Tl, w.y1);
     b.gn_out = w.gn2;
+    nt2 = b.gn_parts = vconv_gn_parts(B, Tl, C);
     if ((rc = launch_vconv(VE_GNSTATS, b, st))) return rc;
-    nt2 = vconv_gn_parts(B, Tl, C);
     yb2 = w.y1;
   } else {
     ConvArgs b = gemm_args(R.c2, P, B, Tl);
@@ -744,8 +744,8 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   if (mio && vc(fconv)) {
     VConvArgs a = vargs(fconv, P, w, w.U, B, T, w.y1);
     a.gn_out = w.gn1;
+    ntf = a.gn_parts = vconv_gn_parts(B, T, C);
     if ((rc = launch_vconv(VE_GNSTATS, a, st))) return rc;
-    ntf = vconv_gn_parts(B, T, C);
   } else {
     ConvArgs a = gemm_args(fconv, P, B, T);
     a.x0 = w.U;

@@ -26,7 +26,9 @@ __global__ __launch_bounds__(256) void mas_kernel(const float* __restrict__ valu
   __shared__ float D[2][MAS_MAXX];
   constexpr int XPT = MAS_MAXX / 256;  // tokens per thread
   const int b = blockIdx.x, tid = threadIdx.x;
-  const int tx = t_xs[b], ty = t_ys[b];
+  // lengths come from mask sums: clamp to the table so a non-binary / oversized mask cannot write
+  // outside this utterance's path, diagonal and output rows
+  const int tx = min(t_xs[b], Tx), ty = min(t_ys[b], Ty);
   const float* v = value + (size_t)b * Tx * Ty;
   float* dg = diag + (size_t)b * (Tx + Ty) * Tx;  // [d][x]
   float* o = out + (size_t)b * Tx * Ty;

@@ -1,5 +1,6 @@
 #include "mt_probe.h"
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -10,6 +11,7 @@ int g_site = PROBE_NONE;
 std::vector<hipEvent_t> g_ev;  // 2 per launch: begin, end
 int g_n = 0, g_cap = 0;
 double g_flops = 0, g_bytes = 0;
+std::vector<double> g_lf, g_lb;  // per launch: algorithmic FLOPs, bytes
 bool g_open = false;
 
 void release() {
@@ -17,6 +19,8 @@ void release() {
   g_ev.clear();
   g_n = g_cap = 0;
   g_flops = g_bytes = 0;
+  g_lf.clear();
+  g_lb.clear();
   g_site = PROBE_NONE;
   g_open = false;
 }
@@ -41,6 +45,8 @@ void probe_end(int site, hipStream_t st, double flops, double bytes) {
   ++g_n;
   g_flops += flops;
   g_bytes += bytes;
+  g_lf.push_back(flops);
+  g_lb.push_back(bytes);
 }
 
 int probe_start(int site, int max_launches) {
@@ -55,9 +61,12 @@ int probe_start(int site, int max_launches) {
   return 0;
 }
 
-int probe_stop(int* launches, double* total_ms, double* flops, double* bytes) {
+int probe_stop(int* launches, double* total_ms, double* flops, double* bytes, double peak_flops, double peak_bw,
+               double* roof_ms) {
   std::lock_guard<std::mutex> lk(g_mu);
-  double ms = 0;
+  double ms = 0, roof = 0;
+  for (int i = 0; i < g_n; ++i)  // per-launch roofline time max(F / peak_F, B / peak_BW)
+    roof += 1e3 * std::max(peak_flops > 0 ? g_lf[i] / peak_flops : 0.0, peak_bw > 0 ? g_lb[i] / peak_bw : 0.0);
   int rc = 0;
   for (int i = 0; i < g_n && rc == 0; ++i) {
     float t = 0.f;
@@ -72,8 +81,42 @@ int probe_stop(int* launches, double* total_ms, double* flops, double* bytes) {
   if (total_ms) *total_ms = ms;
   if (flops) *flops = g_flops;
   if (bytes) *bytes = g_bytes;
+  if (roof_ms) *roof_ms = roof;
   release();
   return rc;
+}
+
+namespace {
+std::vector<int> g_log;
+int g_log_cap = 0;
+bool g_log_on = false;
+}  // namespace
+
+void vclog_record(const int (&rec)[VCLOG_FIELDS]) {
+  if (!g_log_on) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if ((int)g_log.size() >= g_log_cap * VCLOG_FIELDS) return;
+  g_log.insert(g_log.end(), rec, rec + VCLOG_FIELDS);
+}
+
+int vclog_start(int cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  MT_REQUIRE(cap > 0 && cap <= (1 << 20), "vconv log: capacity %d", cap);
+  g_log.clear();
+  g_log.reserve((size_t)cap * VCLOG_FIELDS);
+  g_log_cap = cap;
+  g_log_on = true;
+  return 0;
+}
+
+int vclog_stop(int* out, int cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int n = std::min<int>((int)g_log.size() / VCLOG_FIELDS, cap);
+  if (out)
+    for (int i = 0; i < n * VCLOG_FIELDS; ++i) out[i] = g_log[i];
+  g_log.clear();
+  g_log_on = false;
+  return n;
 }
 
 }  // namespace mt

@@ -18,6 +18,16 @@ bool probe_armed(int site);
 void probe_begin(int site, hipStream_t st);
 void probe_end(int site, hipStream_t st, double flops, double bytes);
 int probe_start(int site, int max_launches);
-int probe_stop(int* launches, double* total_ms, double* flops, double* bytes);
+// roof_ms: sum over launches of max(flops / peak_flops, bytes / peak_bw) in ms (the roofline time)
+int probe_stop(int* launches, double* total_ms, double* flops, double* bytes, double peak_flops, double peak_bw,
+               double* roof_ms);
+
+// Launch log (test coverage only): while armed, every launch_vconv appends the variant it picked and
+// the grid it used, so parity tests can show which instantiations ran and whether workgroups walked
+// more than one tile. Host-only state, off unless vclog_start() armed it.
+constexpr int VCLOG_FIELDS = 11;  // ef, BM, BN, K1, ntiles, grid, taps, M, cin, B, L
+void vclog_record(const int (&rec)[VCLOG_FIELDS]);
+int vclog_start(int cap);
+int vclog_stop(int* out, int cap);  // -> records written (cap records of VCLOG_FIELDS ints)
 
 }  // namespace mt

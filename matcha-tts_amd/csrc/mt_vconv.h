@@ -58,6 +58,8 @@ struct VConvArgs {
   int ylim;
   long long ystride;   // elements per utterance of y
   int mask_div;        // VE_PMASK: output elements per frame
+  int gn_parts;        // VE_GNSTATS: partial slots the consumer will merge (0: unchecked); must equal
+                       // what this launch writes
 };
 
 // partial-sum slots per (utterance, group) that VE_GNSTATS writes: column tiles x waves across columns

@@ -676,9 +676,19 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   const bool half = !k1 && !placed && vconv_tile_frames(a.B, a.L, a.Mpad, ef) == 128;
   if (half) ntiles = (long)a.B * ((a.L + 127) / 128) * (a.Mpad / BM);
   const int G = (int)std::min<long>(ntiles, cu_count());
+  MT_REQUIRE(!(ef & VE_GNSTATS) || a0.gn_parts == 0 ||
+                 a0.gn_parts == ((a.L + (half ? 128 : BN) - 1) / (half ? 128 : BN)) * (8 / (BM / 64)),
+             "vconv: caller expects %d GroupNorm partial slots, the launch writes a different count", a0.gn_parts);
+  {
+    const int bn = k1 ? (small ? 128 : BN) : (BM == 64 ? 384 : half ? 128 : BN);
+    const int rec[VCLOG_FIELDS] = {ef, BM, bn, (int)k1, (int)ntiles, G, a.taps, a.M, a.cin, a.B, a.L};
+    vclog_record(rec);
+  }
   const double flops = 2.0 * a.M * a.cin * a.taps * (double)a.B * a.Lout;
-  const int touts = 1 + ((ef & VE_RESID) ? 1 : 0) + ((ef & VE_ACCUM) ? 1 : 0) + ((ef & VE_DUAL) ? 1 : 0);
-  const double bytes = 2.0 * a.B * ((double)a.L * a.cin + (double)a.Lout * a.M * touts) + 2.0 * a.M * a.cin * a.taps;
+  // algorithmic bytes by SURVEY.md §8d's layer-boundary definition: the conv reads its input once and writes
+  // its output once (bf16), + its weights; the residual / accumulator / activated-copy traffic this
+  // implementation adds is NOT counted (it shows up as the PMC traffic ratio instead)
+  const double bytes = 2.0 * a.B * ((double)a.L * a.cin + (double)a.Lout * a.M) + 2.0 * a.M * a.cin * a.taps;
   // the probe site covers the HiFi-GAN ResBlock convs (k >= 3), the bench's roofline family
   const int site = a.probe ? a.probe : PROBE_VCONV;
   const bool probed = !k1 && site > 0;

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_float, c_int, c_int64, c_size_t, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_void_p
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "libmatcha_hip.so")
@@ -78,7 +78,9 @@ SIGNATURES = {
                             c_int, P, c_size_t, P]),
     "mt_op_attention": (c_int, [c_int, P, P, P, c_int, c_int, c_int, P]),
     "mt_probe_start": (c_int, [c_int, c_int]),
-    "mt_probe_stop": (c_int, [P, P, P, P]),
+    "mt_probe_stop": (c_int, [P, P, P, P, c_double, c_double, P]),
+    "mt_vconv_log_start": (c_int, [c_int]),
+    "mt_vconv_log_stop": (c_int, [P, c_int]),
 }
 
 _lib = None

@@ -525,9 +525,28 @@ def probe_start(site: int, max_launches: int) -> None:
     check(lib().mt_probe_start(int(site), int(max_launches)), "probe_start")
 
 
-def probe_stop() -> Dict[str, float]:
-    """Synchronize the probe's events; launches, summed kernel ms, algorithmic FLOPs and bytes."""
+def probe_stop(peak_flops: float = 2.5e15, peak_bw: float = 8.0e12) -> Dict[str, float]:
+    """Synchronize the probe's events: launches, summed kernel ms, algorithmic FLOPs and layer-boundary
+    bytes, and the summed per-launch roofline time max(F / peak_flops, B / peak_bw) in ms (defaults: the
+    MI355X dense bf16 MFMA and HBM peaks of MI355X_MICROARCH.md)."""
     from ctypes import c_double
-    n, ms, fl, by = c_int(0), c_double(0), c_double(0), c_double(0)
-    check(lib().mt_probe_stop(byref(n), byref(ms), byref(fl), byref(by)), "probe_stop")
-    return {"launches": n.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}
+    n, ms, fl, by, roof = c_int(0), c_double(0), c_double(0), c_double(0), c_double(0)
+    check(lib().mt_probe_stop(byref(n), byref(ms), byref(fl), byref(by), float(peak_flops), float(peak_bw),
+                              byref(roof)), "probe_stop")
+    return {"launches": n.value, "ms": ms.value, "flops": fl.value, "bytes": by.value, "roof_ms": roof.value}
+
+
+VCONV_LOG_FIELDS = ("ef", "bm", "bn", "k1", "ntiles", "grid", "taps", "M", "cin", "B", "L")
+
+
+def vconv_log_start(capacity: int = 65536) -> None:
+    """Record the variant and grid of every mt_vconv launch from now on (test coverage)."""
+    check(lib().mt_vconv_log_start(int(capacity)), "vconv_log_start")
+
+
+def vconv_log_stop(capacity: int = 65536) -> List[Dict[str, int]]:
+    """Disarm the launch log; one dict per launch (fields VCONV_LOG_FIELDS)."""
+    buf = (c_int * (capacity * len(VCONV_LOG_FIELDS)))()
+    n = lib().mt_vconv_log_stop(buf, int(capacity))
+    k = len(VCONV_LOG_FIELDS)
+    return [dict(zip(VCONV_LOG_FIELDS, buf[i * k:(i + 1) * k])) for i in range(n)]

@@ -35,3 +35,23 @@ def test_hifigan_generator_file(tmp_path):
         assert torch.equal(dst.state_dict()[k], v), k
     folded = checkpoints.load_hifigan(make_generator("fp32"), tmp_path / "g_02500000")
     assert not any(k.endswith("weight_g") for k in folded.state_dict())
+
+
+class _HParams:  # stands in for a pickled Lightning hyper-parameter object
+    def __init__(self, lr):
+        self.lr = lr
+
+
+def test_pickled_objects_need_an_allowlist(tmp_path):
+    """Only weights_only=True loading exists: a pickled non-tensor object is refused unless its class
+    is allowlisted (safe_globals); nothing in the file is ever executed."""
+    import pickle
+
+    import pytest
+    sd = make_matcha(1, "fp32").state_dict()
+    path = tmp_path / "with_hparams.ckpt"
+    torch.save({"hyper_parameters": _HParams(1e-4), "state_dict": {"model." + k: v for k, v in sd.items()}}, path)
+    with pytest.raises(pickle.UnpicklingError):
+        checkpoints.load_matcha(make_matcha(1, "fp32"), path)
+    dst = checkpoints.load_matcha(make_matcha(1, "fp32"), path, safe_globals=[_HParams])
+    assert torch.equal(dst.state_dict()["mel_std"], sd["mel_std"])

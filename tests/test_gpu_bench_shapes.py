@@ -1,0 +1,242 @@
+"""Parity at the shapes the bench times (MI355X).
+
+The headline number comes from kernel variants that tiny test shapes never select: mt_vconv picks
+its tile width / pipeline from the problem size and runs a persistent grid of one workgroup per CU,
+so only grids with more tiles than CUs exercise the multi-tile walk (cross-tile prefetch, the
+``nmine >= 2`` loop, the XCD remap). These tests run
+
+  (a) one bf16 estimator evaluation at the bench shape (B=32, T=728) and at B=80 (every k=3
+      GroupNorm conv multi-tile), whole batch against the fp32 oracle;
+  (b) the bf16 Generator at B=8, T=728 (stage-1 convs with 368 tiles, stages 2-3 >1000 tiles);
+  (c) the exact bench step (bf16 text->wav: encoder, 10-step Euler CFM, HiFi-GAN, denoiser) at
+      B=32 and at the north-star batch B=256, rows against the oracle run on those rows at the
+      batch's padded length (rows are independent given T_pad and their z slice);
+  (d) an fp32 10-step CFM solve against the oracle,
+
+and record every mt_vconv launch (variant + grid) so the last test can assert that each variant
+the bench step launches was parity-checked here with a multi-tile grid whenever the bench runs it
+multi-tile. Tolerances: bf16 vs the fp32 oracle by relative RMS 2e-2 (the SURVEY §8c bf16 bar; the
+reference itself under autocast-bf16 is ~3e-3) on the estimator, encoder mu, generator waveform and
+on the bench rows' mel and denoised waveform (measured on MI355X: 1.0e-2, 1.1e-2, 5.5e-3, 5.7e-3 and
+9.6e-3); fp32 CFM atol 2e-4 (SURVEY §8c fp32 mode; measured 3.9e-6).
+Reference: model.py:964-1048, 1084-1109, 1264-1300; hifigan/models.py:181-197;
+hifigan/denoiser.py:62-68.
+"""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, make_decoder, make_generator, rel_rms
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+LOGS = {}  # test name -> vconv launch records
+
+
+def _variant(r):
+    return (r["ef"], r["bm"], r["bn"], r["k1"], r["taps"])
+
+
+def _synth_sd(mod, seed):
+    from matcha_hip import synthetic
+    return {k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(
+        [(k, tuple(v.shape)) for k, v in mod.state_dict().items()], seed).items()}
+
+
+def _bench():
+    if REPO not in sys.path:
+        sys.path.insert(0, REPO)
+    import bench
+    return bench
+
+
+# ------------------------------------------------------------------------------- (a) estimator
+@pytest.mark.parametrize("B", [32, 80])
+def test_decoder_bf16_step_bench_shape_vs_oracle(B):
+    from matcha_hip import runtime as rt
+    from oracle import matcha_oracle as O
+    dec = make_decoder(160, "bf16")
+    sd = _synth_sd(dec, 5)
+    dec.load_state_dict(sd)
+    dec = dec.to(DEV).eval()
+    T = 728
+    rs = np.random.RandomState(B)
+    lens = np.clip(np.round(rs.normal(566, 150, B)), 96, T).astype(np.int64)
+    lens[0] = T  # one unpadded row (the mask quirk inactive there), the rest ragged
+    g = torch.Generator().manual_seed(B)
+    x, mu = torch.randn(B, 80, T, generator=g) * 0.667, torch.randn(B, 80, T, generator=g)
+    mask = (torch.arange(T)[None] < torch.from_numpy(lens)[:, None]).float()[:, None]
+    tt = torch.full((B,), 0.3)
+    rt.vconv_log_start()
+    out = dec(x.to(DEV), mask.to(DEV), (mu * mask).to(DEV), tt.to(DEV)).cpu()
+    torch.cuda.synchronize()
+    LOGS[f"decoder{B}"] = rt.vconv_log_stop()
+    ref = O.decoder_forward(sd, x, mask, mu * mask, tt)
+    err = rel_rms(out, ref)
+    worst = max(rel_rms(out[i], ref[i]) for i in range(B))
+    print(f"decoder B={B} T={T}: rel-RMS {err:.3e}, worst row {worst:.3e}")
+    assert torch.isfinite(out).all()
+    assert err < 2e-2 and worst < 2e-2, (err, worst)
+    gn = [r for r in LOGS[f"decoder{B}"] if r["ef"] & 256]
+    assert {r["bn"] for r in gn} == {128, 256}, "both GroupNorm-conv tile widths must run"
+    if B == 80:
+        assert all(r["ntiles"] > r["grid"] for r in gn), "GroupNorm convs must walk several tiles"
+
+
+@pytest.mark.parametrize("B", [32, 256])
+def test_text_encoder_bf16_bench_batch_vs_oracle(B):
+    """The bench's text batch (x_len ~ U[150,251] with blanks) through the bf16 encoder; at B=256 its
+    FFN convs run multi-tile."""
+    from matcha_hip import runtime as rt
+    from oracle import matcha_oracle as O
+    bench = _bench()
+    m, _, _, msd, _ = bench.build_models(torch.device(DEV), "bf16", 1234)
+    x, xl = bench.shard_inputs(0, 1, B, 1234)
+    rt.vconv_log_start()
+    mu, logw, xm = m.encoder(x.to(DEV), xl.to(DEV))
+    torch.cuda.synchronize()
+    LOGS[f"encoder{B}"] = rt.vconv_log_stop()
+    sd = {k[len("encoder."):]: v.cpu() for k, v in msd.items() if k.startswith("encoder.")}
+    mu_o, logw_o, xm_o = O.text_encoder(sd, x, xl, dict(n_channels=192, n_layers=6, n_heads=2, kernel_size=3,
+                                                        dp_kernel_size=3, n_spks=1))
+    assert torch.equal(xm.cpu(), xm_o) and torch.equal(logw.cpu(), logw_o)
+    err = rel_rms(mu.cpu(), mu_o)
+    print(f"encoder B={B} Tx={x.shape[1]}: mu rel-RMS {err:.3e}")
+    assert err < 2e-2, err
+
+
+# ------------------------------------------------------------------------------- (b) generator
+def test_generator_bf16_bench_length_vs_oracle():
+    from hifigan.config import v1
+    from matcha_hip import runtime as rt
+    from oracle import matcha_oracle as O
+    gen = make_generator("bf16")
+    gen.load_state_dict(_synth_sd(gen, 8))
+    gen = gen.to(DEV).eval()
+    gen.remove_weight_norm()
+    B, T = 8, 728
+    mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(9)) * 2.1 - 5.5
+    rt.vconv_log_start()
+    wav = gen(mel.to(DEV)).cpu()
+    torch.cuda.synchronize()
+    LOGS["generator"] = rt.vconv_log_stop()
+    ref = O.generator_forward({k: v.cpu() for k, v in gen.state_dict().items()}, mel, v1)
+    err = rel_rms(wav, ref)
+    worst = max(rel_rms(wav[i], ref[i]) for i in range(B))
+    print(f"generator B={B} T={T}: rel-RMS {err:.3e}, worst row {worst:.3e}")
+    assert err < 2e-2 and worst < 2e-2, (err, worst)
+    res = [r for r in LOGS["generator"] if not r["k1"] and r["taps"] >= 3]
+    assert len(res) == 54 and all(r["ntiles"] > r["grid"] for r in res), \
+        [(r["M"], r["ntiles"], r["grid"]) for r in res if r["ntiles"] <= r["grid"]]
+
+
+# ------------------------------------------------------------------------------- (c) bench step
+def _bench_rows_vs_oracle(batch, rows, tag):
+    from hifigan.config import v1
+    from matcha_hip import runtime as rt
+    from oracle import matcha_oracle as O
+    bench = _bench()
+    m, g, den, msd, gsd = bench.build_models(torch.device(DEV), "bf16", 1234)
+    x, xl = bench.shard_inputs(0, 1, batch, 1234)
+    real = torch.randn_like
+    zs = []
+
+    def noise(ref, *a, **k):
+        zs.append(real(ref))
+        return zs[-1].clone()
+
+    torch.randn_like = noise
+    try:
+        rt.vconv_log_start()
+        mel, yl, wav = bench.step(m, g, den, x.to(DEV), xl.to(DEV), 10, True)
+        torch.cuda.synchronize()
+        LOGS[tag] = rt.vconv_log_stop()
+    finally:
+        torch.randn_like = real
+    assert len(zs) == 1
+    z = zs[0].cpu() * 0.667
+    yl = yl.cpu()
+    t_y = int(yl.max())
+    t_pad = 4 * math.ceil(t_y / 4)
+    assert z.shape[-1] == t_pad and mel.shape[-1] == t_y
+    rows = sorted(set(r % batch for r in rows) | {int(yl.argmax())})
+    sd = {k: v.detach().cpu() for k, v in msd.items()}
+    hp = dict(n_channels=192, n_layers=6, n_heads=2, kernel_size=3, dp_kernel_size=3, n_spks=1)
+    with torch.inference_mode():
+        mu, logw, x_mask = O.text_encoder(O.sub(sd, "encoder"), x[rows], xl[rows], hp)
+        w_ceil, y_ref = O.durations(logw, x_mask)
+        assert torch.equal(y_ref, yl[rows]), "duration path must be exact (forced duration head)"
+        y_mask = O.sequence_mask(y_ref, t_pad).unsqueeze(1).float()
+        attn = O.generate_path(w_ceil.squeeze(1), (x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)).squeeze(1))
+        mu_y = torch.matmul(attn.transpose(1, 2), mu.transpose(1, 2)).transpose(1, 2)
+        zr = O.cfm_solve(O.sub(sd, "decoder.estimator"), mu_y, y_mask, 10, z[rows])
+        mel_ref = O.denormalize(zr, sd["mel_mean"], sd["mel_std"])[:, :, :t_y]
+        gs = {k: v.detach().cpu() for k, v in gsd.items()}
+        wav_ref = O.generator_forward(gs, mel_ref, v1).clamp(-1, 1)
+        den_ref = O.denoise(wav_ref.squeeze(1), O.denoiser_bias_spec(gs, v1), 0.00025)
+    mean, std = float(sd["mel_mean"]), float(sd["mel_std"])
+    mel_r = mel.cpu()[rows]
+    e_mel = rel_rms((mel_r - mean) / std, (mel_ref - mean) / std)
+    e_wav = rel_rms(wav.cpu()[rows], den_ref)
+    print(f"bench step B={batch} rows {rows}: mel rel-RMS {e_mel:.3e}, denoised wav rel-RMS {e_wav:.3e}")
+    for i, r in enumerate(rows):  # every row inside its useful length, and silence-free
+        n = int(yl[r]) * 256
+        assert rel_rms(wav.cpu()[r, :n], den_ref[i, :n]) < 2e-2
+    assert e_mel < 2e-2 and e_wav < 2e-2, (e_mel, e_wav)
+
+
+def test_bench_step_rows_vs_oracle_b32():
+    """BASELINE configs[1]: the bench's own workload, rows first / middle / last / longest."""
+    _bench_rows_vs_oracle(32, [0, 13, 31], "bench32")
+
+
+def test_bench_step_rows_vs_oracle_b256():
+    """The north-star point (B=256 on one GPU): same check on rows across the whole batch."""
+    _bench_rows_vs_oracle(256, [0, 129, 255], "bench256")
+
+
+# ------------------------------------------------------------------------------- (d) fp32 10 steps
+def test_cfm_fp32_ten_steps_vs_oracle():
+    from oracle import matcha_oracle as O
+    dec = make_decoder(160, "fp32")
+    sd = _synth_sd(dec, 12)
+    dec.load_state_dict(sd)
+    dec = dec.to(DEV).eval()
+    B, T = 3, 240
+    g = torch.Generator().manual_seed(3)
+    mu = torch.randn(B, 80, T, generator=g)
+    mask = (torch.arange(T)[None] < torch.tensor([240, 187, 61])[:, None]).float()[:, None]
+    z = torch.randn(B, 80, T, generator=g)
+    out = dec.engine().solve(dec.packed(DEV), z.to(DEV), 0.667, (mu * mask).to(DEV), mask.to(DEV), None, 10,
+                             "euler").cpu()
+    ref = O.cfm_solve(sd, mu * mask, mask, 10, z * 0.667)
+    err = (out - ref).abs().max().item()
+    print(f"fp32 10-step CFM: max|d| {err:.3e}")
+    assert err < 2e-4, err
+
+
+# ------------------------------------------------------------------------------- coverage
+def test_every_bench_vconv_variant_was_parity_checked():
+    """Each (epilogue, tile rows, tile frames, pipeline, taps) variant the bench step launches ran in
+    a WHOLE-BATCH parity test above (estimator, encoder, generator), with a multi-tile grid whenever
+    the bench runs it multi-tile (the bench steps themselves are only row-checked)."""
+    whole = ("decoder32", "decoder80", "encoder32", "encoder256", "generator")
+    if any(k not in LOGS for k in whole + ("bench32", "bench256")):
+        pytest.skip("needs the whole module's run")
+    checked = {}
+    for k in whole:
+        for r in LOGS[k]:
+            v = _variant(r)
+            checked[v] = checked.get(v, False) or r["ntiles"] > r["grid"]
+    missing, single = [], []
+    for r in LOGS["bench32"] + LOGS["bench256"]:
+        v = _variant(r)
+        if v not in checked:
+            missing.append(v)
+        elif r["ntiles"] > r["grid"] and not checked[v]:
+            single.append(v)
+    assert not missing and not single, (missing, single)
