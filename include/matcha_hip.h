@@ -169,6 +169,17 @@ int mt_denoise(const float* audio, int B, int L, const float* bias_spec, float s
 int mt_stft_magnitude(const float* audio, int B, int L, float* mag, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Log-mel featurizer (§8f rank 4), replacing train_standalone.py:164-201 `mel_spectrogram(y, 1024, 80,
+ * 22050, 256, 1024, fmin, fmax, center=False)` + `normalize(mel, mel_mean, mel_std)` (:204-210,
+ * hifigan/meldataset.py:52-89): reflect pad 384 | STFT 1024/256 Hann, center=False | sqrt(|S|^2 + 1e-9) |
+ * mel_basis . | log(clamp(., 1e-5)) | (. - mel_mean) / mel_std.
+ * audio [B][L] fp32 (L > 384), mel_basis [80][513] fp32 (librosa slaney filters, host-computed) ->
+ * mel [B][80][F] fp32, F = (L - 256) / 256 + 1.
+ * ------------------------------------------------------------------------------------- */
+int mt_log_mel(const float* audio, int B, int L, const float* mel_basis, float mel_mean, float mel_std, float* mel,
+               void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Training-side (§8f rank 3): Monotonic Alignment Search, replacing train_standalone.py:280-325
  * `maximum_path(neg_cent, mask)` (a device->host copy + CPU numba/Python DP in the reference) with
  * its exact recurrence as a GPU anti-diagonal wavefront. neg_cent [B][Tx][Ty] fp32, t_xs / t_ys [B]

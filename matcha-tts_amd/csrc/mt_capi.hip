@@ -14,6 +14,7 @@ int denoise(const float* audio, int B, int L, const float* bias_spec, float stre
             size_t ws_bytes, hipStream_t st);
 size_t denoise_workspace_bytes(int B, int L);
 int stft_magnitude(const float* audio, int B, int L, float* mag, hipStream_t st);
+int log_mel(const float* audio, int B, int L, const float* basis, float mean, float stdv, float* mel, hipStream_t st);
 }  // namespace mt
 
 struct mt_encoder {
@@ -242,6 +243,12 @@ int mt_maximum_path(const float* neg_cent, const int32_t* t_xs, const int32_t* t
 int mt_stft_magnitude(const float* audio, int B, int L, float* mag, void* stream) {
   MT_REQUIRE(audio && mag, "stft_magnitude: null argument");
   return mt::stft_magnitude(audio, B, L, mag, (hipStream_t)stream);
+}
+
+int mt_log_mel(const float* audio, int B, int L, const float* mel_basis, float mel_mean, float mel_std, float* mel,
+               void* stream) {
+  MT_REQUIRE(audio && mel_basis && mel, "log_mel: null argument");
+  return mt::log_mel(audio, B, L, mel_basis, mel_mean, mel_std, mel, (hipStream_t)stream);
 }
 
 // ---- op level ----

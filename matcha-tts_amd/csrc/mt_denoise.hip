@@ -9,37 +9,11 @@
 // Kernel 2: overlap-add of the <= 4 frames covering each output sample / window envelope.
 #include <math.h>
 
-#include "mt_common.h"
+#include "mt_fft.h"
 
 namespace mt {
 
 static constexpr int NFFT = 1024, HOP = 256, NBIN = NFFT / 2 + 1;
-
-__device__ __forceinline__ float hann(int n) {
-  const float s = sinpif((float)n / (float)NFFT);
-  return s * s;
-}
-
-__device__ void fft1024(float* re, float* im, const float* twc, const float* tws, float sign) {
-  // in-place iterative radix-2 on bit-reversed input; twiddle e^{sign*2*pi*i*k/N}
-  for (int h = 1; h < NFFT; h <<= 1) {
-    __syncthreads();
-    for (int bfly = threadIdx.x; bfly < NFFT / 2; bfly += blockDim.x) {
-      const int j = bfly % h;
-      const int base = (bfly / h) * 2 * h + j;
-      const int tw = j * (NFFT / (2 * h));
-      const float c = twc[tw], s = sign * tws[tw];
-      const float ar = re[base], ai = im[base];
-      const float br = re[base + h], bi = im[base + h];
-      const float tr = br * c - bi * s, ti = br * s + bi * c;
-      re[base] = ar + tr;
-      im[base] = ai + ti;
-      re[base + h] = ar - tr;
-      im[base + h] = ai - ti;
-    }
-  }
-  __syncthreads();
-}
 
 __global__ __launch_bounds__(256) void stft_denoise_kernel(const float* __restrict__ audio, int L, int nfr,
                                                            const float* __restrict__ bias, float strength,

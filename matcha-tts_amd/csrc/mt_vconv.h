@@ -20,8 +20,9 @@ enum : int {
   VE_SNAKE = 64, // v + ibeta[m] * sin(v * alpha[m])^2 after the bias (SnakeBeta, model.py:580-609)
   VE_MASK = 128, // v * mask[frame] as the last step (a masked copy for consumers that read x * mask)
   VE_GNSTATS = 256,  // per-(utterance, 32-channel group) partial sum / sum of squares of v (fp64) -> gn_out
-  VE_ROWSTATS = 512, // per frame and 64-channel slab: (sum, sum of squares) of the stored values -> row_out
-                     // (the next LayerNorm's statistics, consumed with VE_LNP)
+  VE_ROWSTATS = 512, // per frame and 64-channel slab: (mean, M2 = sum of squared deviations) of the stored
+                     // values -> row_out (the next LayerNorm's statistics, consumed with VE_LNP; Welford /
+                     // Chan form, no E[x^2] - mean^2 cancellation)
   VE_LNP = 1024,     // with VE_LN: ln_stats holds VE_ROWSTATS partials [frames][cin/64] instead of (mean, rstd)
   VE_RELU = 2048,    // max(v, 0) after the bias (text-encoder FFN, model.py:119-130)
   VE_PMASK = 4096,   // placed output: v * emask[output frame], frame = element / mask_div
@@ -46,7 +47,7 @@ struct VConvArgs {
   const float* snake_ibeta;  // [M] 1 / (exp(beta) + 1e-9)
   const float* emask;        // [B*L] frame mask (VE_MASK)
   double* gn_out;            // [B][M/32][vconv_gn_parts(B, L, M)][2] (VE_GNSTATS)
-  float* row_out;            // [B*L][M/64][2] (VE_ROWSTATS)
+  float* row_out;            // [B*L][M/64][2] (mean, M2) per 64-channel slab (VE_ROWSTATS)
   float ln_eps;              // VE_LNP
   int probe;                 // launch-probe site of k >= 2 launches (0: PROBE_VCONV, < 0: none)
   // Output placement (all 0 = the plain [B][L][M] layout). ConvTranspose1d as a polyphase conv
@@ -61,6 +62,15 @@ struct VConvArgs {
   int gn_parts;        // VE_GNSTATS: partial slots the consumer will merge (0: unchecked); must equal
                        // what this launch writes
 };
+
+// LayerNorm (mean, rstd) of a 256-channel frame from its 4 slab partials (mean_i, M2_i), 64 values each,
+// packed (m0, q0, m1, q1), (m2, q2, m3, q3): Chan's merge, var = M2 / 256
+__device__ __forceinline__ float2 ln_merge4(f32x4 p01, f32x4 p23, float eps) {
+  const float mean = 0.25f * ((p01[0] + p01[2]) + (p23[0] + p23[2]));
+  const float d0 = p01[0] - mean, d1 = p01[2] - mean, d2 = p23[0] - mean, d3 = p23[2] - mean;
+  const float m2 = (p01[1] + p01[3]) + (p23[1] + p23[3]) + 64.f * ((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
+  return float2{mean, rsqrtf(m2 * (1.f / 256.f) + eps)};
+}
 
 // partial-sum slots per (utterance, group) that VE_GNSTATS writes: column tiles x waves across columns
 int vconv_gn_parts(int B, int L, int M);

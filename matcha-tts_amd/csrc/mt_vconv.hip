@@ -234,18 +234,12 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
     double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};  // VE_GNSTATS: this lane's sums per 32-channel group
-    float rsum[FN], rsq[FN];                         // VE_ROWSTATS: this lane's 16 channels of frame fn
+    float rmean[FN], rm2[FN];  // VE_ROWSTATS: Welford (mean, M2) of this lane's 16 channels of frame fn
 #pragma unroll
-    for (int fn = 0; fn < FN; ++fn) rsum[fn] = rsq[fn] = 0.f;
+    for (int fn = 0; fn < FN; ++fn) rmean[fn] = rm2[fn] = 0.f;
     if constexpr ((EF & VE_LNP) != 0) {
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        const float s = (lnr[fn][0][0] + lnr[fn][0][2]) + (lnr[fn][1][0] + lnr[fn][1][2]);
-        const float q = (lnr[fn][0][1] + lnr[fn][0][3]) + (lnr[fn][1][1] + lnr[fn][1][3]);
-        const float mean = s * (1.f / 256.f);
-        const float var = fmaxf(q * (1.f / 256.f) - mean * mean, 0.f);
-        lns[fn] = float2{mean, rsqrtf(var + a.ln_eps)};
-      }
+      for (int fn = 0; fn < FN; ++fn) lns[fn] = ln_merge4(lnr[fn][0], lnr[fn][1], a.ln_eps);
     }
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
@@ -307,10 +301,10 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
             if constexpr ((EF & VE_MASK) != 0) v = v * mk[fn];
             if constexpr ((EF & VE_PMASK) != 0) v = v * pmk;
             const bf16 rb = (bf16)v;
-            if constexpr ((EF & VE_ROWSTATS) != 0) {
-              const float fr = (float)rb;
-              rsum[fn] += fr;
-              rsq[fn] += fr * fr;
+            if constexpr ((EF & VE_ROWSTATS) != 0) {  // Welford over the lane's values (k-th value: 1/k)
+              const float fr = (float)rb, dl = fr - rmean[fn];
+              rmean[fn] += dl * (1.f / (float)(fp * 8 + h * 4 + r + 1));
+              rm2[fn] += dl * (fr - rmean[fn]);
             }
             const bf16 av = (bf16)lrelu_f((float)rb, a.slope);
             ob[r] = (EF & VE_ACT) ? av : rb;
@@ -339,14 +333,19 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       const int ns = a.M >> 6, slab = (m0 >> 6) + wm;
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
-        float s = rsum[fn], q = rsq[fn];
-        s += __shfl_xor(s, 16, 64);
-        q += __shfl_xor(q, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        q += __shfl_xor(q, 32, 64);
+        // Chan's merge of equal-count (16, then 32) groups across the 4 lane rows: the slab's (mean, M2)
+        float mu = rmean[fn], m2 = rm2[fn];
+#pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) {
+          const float mo = __shfl_xor(mu, o, 64), qo = __shfl_xor(m2, o, 64);
+          const float dl = mo - mu;
+          const float nh = (float)(o == 16 ? 16 : 32);  // count of each half
+          m2 = m2 + qo + dl * dl * (nh * 0.5f);
+          mu = 0.5f * (mu + mo);
+        }
         const int n = n0 + wn * WNC + fn * 16 + l16;
         if (g4 == 0 && n < L)
-          *reinterpret_cast<float2*>(a.row_out + 2 * (((size_t)b * L + n) * ns + slab)) = float2{s, q};
+          *reinterpret_cast<float2*>(a.row_out + 2 * (((size_t)b * L + n) * ns + slab)) = float2{mu, m2};
       }
     }
     if constexpr ((EF & VE_GNSTATS) != 0) {

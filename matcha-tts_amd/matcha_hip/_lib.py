@@ -68,6 +68,7 @@ SIGNATURES = {
     "mt_decoder_step_times": (c_int, [P, P, P, P, P, P, P, c_int, c_int, P, P, c_size_t, P]),
     "mt_maximum_path": (c_int, [P, P, P, c_int, c_int, c_int, P, P, c_size_t, P]),
     "mt_stft_magnitude": (c_int, [P, c_int, c_int, P, P]),
+    "mt_log_mel": (c_int, [P, c_int, c_int, P, c_float, c_float, P, P]),
     "mt_op_conv1d_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     "mt_op_conv1d": (c_int, [c_int, P, c_int, c_int, c_int, P, P, c_int, c_int, c_int, c_int, c_int,
                              c_int, c_float, P, c_int, P, c_size_t, P]),

@@ -6,14 +6,14 @@ decoder_params, cfm_params, duration_predictor_params)``, ``.synthesize(...) ->
 (mel, y_lengths, attn)`` (model.py:1264-1300), plus the upstream-style
 ``synthesise(...) -> dict`` used by the notebooks.
 
-What runs where:
-  * text encoder + duration predictor (model.py:148-535): host PyTorch (ROCm), as the
-    north star keeps it (SURVEY.md §2, §8f row 1 = next);
-  * duration -> alignment index path, CFM Euler/midpoint solver over the U-Net
-    estimator, denormalize/crop: hand-written HIP kernels behind the C ABI
-    (include/matcha_hip.h) — ``matcha_hip.runtime``.
-The estimator modules below only hold parameters (reference names/shapes); their
-forward is the HIP kernels. There is no CPU fallback for the HIP parts.
+Everything on the synthesis path runs as hand-written HIP kernels behind the C ABI
+(include/matcha_hip.h, ``matcha_hip.runtime``):
+  * text encoder + duration predictor (model.py:148-535): ``TextEncoder.forward`` is one
+    ``mt_encoder_forward`` call;
+  * duration -> alignment index path, CFM Euler/midpoint solver over the U-Net estimator,
+    denormalize/crop: ``mt_durations``, ``mt_alignment``, ``mt_cfm_solve``, ``mt_denorm_crop``.
+The submodules below only hold parameters under the reference names and shapes (so reference
+checkpoints load unchanged); calling one of them directly raises. There is no CPU fallback.
 """
 from __future__ import annotations
 
@@ -63,11 +63,19 @@ def _get(p, k, default=None):
 
 
 # ======================================================================================
-# text encoder (host PyTorch)  model.py:148-535
+# text encoder parameter containers (state_dict keys of model.py:148-535); TextEncoder.forward is mt_encoder
 # ======================================================================================
 
-class LayerNorm(nn.Module):
-    """Channel LayerNorm over dim 1 of [B,C,T] (model.py:148-166)."""
+class _Params(nn.Module):
+    """Parameter container of a reference submodule; its arithmetic is a HIP kernel of the owning module."""
+
+    def forward(self, *a, **k):
+        raise RuntimeError(f"{type(self).__name__} is evaluated by the HIP path of its owning module "
+                           "(TextEncoder.forward / Decoder.forward); it has no forward of its own")
+
+
+class LayerNorm(_Params):
+    """Channel LayerNorm over dim 1 of [B,C,T] (model.py:148-166): gamma, beta."""
 
     def __init__(self, channels: int, eps: float = 1e-4):
         super().__init__()
@@ -75,14 +83,8 @@ class LayerNorm(nn.Module):
         self.gamma = nn.Parameter(torch.ones(channels))
         self.beta = nn.Parameter(torch.zeros(channels))
 
-    def forward(self, x):
-        mean = x.mean(1, keepdim=True)
-        var = ((x - mean) ** 2).mean(1, keepdim=True)
-        y = (x - mean) * torch.rsqrt(var + self.eps)
-        return y * self.gamma[None, :, None] + self.beta[None, :, None]
 
-
-class ConvReluNorm(nn.Module):
+class ConvReluNorm(_Params):
     """Prenet (model.py:171-208): n x (conv(x*mask) -> LayerNorm -> ReLU), zero-init 1x1 proj, residual."""
 
     def __init__(self, in_channels, hidden_channels, out_channels, kernel_size, n_layers, p_dropout):
@@ -97,14 +99,8 @@ class ConvReluNorm(nn.Module):
         nn.init.zeros_(self.proj.weight)
         nn.init.zeros_(self.proj.bias)
 
-    def forward(self, x, x_mask):
-        h = x
-        for conv, norm in zip(self.conv_layers, self.norm_layers):
-            h = self.relu_drop(norm(conv(h * x_mask)))
-        return (x + self.proj(h)) * x_mask
 
-
-class DurationPredictor(nn.Module):
+class DurationPredictor(_Params):
     """model.py:210-235: conv -> relu -> LayerNorm (x2) -> 1x1 -> log-durations."""
 
     def __init__(self, in_channels, filter_channels, kernel_size, p_dropout):
@@ -116,42 +112,27 @@ class DurationPredictor(nn.Module):
         self.norm_2 = LayerNorm(filter_channels)
         self.proj = nn.Conv1d(filter_channels, 1, 1)
 
-    def forward(self, x, x_mask):
-        h = self.drop(self.norm_1(torch.relu(self.conv_1(x * x_mask))))
-        h = self.drop(self.norm_2(torch.relu(self.conv_2(h * x_mask))))
-        return self.proj(h * x_mask) * x_mask
 
-
-class RotaryPositionalEmebeddings(nn.Module):
-    """RoPE on the first d features of [B,H,T,C] (model.py:244-292; name kept for compatibility)."""
+class RotaryPositionalEmebeddings(_Params):
+    """RoPE on the first d features (model.py:244-292; name kept for compatibility). No parameters: the
+    HIP encoder applies it (rope_kernel) with the theta table of runtime.rope_theta."""
 
     def __init__(self, d, base: int = 10_000):
         super().__init__()
         self.d, self.base = int(d), base
 
-    def forward(self, x):
-        t = x.shape[2]
-        theta = 1.0 / (self.base ** (torch.arange(0, self.d, 2, device=x.device).float() / self.d))
-        ang = torch.outer(torch.arange(t, device=x.device).float(), theta)
-        ang = torch.cat([ang, ang], dim=1)
-        cos, sin = ang.cos()[None, None], ang.sin()[None, None]
-        xr, xp = x[..., : self.d], x[..., self.d:]
-        h = self.d // 2
-        rot = torch.cat([-xr[..., h:], xr[..., :h]], dim=-1)
-        return torch.cat([xr * cos + rot * sin, xp], dim=-1)
 
-
-class MultiHeadAttention(nn.Module):
+class MultiHeadAttention(_Params):
     """RoPE multi-head attention with 1x1-conv projections (model.py:294-372)."""
 
     def __init__(self, channels, out_channels, n_heads, heads_share=True, p_dropout=0.0,
                  proximal_bias=False, proximal_init=False):
         super().__init__()
         assert channels % n_heads == 0, "channels must be divisible by n_heads"
+        if proximal_bias:
+            raise NotImplementedError("proximal_bias is not used by the reference encoder (model.py:437)")
         self.channels, self.n_heads = channels, n_heads
         self.k_channels = channels // n_heads
-        self.proximal_bias = proximal_bias
-        self.attn = None
         self.conv_q = nn.Conv1d(channels, channels, 1)
         self.conv_k = nn.Conv1d(channels, channels, 1)
         self.conv_v = nn.Conv1d(channels, channels, 1)
@@ -167,41 +148,20 @@ class MultiHeadAttention(nn.Module):
                 self.conv_k.bias.copy_(self.conv_q.bias)
         nn.init.xavier_uniform_(self.conv_v.weight)
 
-    def forward(self, x, c, attn_mask=None):
-        q, k, v = self.conv_q(x), self.conv_k(c), self.conv_v(c)
-        b, d, t = k.shape
-        tq = q.shape[2]
 
-        def heads(z, n):
-            return z.view(b, self.n_heads, self.k_channels, n).transpose(2, 3)
+class FFN(_Params):
+    """model.py:375-393: conv(x*mask) -> ReLU -> conv(.*mask) * mask."""
 
-        q, k, v = heads(q, tq), heads(k, t), heads(v, t)
-        q, k = self.query_rotary_pe(q), self.key_rotary_pe(k)
-        s = torch.matmul(q, k.transpose(-2, -1)) / math.sqrt(self.k_channels)
-        if self.proximal_bias:
-            r = torch.arange(t, dtype=torch.float32, device=s.device)
-            s = s + (-torch.log1p(torch.abs(r[None] - r[:, None])))[None, None].to(s.dtype)
-        if attn_mask is not None:
-            s = s.masked_fill(attn_mask == 0, -1e4)
-        p = self.drop(torch.softmax(s, dim=-1))
-        self.attn = p
-        o = torch.matmul(p, v).transpose(2, 3).contiguous().view(b, d, tq)
-        return self.conv_o(o)
-
-
-class FFN(nn.Module):
     def __init__(self, in_channels, out_channels, filter_channels, kernel_size, p_dropout=0.0):
         super().__init__()
         self.conv_1 = nn.Conv1d(in_channels, filter_channels, kernel_size, padding=kernel_size // 2)
         self.conv_2 = nn.Conv1d(filter_channels, out_channels, kernel_size, padding=kernel_size // 2)
         self.drop = nn.Dropout(p_dropout)
 
-    def forward(self, x, x_mask):
-        h = self.drop(torch.relu(self.conv_1(x * x_mask)))
-        return self.conv_2(h * x_mask) * x_mask
 
+class Encoder(_Params):
+    """model.py:396-444: n_layers x (x + MHA -> LayerNorm, x + FFN -> LayerNorm)."""
 
-class Encoder(nn.Module):
     def __init__(self, hidden_channels, filter_channels, n_heads, n_layers, kernel_size=1, p_dropout=0.0):
         super().__init__()
         self.n_layers = n_layers
@@ -214,14 +174,6 @@ class Encoder(nn.Module):
             [FFN(hidden_channels, hidden_channels, filter_channels, kernel_size, p_dropout=p_dropout)
              for _ in range(n_layers)])
         self.norm_layers_2 = nn.ModuleList([LayerNorm(hidden_channels) for _ in range(n_layers)])
-
-    def forward(self, x, x_mask):
-        amask = x_mask.unsqueeze(2) * x_mask.unsqueeze(-1)
-        for attn, n1, ffn, n2 in zip(self.attn_layers, self.norm_layers_1, self.ffn_layers, self.norm_layers_2):
-            x = x * x_mask
-            x = n1(x + self.drop(attn(x, x, amask)))
-            x = n2(x + self.drop(ffn(x, x_mask)))
-        return x * x_mask
 
 
 class TextEncoder(nn.Module):
@@ -244,7 +196,7 @@ class TextEncoder(nn.Module):
             self.prenet = ConvReluNorm(self.n_channels, self.n_channels, self.n_channels, kernel_size=5,
                                        n_layers=3, p_dropout=0.5)
         else:
-            self.prenet = lambda x, x_mask: x
+            self.prenet = None  # no prenet parameters (the HIP encoder skips the stage)
         width = self.n_channels + (spk_emb_dim if n_spks > 1 else 0)
         self.encoder = Encoder(width, _get(encoder_params, "filter_channels"), _get(encoder_params, "n_heads"),
                                _get(encoder_params, "n_layers"), _get(encoder_params, "kernel_size"),
@@ -266,7 +218,7 @@ class TextEncoder(nn.Module):
             self._engines[self.precision] = rt.EncoderEngine(
                 self.n_vocab, self.n_channels, enc.ffn_layers[0].conv_1.out_channels, enc.attn_layers[0].n_heads,
                 enc.n_layers, enc.ffn_layers[0].conv_1.kernel_size[0], self.n_spks, self.spk_emb_dim,
-                self.proj_w.conv_1.out_channels, self.proj_w.conv_1.kernel_size[0], isinstance(self.prenet, nn.Module),
+                self.proj_w.conv_1.out_channels, self.proj_w.conv_1.kernel_size[0], self.prenet is not None,
                 self.precision)
         return self._engines[self.precision]
 
@@ -288,11 +240,6 @@ class TextEncoder(nn.Module):
 # U-Net estimator parameter containers (state_dict keys of model.py:576-962).
 # Their arithmetic is the HIP estimator; they have no torch forward of their own.
 # ======================================================================================
-
-class _Params(nn.Module):
-    def forward(self, *a, **k):
-        raise RuntimeError(f"{type(self).__name__} is evaluated by the HIP estimator (Decoder.forward)")
-
 
 class LoRACompatibleLinear(nn.Linear):
     pass

@@ -499,3 +499,45 @@ def maximum_path(neg_cent: Tensor, mask: Tensor) -> Tensor:
             if y > 0 and index > 0 and p[index - 1, y - 1] > p[index, y - 1]:
                 index -= 1
     return torch.from_numpy(paths)
+
+
+# ---------------------------------------------------------------------------------------------------
+# §8f rank 4: the log-mel featurizer of the training data path, train_standalone.py:164-201 (identical
+# to hifigan/meldataset.py:52-89) and normalize :204-210. librosa (the filterbank's source) is not
+# installed here: `librosa_mel_basis` restates librosa.filters.mel (htk=False, norm="slaney", float32)
+# element by element — parity of the filterbank values is UNPINNED (no librosa output exists in the
+# reference to check against); the STFT / magnitude / log / normalisation are the reference's torch ops.
+# ---------------------------------------------------------------------------------------------------
+def librosa_mel_basis(sr: int, n_fft: int, n_mels: int, fmin: float, fmax: float) -> Tensor:
+    f_sp, min_log_hz = 200.0 / 3, 1000.0
+    min_log_mel, logstep = min_log_hz / f_sp, math.log(6.4) / 27.0
+
+    def hz_to_mel(f):
+        return min_log_mel + math.log(f / min_log_hz) / logstep if f >= min_log_hz else f / f_sp
+
+    def mel_to_hz(m):
+        return min_log_hz * math.exp(logstep * (m - min_log_mel)) if m >= min_log_mel else f_sp * m
+
+    lo, hi = hz_to_mel(float(fmin)), hz_to_mel(float(fmax))
+    edges = [mel_to_hz(lo + (hi - lo) * i / (n_mels + 1)) for i in range(n_mels + 2)]
+    import numpy as np
+    w = np.zeros((n_mels, n_fft // 2 + 1), dtype=np.float32)
+    for m in range(n_mels):
+        for k in range(n_fft // 2 + 1):
+            fk = k * sr / n_fft
+            lower = (fk - edges[m]) / (edges[m + 1] - edges[m])
+            upper = (edges[m + 2] - fk) / (edges[m + 2] - edges[m + 1])
+            w[m, k] = max(0.0, min(lower, upper))
+        w[m] = (w[m].astype(np.float64) * (2.0 / (edges[m + 2] - edges[m]))).astype(np.float32)
+    return torch.from_numpy(w)
+
+
+def mel_spectrogram(y: Tensor, basis: Tensor, n_fft=1024, hop=256, win=1024) -> Tensor:
+    """train_standalone.py:176-201 with the filterbank given: y [B,L] -> log-mel [B,80,F]."""
+    p = (n_fft - hop) // 2
+    y = F.pad(y.unsqueeze(1), (p, p), mode="reflect").squeeze(1)
+    s = torch.view_as_real(torch.stft(y, n_fft, hop_length=hop, win_length=win, window=torch.hann_window(win),
+                                      center=False, pad_mode="reflect", normalized=False, onesided=True,
+                                      return_complex=True))
+    s = torch.sqrt(s.pow(2).sum(-1) + 1e-9)
+    return torch.log(torch.clamp(torch.matmul(basis, s), min=1e-5))

@@ -1,0 +1,74 @@
+"""§8f rank 4: the log-mel featurizer (train_standalone.py:164-210 / hifigan/meldataset.py:52-89).
+
+CPU: the product's Slaney filterbank (hifigan/meldataset.librosa_mel_fn, vectorised) against the oracle's
+element-wise restatement of librosa.filters.mel (parity with librosa itself is UNPINNED: librosa is not
+installed and the reference holds no filterbank or mel output to compare with; the filterbank's
+published properties are checked instead), and the oracle's framing against an independent numpy
+rfft. GPU: the one-launch HIP featurizer against the oracle, atol 1e-4 on log-mel (fp32)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from hifigan.meldataset import librosa_mel_fn, mel_spectrogram
+from oracle import matcha_oracle as O
+
+SR, NFFT, HOP, NMEL, FMIN, FMAX = 22050, 1024, 256, 80, 0.0, 8000.0
+
+
+def test_filterbank_matches_elementwise_restatement():
+    a = librosa_mel_fn(SR, NFFT, NMEL, FMIN, FMAX)
+    b = O.librosa_mel_basis(SR, NFFT, NMEL, FMIN, FMAX).numpy()
+    assert a.shape == (80, 513) and a.dtype == np.float32
+    assert np.abs(a - b).max() <= 2e-9, np.abs(a - b).max()
+
+
+def test_filterbank_properties():
+    """Slaney filters: triangular with unit area in Hz (peak 2 / bandwidth; the 513-bin sampling of a
+    triangle leaves each within 6 %, their mean within 0.1 %), peaks in increasing order, nothing above fmax,
+    one contiguous support per filter."""
+    w = librosa_mel_fn(SR, NFFT, NMEL, FMIN, FMAX).astype(np.float64)
+    df = SR / NFFT
+    area = w.sum(1) * df
+    assert np.all(np.abs(area - 1) < 0.06) and abs(area.mean() - 1) < 1e-3, area
+    peaks = w.argmax(1)
+    assert np.all(np.diff(peaks) >= 0) and peaks[-1] * df < FMAX
+    assert np.all(w[:, int(math.ceil(FMAX / df)) + 1:] == 0)
+    for m in range(NMEL):  # one contiguous non-zero run per filter
+        nz = np.flatnonzero(w[m])
+        assert nz.size and np.all(np.diff(nz) == 1)
+
+
+def test_oracle_framing_matches_numpy_rfft():
+    g = np.random.RandomState(0)
+    y = (g.rand(2, 5000).astype(np.float32) * 2 - 1) * 0.5
+    basis = O.librosa_mel_basis(SR, NFFT, NMEL, FMIN, FMAX)
+    ref = O.mel_spectrogram(torch.from_numpy(y), basis).numpy()
+    p = (NFFT - HOP) // 2
+    yp = np.pad(y.astype(np.float64), ((0, 0), (p, p)), mode="reflect")
+    nfr = (yp.shape[1] - NFFT) // HOP + 1
+    win = np.sin(np.pi * np.arange(NFFT) / NFFT) ** 2
+    frames = np.stack([yp[:, f * HOP:f * HOP + NFFT] * win for f in range(nfr)], axis=-1)  # [B, n, F]
+    spec = np.fft.rfft(frames, axis=1)
+    mag = np.sqrt(np.abs(spec) ** 2 + 1e-9)
+    mine = np.log(np.maximum(np.einsum("mk,bkf->bmf", basis.numpy().astype(np.float64), mag), 1e-5))
+    assert ref.shape == (2, 80, (5000 - 256) // 256 + 1)
+    assert np.abs(ref - mine).max() < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L", [385, 22050 + 123, 3 * 22050])
+def test_hip_log_mel_matches_oracle(L):
+    g = torch.Generator().manual_seed(L)
+    y = (torch.rand(3, L, generator=g) * 2 - 1) * torch.linspace(0.01, 0.9, 3)[:, None]
+    basis = O.librosa_mel_basis(SR, NFFT, NMEL, FMIN, FMAX)
+    ref = O.mel_spectrogram(y, basis)
+    out = mel_spectrogram(y.cuda(), NFFT, NMEL, SR, HOP, 1024, FMIN, FMAX, center=False).cpu()
+    assert out.shape == ref.shape
+    err = (out - ref).abs().max().item()
+    assert err < 1e-4, err
+    # normalisation fused (train_standalone.py:204-210, LJSpeech statistics :802-805)
+    outn = mel_spectrogram(y.cuda(), NFFT, NMEL, SR, HOP, 1024, FMIN, FMAX, mel_mean=-5.536622,
+                           mel_std=2.116101).cpu()
+    assert (outn - (ref + 5.536622) / 2.116101).abs().max().item() < 1e-4
