@@ -192,6 +192,11 @@ int mt_vocoder_set_vconv(mt_vocoder* v, int enable) {
   v->v.vconv = enable < 0 ? 0 : enable;
   return 0;
 }
+int mt_vocoder_set_pair(mt_vocoder* v, int enable) {
+  MT_REQUIRE(v, "null vocoder");
+  v->v.pair = enable ? 1 : 0;
+  return 0;
+}
 size_t mt_vocoder_packed_bytes(const mt_vocoder* v) { return v ? v->v.packed_bytes : 0; }
 int mt_vocoder_pack(const mt_vocoder* v, const float* const* params, void* packed, void* stream) {
   MT_REQUIRE(v && params && packed, "vocoder_pack: null argument");

@@ -13,6 +13,7 @@
 #include "mt_model.h"
 #include "mt_rbfuse.h"
 #include "mt_vconv.h"
+#include "mt_vpair.h"
 
 namespace mt {
 
@@ -220,6 +221,18 @@ bool Vocoder::stage_vc(int i) const {
   return vconv >= 2 || !(fuse && rbfuse_supported(dtype, C));
 }
 
+bool Vocoder::stage_vp(int i) const {
+  if (!pair || vconv < 2 || !stage_vc(i)) return false;
+  const int nk = (int)rb_kernels.size();
+  for (int j = 0; j < nk; ++j)
+    for (size_t q = 0; q < rb1[(size_t)i * nk + j].size(); ++q) {
+      const GemmW& a = rb1[(size_t)i * nk + j][q];
+      const GemmW& b = rb2[(size_t)i * nk + j][q];
+      if (!vpair_supported(a.cout, a.k, a.dil) || b.k != a.k || b.dil != 1) return false;
+    }
+  return true;
+}
+
 bool Vocoder::ups_vc(int i) const {
   return vconv && dtype == BF16 && ups[(size_t)i].vc && (i == 0 || stage_vc(i - 1));
 }
@@ -281,6 +294,48 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
   const int nk = (int)rb_kernels.size();
   const bf16* zero = (const bf16*)(P + zero_off);
   int rc;
+  if (stage_vp(i)) {
+    // one launch per pair; the chain state ping-pongs between R and Tb (a pair reads its input's halo, so it
+    // cannot write in place); activations of the inputs are applied in LDS
+    for (int j = 0; j < nk; ++j) {
+      const std::vector<GemmW>& c1 = rb1[(size_t)i * nk + j];
+      const std::vector<GemmW>& c2 = rb2[(size_t)i * nk + j];
+      const int np = (int)c1.size();
+      const char* state = X;
+      for (int q = 0; q < np; ++q) {
+        const bool last = q == np - 1;
+        VPairArgs a{};
+        a.x = (const bf16*)state;
+        a.B = B;
+        a.L = L;
+        a.w1 = (const bf16*)(P + c1[q].v_off);
+        a.b1 = (const float*)(P + c1[q].b_off);
+        a.w2 = (const bf16*)(P + c2[q].v_off);
+        a.b2 = (const float*)(P + c2[q].b_off);
+        a.taps = c1[q].k;
+        a.dil = c1[q].dil;
+        a.div = (float)nk;
+        a.slope = 0.1f;
+        a.zero = zero;
+        a.trash = (bf16*)trash;
+        int ef = 0;
+        if (!last) {
+          a.y = (bf16*)((q & 1) ? Tb : R);
+        } else {
+          a.y = (bf16*)XS;
+          if (j > 0) ef |= VE_ACCUM;
+          if (j == nk - 1) ef |= VE_DIV;
+          if (j == nk - 1 && act_out) {  // lrelu(xs) for the next upsampler
+            a.y2 = (bf16*)RA;
+            ef |= VE_DUAL;
+          }
+        }
+        if ((rc = launch_vpair(ef, a, st))) return rc;
+        state = (const char*)a.y;
+      }
+    }
+    return 0;
+  }
   for (int j = 0; j < nk; ++j) {
     const std::vector<GemmW>& c1 = rb1[(size_t)i * nk + j];
     const std::vector<GemmW>& c2 = rb2[(size_t)i * nk + j];
@@ -377,14 +432,15 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     if constexpr (std::is_same<E, bf16>::value) {
       const bool svc = stage_vc((int)i);
       if (ups_vc((int)i)) {  // polyphase vconv from lrelu(xs) (RA); + XA = lrelu(X) for a vconv stage
-        if ((rc = ups_vconv(P, (int)i, B, L, RA, X, XA, svc, trash, st))) return rc;
+        if ((rc = ups_vconv(P, (int)i, B, L, RA, X, XA, svc && !stage_vp((int)i), trash, st))) return rc;
         done_up = true;
       }
       if (svc) {
         // X and XA = lrelu(X): the three resblocks' first convs read XA, their residual X
         if (!done_up) {
           u.y2 = XA;
-          if ((rc = launch_conv<E, PF_LRELU, EF_DUAL>(u, st))) return rc;
+          if ((rc = stage_vp((int)i) ? launch_conv<E, PF_LRELU, 0>(u, st) : launch_conv<E, PF_LRELU, EF_DUAL>(u, st)))
+            return rc;
         }
         L = u.Tout;
         const bool act_out = i + 1 < ups.size() && ups_vc((int)i + 1);

@@ -1,0 +1,381 @@
+// Fused HiFi-GAN ResBlock1 PAIR for the 64-channel stage (bf16, gfx950):
+//
+//   t = conv_{k, d}(lrelu(x)) ;  y = conv_{k, 1}(lrelu(t)) + x          (hifigan/models.py:90-97)
+//   (the last pair of resblock j: xs = [xs +] y [/ nk], + lrelu(xs) for the next upsampler, models.py:187-192)
+//
+// One persistent 512-thread workgroup per CU walks tiles of 368 output frames of one utterance. Per tile:
+//   1. the RAW input rows (384 conv1 frames + the conv1 halo, <= 448 rows x 64 channels) land in LDS by
+//      global_load_lds_dwordx4 (issued during the previous tile's second conv); one in-place VALU pass
+//      turns them into lrelu(rows), so no producer has to store an activated copy;
+//   2. conv1: 64 rows x 384 frames (frames n0-8 .. n0+375) over k taps, B = the activated rows shifted by
+//      t*d; epilogue lrelu(round(acc + b1)), zero outside [0, L) (conv2's zero padding) -> T in LDS;
+//   3. conv2: 64 rows x 368 frames over k taps of T; epilogue + b2 + x (residual rows loaded from L2/HBM
+//      at conv1's first step) [+ xs, / nk] -> y (+ lrelu(y)).
+// Waves: 8 along frames (48 frames = 3 fragments each), all 64 rows. Weights stream two taps (16 KiB) per
+// step (48 MFMAs per wave between barriers) through a 3-slot LDS ring; each step's wait covers the next
+// step's weights too, so the next step's first K-slice fragments are read under this step's MFMAs (the mt_vconv pipeline: counted vmcnt, one
+// s_barrier per step, XOR-swizzled 128-byte rows).
+// HBM traffic per pair: x read once (+ halo) and y written once (+ x re-read for the residual, mostly from
+// L2), instead of the per-layer path's x_act read, t written and read back, x read, y and y_act written.
+// Rounding points are the per-layer path's (every stored tensor rounded to bf16, lrelu of the rounded value)
+// and the MFMA accumulation order per output is the same (taps ascending, one 64-channel chunk, two K-slices),
+// so the results are the same bits.
+#include <algorithm>
+
+#include "mt_probe.h"
+#include "mt_vpair.h"
+
+namespace mt {
+
+namespace {
+constexpr int NT = 512, C = 64;
+constexpr int FN = 3;                // 16-frame fragments per wave (8 waves along frames, all 64 rows each)
+constexpr int WNC = 16 * FN;         // frames per wave
+constexpr int NF1 = 8 * WNC;         // conv1 frames per tile: n0 - HALO2 .. n0 - HALO2 + 383
+constexpr int HALO2 = 8;             // >= (k - 1) / 2 of conv2
+constexpr int BN = NF1 - 2 * HALO2;  // output frames per tile (368)
+constexpr int XROWS = NF1 + 64;      // staged input rows >= NF1 + 2 * h1, h1 = d (k - 1) / 2 <= 32
+constexpr int XBUF = XROWS * 128;
+constexpr int TROWS = NF1 + 16;      // conv2's last (discarded) fragment reads up to row NF1 - 1 + 16
+constexpr int TBUF = TROWS * 128;
+constexpr int TAPW = 64 * 128;       // one tap: 64 output rows x 64 input channels
+constexpr int WSLOT = 2 * TAPW;      // a step = two taps (the last step of an odd-k conv uses one)
+constexpr int NWS = 3;
+constexpr int T_OFF = XBUF, W_OFF = T_OFF + TBUF, PAR_OFF = W_OFF + NWS * WSLOT;
+constexpr int LDS_BYTES = PAR_OFF + 2 * C * 4;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+}  // namespace
+
+__device__ __forceinline__ void vp_glds16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ void vp_wait_vmcnt(int n) {
+  if (n < 7) {
+    if (n < 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (n < 4) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else if (n < 15) {
+    if (n < 10) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  } else {
+    if (n < 23) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+    else if (n < 31) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(31)" ::: "memory");
+  }
+}
+
+__device__ __forceinline__ void vp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int EF>
+__global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g4 = lane >> 4, l16 = lane & 15, lrow = lane >> 3, lp = lane & 7;
+  const int k = a.taps, d = a.dil, L = a.L;
+  const int h1 = d * (k - 1) / 2, h2 = (k - 1) / 2;
+  const int ntn = (L + BN - 1) / BN, ntiles = a.B * ntn;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
+  const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
+  if (nmine == 0) return;
+  for (int i = tid; i < C; i += NT) {
+    reinterpret_cast<float*>(smem + PAR_OFF)[i] = a.b1[i];
+    reinterpret_cast<float*>(smem + PAR_OFF)[C + i] = a.b2[i];
+  }
+  __syncthreads();
+
+  int issued = 0, xmk = 0;
+  int wmk[NWS] = {};
+  const int ns = (k + 1) / 2;    // steps per conv
+  const int S = nmine * 2 * ns;  // weight steps of this workgroup
+  auto tile_of = [&](int ti, int& b, int& n0) {
+    const int tile = gl + ti * G;
+    b = tile / ntn;
+    n0 = (tile - b * ntn) * BN;
+  };
+  auto stage_w = [&](int s) {  // taps 2m, 2m+1 (clamped to k-1) of conv1 or conv2, m = step within the conv
+    const int r2 = s % (2 * ns);
+    const int m = r2 < ns ? r2 : r2 - ns;
+    const bf16* w = r2 < ns ? a.w1 : a.w2;
+    const int r = 8 * wave + lrow;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16* base = w + (size_t)min(2 * m + u, k - 1) * C * 64;
+      vp_glds16(base + r * 64 + (lp ^ (r & 6)) * 8, smem + W_OFF + (s % NWS) * WSLOT + u * TAPW + wave * 1024);
+    }
+    issued += 2;
+    wmk[s % NWS] = issued;
+  };
+  auto stage_x = [&](int ti) {  // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r
+    int b, n0;
+    tile_of(ti, b, n0);
+    const bf16* xb = a.x + (size_t)b * L * C;
+    const int f0 = n0 - HALO2 - h1, R1 = NF1 + 2 * h1;
+#pragma unroll
+    for (int i = 0; i < XROWS / 64; ++i) {
+      const int j = wave + 8 * i;
+      const int r = 8 * j + lrow;
+      const int q = lp ^ (r & 6);
+      const int f = f0 + r;
+      const bool ok = r < R1 && f >= 0 && f < L;
+      vp_glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + j * 1024);
+    }
+    issued += XROWS / 64;
+    xmk = issued;
+  };
+
+  auto swap16 = [](uint32_t& x, uint32_t& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+  };
+  auto bf2 = [](uint32_t w, int i) -> float { return __uint_as_float(i ? (w & 0xffff0000u) : (w << 16)); };
+  auto pack2 = [](bf16 lo, bf16 hi) -> uint32_t {
+    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+  };
+  const int ha = l16 & 6;
+
+  f32x4 acc[4][FN];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  struct Frag {
+    bf16x8 A[4], B[FN];
+  };
+  // K-slice ks of tap u of a step: A = the slot's 4 row fragments of that tap, B = FN frame fragments at
+  // rows rb + 16 fn of `src`
+  auto read_frag = [&](Frag& F, int ks, int slot, int u, const char* src, int rb0) {
+    const char* pa = smem + W_OFF + slot * WSLOT + u * TAPW + l16 * 128 + (((ks * 4 + g4) ^ ha) * 16);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048);
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int rb = rb0 + fn * 16;
+      F.B[fn] = *reinterpret_cast<const bf16x8*>(src + rb * 128 + (((ks * 4 + g4) ^ (rb & 6)) * 16));
+    }
+  };
+  // 4 x FN MFMAs of one K-slice with the reads of another slice interleaved, one per MFMA issue slot
+  auto mma_slice = [&](const Frag& F) {
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+    constexpr int NR = 4 + FN, NMF = 4 * FN;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF - NR, 0);
+  };
+  // one conv over `src`: ns steps of two taps (row of tap t for this lane's first fragment: rb0 + t * tstride);
+  // slices in order (tap, K-slice), each read under the previous slice's MFMAs, the next step's first slice
+  // under this step's last
+  Frag F0, F1;
+  int s = 0;
+  auto conv = [&](const char* src, int rb0, int tstride, auto&& at_first_step) {
+    for (int m = 0; m < ns; ++m, ++s) {
+      const bool more = m + 1 < ns, two = 2 * m + 1 < k;
+      vp_wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);  // this step's weights and the next step's
+      vp_barrier();
+      if (s + NWS - 1 < S) stage_w(s + NWS - 1);
+      const int sl = s % NWS, t0 = 2 * m;
+      if (m == 0) {
+        at_first_step();
+        read_frag(F0, 0, sl, 0, src, rb0);
+      }
+      read_frag(F1, 1, sl, 0, src, rb0 + t0 * tstride);
+      mma_slice(F0);
+      if (two) {
+        read_frag(F0, 0, sl, 1, src, rb0 + (t0 + 1) * tstride);
+        mma_slice(F1);
+        read_frag(F1, 1, sl, 1, src, rb0 + (t0 + 1) * tstride);
+        mma_slice(F0);
+      }
+      if (more) read_frag(F0, 0, (s + 1) % NWS, 0, src, rb0 + (t0 + 2) * tstride);
+      mma_slice(F1);
+    }
+  };
+
+  // ---- prologue ----
+  stage_x(0);
+#pragma unroll
+  for (int p = 0; p < NWS - 1; ++p)
+    if (p < S) stage_w(p);
+
+  const float* par = reinterpret_cast<const float*>(smem + PAR_OFF);
+  const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;  // + fp * 32: this lane's 8 channels after the pair swap
+  for (int ti = 0; ti < nmine; ++ti) {
+    int b, n0;
+    tile_of(ti, b, n0);
+    // ---- 1. in-place lrelu of the landed raw rows ----
+    vp_wait_vmcnt(issued - xmk);
+    vp_barrier();
+#pragma unroll
+    for (int i = 0; i < XROWS * 8 / NT; ++i) {
+      const int e = tid + i * NT;
+      u32x4 v = *reinterpret_cast<const u32x4*>(smem + e * 16);
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        v[w] = pack2((bf16)lrelu_f(bf2(v[w], 0), a.slope), (bf16)lrelu_f(bf2(v[w], 1), a.slope));
+      *reinterpret_cast<u32x4*>(smem + e * 16) = v;
+    }
+    // ---- 2. conv1 (published by its first step's barrier) ----
+    zero_acc();
+    u32x4 rv[2][FN], yv[2][FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
+    conv(smem, wave * WNC + l16, d, [&] {
+      // the residual / old-xs rows of this tile's outputs: loaded now, consumed after conv2
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int i = min(n0 + wave * WNC + fn * 16 + l16, L - 1);
+          const size_t o = ((size_t)b * L + i) * C + fp * 32 + ch16;
+          rv[fp][fn] = *reinterpret_cast<const u32x4*>(a.x + o);
+          if constexpr ((EF & VE_ACCUM) != 0) yv[fp][fn] = *reinterpret_cast<const u32x4*>(a.y + o);
+        }
+      issued += 2 * FN * ((EF & VE_ACCUM) ? 2 : 1);
+    });
+    // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - HALO2 + j), zero outside [0, L)
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int j = wave * WNC + fn * 16 + l16;
+        const int f = n0 - HALO2 + j;
+        const bool ok = f >= 0 && f < L;
+        uint32_t o[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int fm = 2 * fp + h;
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + fm * 16 + 4 * g4);
+          bf16 ob[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const bf16 rb = (bf16)(acc[fm][fn][r] + b4[r]);
+            ob[r] = ok ? (bf16)lrelu_f((float)rb, a.slope) : (bf16)0.f;
+          }
+          o[h][0] = pack2(ob[0], ob[1]);
+          o[h][1] = pack2(ob[2], ob[3]);
+        }
+        swap16(o[0][0], o[1][0]);
+        swap16(o[0][1], o[1][1]);
+        const int q = fp * 4 + (g4 & 1) * 2 + (g4 >> 1);
+        *reinterpret_cast<u32x4*>(smem + T_OFF + j * 128 + ((q ^ (j & 6)) * 16)) =
+            u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
+      }
+    // ---- 3. conv2 ----
+    zero_acc();
+    conv(smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, [&] {
+      // every wave is past conv1's reads of the row buffer: stage the next tile's raw rows into it
+      if (ti + 1 < nmine) stage_x(ti + 1);
+    });
+    // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int i = wave * WNC + fn * 16 + l16;  // output frame n0 + i
+        uint32_t rx0 = rv[fp][fn][0], rx1 = rv[fp][fn][1], ry0 = rv[fp][fn][2], ry1 = rv[fp][fn][3];
+        swap16(rx0, ry0);  // back to the accumulator layout
+        swap16(rx1, ry1);
+        uint32_t yx0 = 0, yx1 = 0, yy0 = 0, yy1 = 0;
+        if constexpr ((EF & VE_ACCUM) != 0) {
+          yx0 = yv[fp][fn][0], yx1 = yv[fp][fn][1], yy0 = yv[fp][fn][2], yy1 = yv[fp][fn][3];
+          swap16(yx0, yy0);
+          swap16(yx1, yy1);
+        }
+        uint32_t o1[2][2], o2[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int fm = 2 * fp + h;
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + C + fm * 16 + 4 * g4);
+          const uint32_t rr[2] = {h ? ry0 : rx0, h ? ry1 : rx1};
+          const uint32_t yy[2] = {h ? yy0 : yx0, h ? yy1 : yx1};
+          bf16 ob[4], ab[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[fm][fn][r] + b4[r];
+            v = v + bf2(rr[r >> 1], r & 1);
+            if constexpr ((EF & VE_ACCUM) != 0) v = bf2(yy[r >> 1], r & 1) + v;
+            if constexpr ((EF & VE_DIV) != 0) v = v / a.div;
+            ob[r] = (bf16)v;
+            ab[r] = (bf16)lrelu_f((float)ob[r], a.slope);
+          }
+          o1[h][0] = pack2(ob[0], ob[1]);
+          o1[h][1] = pack2(ob[2], ob[3]);
+          o2[h][0] = pack2(ab[0], ab[1]);
+          o2[h][1] = pack2(ab[2], ab[3]);
+        }
+        swap16(o1[0][0], o1[1][0]);
+        swap16(o1[0][1], o1[1][1]);
+        const bool ok = i < BN && n0 + i < L;
+        const size_t o = ((size_t)b * L + n0 + i) * C + fp * 32 + ch16;
+        *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
+        if constexpr ((EF & VE_DUAL) != 0) {
+          swap16(o2[0][0], o2[1][0]);
+          swap16(o2[0][1], o2[1][1]);
+          *reinterpret_cast<u32x4*>(ok ? a.y2 + o : a.trash + 8 * lane) = u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]};
+        }
+      }
+    issued += 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+  }
+}
+
+bool vpair_supported(int C_, int k, int d) {
+  return C_ == C && k >= 2 && (k - 1) / 2 <= HALO2 && NF1 + d * (k - 1) <= XROWS;
+}
+
+static int vp_cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+int launch_vpair(int ef, const VPairArgs& a, hipStream_t st) {
+  MT_REQUIRE(a.x && a.w1 && a.w2 && a.b1 && a.b2 && a.y && a.zero && a.trash && a.B > 0 && a.L > 0,
+             "vpair: null argument / empty");
+  MT_REQUIRE(vpair_supported(C, a.taps, a.dil) && a.taps % 2 == 1, "vpair: k %d d %d", a.taps, a.dil);
+  MT_REQUIRE(!(ef & VE_DUAL) || a.y2, "vpair: y2");
+  MT_REQUIRE(a.y != a.x, "vpair: y must not alias x (neighbour tiles read x's halo)");
+  const long ntiles = (long)a.B * ((a.L + BN - 1) / BN);
+  const int G = (int)std::min<long>(ntiles, vp_cu_count());
+  // probe: the pair is two of the family's convs (SURVEY §8d algorithmic FLOPs and layer-boundary bytes)
+  const double flops = 2.0 * 2.0 * C * C * a.taps * (double)a.B * a.L;
+  const double bytes = 2.0 * (2.0 * 2.0 * C * (double)a.B * a.L) + 2.0 * 2.0 * C * C * a.taps;
+  probe_begin(PROBE_VCONV, st);
+  switch (ef) {
+    case 0: hipLaunchKernelGGL((vpair_kernel<0>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_ACCUM: hipLaunchKernelGGL((vpair_kernel<VE_ACCUM>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_ACCUM | VE_DIV: hipLaunchKernelGGL((vpair_kernel<VE_ACCUM | VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_ACCUM | VE_DIV | VE_DUAL:
+      hipLaunchKernelGGL((vpair_kernel<VE_ACCUM | VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a);
+      break;
+    case VE_DIV: hipLaunchKernelGGL((vpair_kernel<VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_DIV | VE_DUAL: hipLaunchKernelGGL((vpair_kernel<VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a); break;
+    default: set_error("vpair: epilogue %d not compiled in", ef); return -1;
+  }
+  MT_CHECK_HIP(hipGetLastError());
+  probe_end(PROBE_VCONV, st, flops, bytes);
+  const int rec[VCLOG_FIELDS] = {ef | 0x10000, C, BN, 0, (int)ntiles, G, a.taps, C, C, a.B, a.L};
+  vclog_record(rec);
+  return 0;
+}
+
+}  // namespace mt

@@ -54,6 +54,7 @@ SIGNATURES = {
     "mt_vocoder_packed_bytes": (c_size_t, [P]),
     "mt_vocoder_set_fusion": (c_int, [P, c_int]),
     "mt_vocoder_set_vconv": (c_int, [P, c_int]),
+    "mt_vocoder_set_pair": (c_int, [P, c_int]),
     "mt_decoder_set_vconv": (c_int, [P, c_int]),
     "mt_vocoder_pack": (c_int, [P, POINTER(c_void_p), P, P]),
     "mt_vocoder_workspace_bytes": (c_size_t, [P, c_int, c_int]),

@@ -324,6 +324,10 @@ class VocoderEngine:
     def set_fusion(self, enable: bool) -> None:
         check(lib().mt_vocoder_set_fusion(self.h, int(bool(enable))), "vocoder_set_fusion")
 
+    def set_pair(self, enable) -> None:
+        """bf16: the 64-channel stage's ResBlock pairs fused into one launch each (default) or per layer."""
+        check(lib().mt_vocoder_set_pair(self.h, int(bool(enable))), "vocoder_set_pair")
+
     def set_vconv(self, mode) -> None:
         """0 generic per-layer kernel, 1 vconv for the 128/256-channel stages, 2 (default) also for 64."""
         check(lib().mt_vocoder_set_vconv(self.h, int(mode)), "vocoder_set_vconv")

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""In-process A/B of the bf16 vocoder: mt_vconv wide stages on vs the generic per-layer kernel
-(interleaved rounds, one process, random-data mel). Usage: python tools_voc_ab.py [B] [T] [rounds]"""
+"""In-process A/B of the bf16 vocoder (interleaved rounds, one process, random-data mel). MODES: digits of
+vconv modes (2: per-layer vconv incl. the 64-channel stage, 1: that stage on the fused rbfuse kernel, 0: generic);
+PAIR=1 adds "p" = mode 2 with the 64-channel stage's ResBlock pairs fused (mt_vpair).
+Usage: [MODES=210] [PAIR=1] python tools_voc_ab.py [B] [T] [rounds]"""
 import os
 import sys
 import time
@@ -16,7 +18,7 @@ from matcha_hip import synthetic  # noqa: E402
 if os.environ.get("MT_LIB"):  # timing experiments: another build of the library
     import matcha_hip._lib as _L  # noqa: E402
     _L.LIB_PATH = os.environ["MT_LIB"]
-MODES = tuple(int(c) for c in os.environ.get("MODES", "210"))
+MODES = tuple(int(c) for c in os.environ.get("MODES", "210")) + (("p",) if os.environ.get("PAIR") == "1" else ())
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 728
@@ -31,7 +33,8 @@ eng = g.engine()
 res = {m: [] for m in MODES}
 for r in range(R + 1):
     for on in MODES:
-        eng.set_vconv(on)
+        eng.set_vconv(2 if on == "p" else on)
+        eng.set_pair(on == "p")
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         wav = g(mel)
