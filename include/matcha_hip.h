@@ -195,6 +195,75 @@ int mt_maximum_path(const float* neg_cent, const int32_t* t_xs, const int32_t* t
                     float* paths, void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Training step (§8f rank 3): fp32 primitives the CFM training step (train_standalone.py:623-707,
+ * MatchaLightningModule.forward / training_step / configure_optimizers; model.py:1147-1162 compute_loss)
+ * is built from, forward and backward (matcha_hip/train.py composes them). Activations are [rows][C]
+ * row-major fp32 device buffers. No reduction uses atomics (bitwise reproducible).
+ * ------------------------------------------------------------------------------------- */
+/* C[z] = alpha op(A[z]) op(B[z]) + beta C[z]; op(A) M x K, op(B) K x N; z < batch, strides in elements */
+int mtt_gemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda, long long sA,
+             const float* B, int ldb, long long sB, float beta, float* C, int ldc, long long sC, int batch, void* stream);
+/* conv1d columns: cols[(b*Tout+o)][c*k+tap] = x[b][o*stride-pad+tap*dil][c] (a torch Conv1d weight [Cout][Cin][k]
+ * is then the GEMM operand as stored); col2im is its adjoint */
+int mtt_im2col(const float* x, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* cols,
+               void* stream);
+int mtt_col2im(const float* dcols, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* dx,
+               int accumulate, void* stream);
+/* out[i] (+)= op(a[i], b[((i/d0)%m0)*s0 + ((i/d1)%m1)*s1], c[i]); op: 0 alpha a + beta b, 1 alpha a b,
+ * 2 mish(a), 3 c mish'(a), 4 silu(a), 5 c silu'(a), 6 relu(a), 7 c [a>0], 8 exp(a), 9 (a-b)^2, 10 sin(a),
+ * 11 cos(a), 12 log(alpha + a), 13 alpha / a */
+int mtt_ew(int op, size_t n, const float* a, const float* b, const float* c, float* out, float alpha, float beta,
+           size_t d0, size_t m0, size_t s0, size_t d1, size_t m1, size_t s1, int accumulate, void* stream);
+/* dst[r][doff+j] (+)= src[r][soff+j], r < rows, j < n (channel concat / split; lds, ldd row strides) */
+int mtt_copy_cols(const float* src, int lds, int soff, float* dst, int ldd, int doff, int rows, int n, int accumulate,
+                  void* stream);
+/* sequence_mask (model.py:42-46, train_standalone.py:328-333): out[b][t] = t < lengths[b], fp32 [B][T] */
+int mtt_seq_mask(const int64_t* lengths, int B, int T, float* out, void* stream);
+/* out[s][c] (+)= sum over rows r of segment s (seg rows each) of a[r][c] (* b[r][c]); scratch >=
+ * mtt_colsum_scratch_floats(rows, C, seg) floats */
+size_t mtt_colsum_scratch_floats(int rows, int C, int seg);
+int mtt_colsum(const float* a, const float* b, int rows, int C, int seg, float* out, int accumulate, float* scratch,
+               void* stream);
+/* out[0] = sum_i a[i] (* b[i]); scratch >= 1024 floats */
+int mtt_sum(const float* a, const float* b, size_t n, float* out, float* scratch, void* stream);
+/* dropout(p) with a counter-based hash mask of (seed, index): out = a * keep / (1 - p); the backward is the same
+ * call on the gradient with the same seed */
+int mtt_dropout(const float* a, size_t n, float p, unsigned seed, float* out, void* stream);
+/* torch.nn.GroupNorm over x [B][T][C] (model.py:764-775); backward writes dx and per-(b, c) partials of the
+ * gamma / beta gradients [B][C] (reduce with mtt_colsum) */
+int mtt_groupnorm_fwd(const float* x, const float* gamma, const float* beta, int B, int T, int C, int G, float eps,
+                      float* y, float* mean, float* rstd, void* stream);
+int mtt_groupnorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd, int B,
+                      int T, int C, int G, float* dx, float* dgamma_part, float* dbeta_part, void* stream);
+/* LayerNorm over the C channels of each row (decoder nn.LayerNorm, encoder channel LayerNorm model.py:148-166) */
+int mtt_layernorm_fwd(const float* x, const float* gamma, const float* beta, int rows, int C, float eps, float* y,
+                      float* mean, float* rstd, void* stream);
+int mtt_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
+                      int rows, int C, float* dx, void* stream);
+/* SnakeBeta (model.py:580-609) on [n/C][C]; backward: dx and per-element log-alpha / log-beta gradient terms */
+int mtt_snake_fwd(const float* x, const float* log_alpha, const float* log_beta, size_t n, int C, float* y,
+                  void* stream);
+int mtt_snake_bwd(const float* x, const float* log_alpha, const float* log_beta, const float* dy, size_t n, int C,
+                  float* dx, float* galpha, float* gbeta, void* stream);
+/* row softmax of scale*s [BH][Tq][Tk] with masked keys (kmask [B][Tk] == 0) or masked queries (qmask [B][Tq],
+ * may be NULL) := +3.4e38 (mode 0, decoder model.py:697) or -1e4 (mode 1, encoder model.py:353) */
+int mtt_softmax_fwd(const float* s, const float* kmask, const float* qmask, int BH, int H, int Tq, int Tk, float scale,
+                    int mode, float* p, void* stream);
+int mtt_softmax_bwd(const float* p, const float* dp, const float* kmask, const float* qmask, int BH, int H, int Tq,
+                    int Tk, float scale, float* ds, void* stream);
+/* RoPE in place on x [B][T][H*dh] (first d features of each head), inverse = 1 for the backward */
+int mtt_rope(float* x, int B, int T, int H, int dh, int d, const float* theta, int inverse, void* stream);
+int mtt_embed_fwd(const int64_t* ids, size_t ntok, const float* table, int C, float scale, float* out, void* stream);
+int mtt_embed_bwd(const int64_t* ids, size_t ntok, const float* dout, int V, int C, float scale, float* dtable,
+                  void* stream);
+/* torch.optim.Adam step (lr, betas, eps; no weight decay) with grad scaled by *gscale (clip / world) */
+int mtt_adam(float* p, const float* g, float* m, float* v, size_t n, const float* gscale, float lr, float beta1,
+             float beta2, float eps, int step, void* stream);
+/* clip factor for a flat gradient holding the SUM over `world` ranks: norm = sqrt(*sumsq) * inv_world (the norm of
+ * the DDP-averaged gradient), out = min(1, max_norm / (norm + 1e-6)) * inv_world (torch.nn.utils.clip_grad_norm_) */
+int mtt_clip_factor(const float* sumsq, float max_norm, float inv_world, float* out, float* norm_out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Op-level entry points (per-kernel parity tests)
  * ------------------------------------------------------------------------------------- */
 /* y = conv(act(x)), x [B][Tin][Cin], y [B][Tout][Cout] in dtype; W fp32 reference layout

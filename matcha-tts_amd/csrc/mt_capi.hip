@@ -7,6 +7,7 @@
 #include "mt_model.h"
 #include "mt_vconv.h"
 #include "mt_probe.h"
+#include "mt_train.h"
 
 namespace mt {
 const char* last_error();
@@ -356,6 +357,93 @@ int mt_probe_start(int site, int max_launches) { return mt::probe_start(site, ma
 int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes, double peak_flops, double peak_bw,
                   double* roof_ms) {
   return mt::probe_stop(launches, total_ms, flops, bytes, peak_flops, peak_bw, roof_ms);
+}
+
+// ---- training-step primitives (fp32) ----
+int mtt_gemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda, long long sA,
+             const float* B, int ldb, long long sB, float beta, float* C, int ldc, long long sC, int batch, void* stream) {
+  mt::GemmF32 g{transA, transB, M, N, K, alpha, beta, A, lda, sA, B, ldb, sB, C, ldc, sC, batch};
+  return mt::gemm_f32(g, (hipStream_t)stream);
+}
+int mtt_im2col(const float* x, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* cols,
+               void* stream) {
+  return mt::im2col(x, B, T, C, k, stride, pad, dil, Tout, cols, (hipStream_t)stream);
+}
+int mtt_col2im(const float* dcols, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* dx,
+               int accumulate, void* stream) {
+  return mt::col2im(dcols, B, T, C, k, stride, pad, dil, Tout, dx, accumulate, (hipStream_t)stream);
+}
+int mtt_ew(int op, size_t n, const float* a, const float* b, const float* c, float* out, float alpha, float beta,
+           size_t d0, size_t m0, size_t s0, size_t d1, size_t m1, size_t s1, int accumulate, void* stream) {
+  mt::EwArgs e{op, n, a, b, c, out, alpha, beta, d0, m0, s0, d1, m1, s1, accumulate};
+  return mt::ew(e, (hipStream_t)stream);
+}
+int mtt_copy_cols(const float* src, int lds, int soff, float* dst, int ldd, int doff, int rows, int n, int accumulate,
+                  void* stream) {
+  return mt::copy_cols(src, lds, soff, dst, ldd, doff, rows, n, accumulate, (hipStream_t)stream);
+}
+int mtt_seq_mask(const int64_t* lengths, int B, int T, float* out, void* stream) {
+  return mt::seq_mask((const long long*)lengths, B, T, out, (hipStream_t)stream);
+}
+size_t mtt_colsum_scratch_floats(int rows, int C, int seg) { return mt::colsum_scratch_floats(rows, C, seg); }
+int mtt_colsum(const float* a, const float* b, int rows, int C, int seg, float* out, int accumulate, float* scratch,
+               void* stream) {
+  return mt::colsum(a, b, rows, C, seg, out, accumulate, scratch, (hipStream_t)stream);
+}
+int mtt_sum(const float* a, const float* b, size_t n, float* out, float* scratch, void* stream) {
+  return mt::sum_all(a, b, n, out, scratch, (hipStream_t)stream);
+}
+int mtt_dropout(const float* a, size_t n, float p, unsigned seed, float* out, void* stream) {
+  return mt::dropout(a, n, p, seed, out, (hipStream_t)stream);
+}
+int mtt_groupnorm_fwd(const float* x, const float* gamma, const float* beta, int B, int T, int C, int G, float eps,
+                      float* y, float* mean, float* rstd, void* stream) {
+  return mt::groupnorm_fwd(x, gamma, beta, B, T, C, G, eps, y, mean, rstd, (hipStream_t)stream);
+}
+int mtt_groupnorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd, int B,
+                      int T, int C, int G, float* dx, float* dgamma_part, float* dbeta_part, void* stream) {
+  return mt::groupnorm_bwd(dy, x, gamma, mean, rstd, B, T, C, G, dx, dgamma_part, dbeta_part, (hipStream_t)stream);
+}
+int mtt_layernorm_fwd(const float* x, const float* gamma, const float* beta, int rows, int C, float eps, float* y,
+                      float* mean, float* rstd, void* stream) {
+  return mt::layernorm_fwd(x, gamma, beta, rows, C, eps, y, mean, rstd, (hipStream_t)stream);
+}
+int mtt_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
+                      int rows, int C, float* dx, void* stream) {
+  return mt::layernorm_bwd(dy, x, gamma, mean, rstd, rows, C, dx, (hipStream_t)stream);
+}
+int mtt_snake_fwd(const float* x, const float* log_alpha, const float* log_beta, size_t n, int C, float* y,
+                  void* stream) {
+  return mt::snake_fwd(x, log_alpha, log_beta, n, C, y, (hipStream_t)stream);
+}
+int mtt_snake_bwd(const float* x, const float* log_alpha, const float* log_beta, const float* dy, size_t n, int C,
+                  float* dx, float* galpha, float* gbeta, void* stream) {
+  return mt::snake_bwd(x, log_alpha, log_beta, dy, n, C, dx, galpha, gbeta, (hipStream_t)stream);
+}
+int mtt_softmax_fwd(const float* s, const float* kmask, const float* qmask, int BH, int H, int Tq, int Tk, float scale,
+                    int mode, float* p, void* stream) {
+  return mt::softmax_fwd(s, kmask, qmask, BH, H, Tq, Tk, scale, mode, p, (hipStream_t)stream);
+}
+int mtt_softmax_bwd(const float* p, const float* dp, const float* kmask, const float* qmask, int BH, int H, int Tq,
+                    int Tk, float scale, float* ds, void* stream) {
+  return mt::softmax_bwd(p, dp, kmask, qmask, BH, H, Tq, Tk, scale, ds, (hipStream_t)stream);
+}
+int mtt_rope(float* x, int B, int T, int H, int dh, int d, const float* theta, int inverse, void* stream) {
+  return mt::rope(x, B, T, H, dh, d, theta, inverse, (hipStream_t)stream);
+}
+int mtt_embed_fwd(const int64_t* ids, size_t ntok, const float* table, int C, float scale, float* out, void* stream) {
+  return mt::embed_fwd((const long long*)ids, ntok, table, C, scale, out, (hipStream_t)stream);
+}
+int mtt_embed_bwd(const int64_t* ids, size_t ntok, const float* dout, int V, int C, float scale, float* dtable,
+                  void* stream) {
+  return mt::embed_bwd((const long long*)ids, ntok, dout, V, C, scale, dtable, (hipStream_t)stream);
+}
+int mtt_adam(float* p, const float* g, float* m, float* v, size_t n, const float* gscale, float lr, float beta1,
+             float beta2, float eps, int step, void* stream) {
+  return mt::adam_step(p, g, m, v, n, gscale, lr, beta1, beta2, eps, step, (hipStream_t)stream);
+}
+int mtt_clip_factor(const float* sumsq, float max_norm, float inv_world, float* out, float* norm_out, void* stream) {
+  return mt::clip_factor(sumsq, max_norm, inv_world, out, norm_out, (hipStream_t)stream);
 }
 
 int mt_vconv_log_start(int capacity) { return mt::vclog_start(capacity); }

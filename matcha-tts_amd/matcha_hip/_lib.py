@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_uint, c_void_p
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "libmatcha_hip.so")
@@ -81,6 +81,31 @@ SIGNATURES = {
     "mt_op_attention": (c_int, [c_int, P, P, P, c_int, c_int, c_int, P]),
     "mt_probe_start": (c_int, [c_int, c_int]),
     "mt_probe_stop": (c_int, [P, P, P, P, c_double, c_double, P]),
+    "mtt_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_float, P, c_int, c_int64, P, c_int, c_int64, c_float,
+                         P, c_int, c_int64, c_int, P]),
+    "mtt_im2col": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "mtt_col2im": (c_int, [P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, P]),
+    "mtt_ew": (c_int, [c_int, c_size_t, P, P, P, P, c_float, c_float, c_size_t, c_size_t, c_size_t, c_size_t,
+                       c_size_t, c_size_t, c_int, P]),
+    "mtt_copy_cols": (c_int, [P, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "mtt_seq_mask": (c_int, [P, c_int, c_int, P, P]),
+    "mtt_colsum_scratch_floats": (c_size_t, [c_int, c_int, c_int]),
+    "mtt_colsum": (c_int, [P, P, c_int, c_int, c_int, P, c_int, P, P]),
+    "mtt_sum": (c_int, [P, P, c_size_t, P, P, P]),
+    "mtt_dropout": (c_int, [P, c_size_t, c_float, c_uint, P, P]),
+    "mtt_groupnorm_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_float, P, P, P, P]),
+    "mtt_groupnorm_bwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, P]),
+    "mtt_layernorm_fwd": (c_int, [P, P, P, c_int, c_int, c_float, P, P, P, P]),
+    "mtt_layernorm_bwd": (c_int, [P, P, P, P, P, c_int, c_int, P, P]),
+    "mtt_snake_fwd": (c_int, [P, P, P, c_size_t, c_int, P, P]),
+    "mtt_snake_bwd": (c_int, [P, P, P, P, c_size_t, c_int, P, P, P, P]),
+    "mtt_softmax_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_float, c_int, P, P]),
+    "mtt_softmax_bwd": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, P, P]),
+    "mtt_rope": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, c_int, P]),
+    "mtt_embed_fwd": (c_int, [P, c_size_t, P, c_int, c_float, P, P]),
+    "mtt_embed_bwd": (c_int, [P, c_size_t, P, c_int, c_int, c_float, P, P]),
+    "mtt_adam": (c_int, [P, P, P, P, c_size_t, P, c_float, c_float, c_float, c_float, c_int, P]),
+    "mtt_clip_factor": (c_int, [P, c_float, c_float, P, P, P]),
     "mt_vconv_log_start": (c_int, [c_int]),
     "mt_vconv_log_stop": (c_int, [P, c_int]),
 }

@@ -165,6 +165,7 @@ def text_encoder(sd: SD, x: Tensor, x_lengths: Tensor, hp, spks: Optional[Tensor
     h = h * x_mask
     mu = _conv(h, sub(sd, "proj_m")) * x_mask
     dk = hp["dp_kernel_size"]
+    h = h.detach()  # model.py:532 — the duration predictor reads a detached copy (matters for autograd only)
     d = _conv(h * x_mask, sub(sd, "proj_w.conv_1"), pad=dk // 2)
     d = channel_layernorm(torch.relu(d), sub(sd, "proj_w.norm_1"))
     d = _conv(d * x_mask, sub(sd, "proj_w.conv_2"), pad=dk // 2)
@@ -499,6 +500,38 @@ def maximum_path(neg_cent: Tensor, mask: Tensor) -> Tensor:
             if y > 0 and index > 0 and p[index - 1, y - 1] > p[index, y - 1]:
                 index -= 1
     return torch.from_numpy(paths)
+
+
+def training_losses(sd: SD, x: Tensor, x_lengths: Tensor, y: Tensor, y_lengths: Tensor, t: Tensor, z: Tensor, hp,
+                    sigma_min: float = 1e-4, heads: int = 2):
+    """train_standalone.py:623-667 (MatchaLightningModule.forward, single speaker, prior_loss on) with
+    CFM.compute_loss model.py:1147-1162, duration_loss :79-81; dropout off (eval-mode modules), the noise
+    t [B] ~ rand and z ~ randn_like(y) passed in. sd: full model state dict ("encoder.*",
+    "decoder.estimator.*"). Differentiable w.r.t. sd's tensors (torch autograd = the gradient oracle).
+    Returns (dur_loss, prior_loss, cfm_loss, attn [B,Tx,Ty], log_prior [B,Tx,Ty])."""
+    n_feats = y.shape[1]
+    mu_x, logw, x_mask = text_encoder(sub(sd, "encoder"), x, x_lengths, hp)
+    y_mask = sequence_mask(y_lengths, y.shape[-1]).unsqueeze(1).to(x_mask)
+    attn_mask = x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)
+    with torch.no_grad():  # :638-647
+        const = -0.5 * math.log(2 * math.pi) * n_feats
+        factor = -0.5 * torch.ones(mu_x.shape, dtype=mu_x.dtype, device=mu_x.device)
+        y_square = torch.matmul(factor.transpose(1, 2), y ** 2)
+        y_mu_double = torch.matmul(2.0 * (factor * mu_x).transpose(1, 2), y)
+        mu_square = torch.sum(factor * (mu_x ** 2), 1).unsqueeze(-1)
+        log_prior = y_square - y_mu_double + mu_square + const
+        attn = maximum_path(log_prior, attn_mask.squeeze(1)).to(y.device)
+    logw_ = torch.log(1e-8 + torch.sum(attn.unsqueeze(1), -1)) * x_mask  # :650-651
+    dur_loss = torch.sum((logw - logw_) ** 2) / torch.sum(x_lengths)
+    mu_y = torch.matmul(attn.transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)  # :654-655
+    tt = t.view(-1, 1, 1)
+    y_t = (1 - (1 - sigma_min) * tt) * z + tt * y  # model.py:1150-1162
+    u_t = y - (1 - sigma_min) * z
+    pred = decoder_forward(sub(sd, "decoder.estimator"), y_t, y_mask, mu_y, t, heads=heads)
+    cfm_loss = F.mse_loss(pred, u_t, reduction="sum") / (torch.sum(y_mask) * u_t.shape[1])
+    prior_loss = torch.sum(0.5 * ((y - mu_y) ** 2 + math.log(2 * math.pi)) * y_mask)  # :661-663
+    prior_loss = prior_loss / (torch.sum(y_mask) * n_feats)
+    return dur_loss, prior_loss, cfm_loss, attn, log_prior
 
 
 # ---------------------------------------------------------------------------------------------------

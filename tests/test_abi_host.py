@@ -13,7 +13,7 @@ from conftest import REPO, make_decoder, make_generator, make_matcha
 def header_functions():
     src = open(os.path.join(REPO, "include", "matcha_hip.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(mt_\w+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(mtt?_\w+)\s*\(", src)))
 
 
 def test_library_exports_every_header_symbol():

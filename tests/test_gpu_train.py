@@ -1,0 +1,336 @@
+"""§8f rank 3, the CFM training step on the GPU (matcha_hip.train) against torch autograd through the oracle
+(oracle/matcha_oracle.py: training_losses restates train_standalone.py:623-667 in plain torch, so autograd
+on it is the gradient oracle). Per-primitive forward/backward checks first (conv / transposed conv via
+im2col + exact-fp32 MFMA GEMM, GroupNorm, LayerNorm, SnakeBeta, masked softmax in both reference mask modes,
+RoPE, embedding, dropout, Adam + clip), then the whole step: losses, the MAS path, every parameter's
+gradient and the Adam update. fp32 throughout; tolerances are stated per test."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import HP, make_matcha, rel_rms
+from matcha_hip import synthetic
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _tr():
+    from matcha_hip import train
+    return train
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+# ----------------------------------------------------------------------------------------- primitives
+@pytest.mark.parametrize("ta,tb,M,N,K,batch", [(0, 0, 70, 33, 19, 1), (1, 0, 64, 64, 100, 3), (0, 1, 5, 130, 64, 2),
+                                               (1, 1, 17, 9, 3, 1)])
+def test_gemm_f32(ta, tb, M, N, K, batch):
+    tr = _tr()
+    g = torch.Generator().manual_seed(M * N + K)
+    A = torch.randn(batch, *((K, M) if ta else (M, K)), generator=g)
+    B = torch.randn(batch, *((N, K) if tb else (K, N)), generator=g)
+    C0 = torch.randn(batch, M, N, generator=g)
+    out = C0.clone().to(DEV)
+    tr.gemm(A.to(DEV), B.to(DEV), M, N, K, out, ta=ta, tb=tb, alpha=0.5, beta=-1.0, batch=batch,
+            sA=A[0].numel(), sB=B[0].numel(), sC=M * N)
+    Ad = A.double().transpose(1, 2) if ta else A.double()
+    Bd = B.double().transpose(1, 2) if tb else B.double()
+    ref = 0.5 * Ad @ Bd - C0.double()
+    assert _rel(out, ref) < 2e-6
+
+
+@pytest.mark.parametrize("k,stride,pad,dil", [(3, 1, 1, 1), (3, 2, 1, 1), (5, 1, 2, 1), (3, 1, 2, 2), (1, 1, 0, 1)])
+def test_conv_fwd_bwd(k, stride, pad, dil):
+    tr = _tr()
+    g = torch.Generator().manual_seed(k * 10 + stride)
+    B, T, Cin, Cout = 2, 37, 24, 40
+    x = torch.randn(B, T, Cin, generator=g, requires_grad=True)
+    W = torch.randn(Cout, Cin, k, generator=g, requires_grad=True)
+    b = torch.randn(Cout, generator=g, requires_grad=True)
+    y = F.conv1d(x.transpose(1, 2), W, b, stride=stride, padding=pad, dilation=dil).transpose(1, 2)
+    dy = torch.randn(y.shape, generator=g)
+    gx, gW, gb = torch.autograd.grad(y, (x, W, b), dy)
+    yd, ctx = tr.conv_fwd(x.detach().to(DEV).contiguous(), W.detach().to(DEV), b.detach().to(DEV), stride, pad, dil)
+    gWd, gbd = torch.empty_like(W, device=DEV), torch.empty_like(b, device=DEV)
+    gxd = tr.conv_bwd(dy.to(DEV).contiguous(), ctx, W.detach().to(DEV), gWd, gbd)
+    assert _rel(yd, y) < 1e-6 and _rel(gxd, gx) < 1e-6 and _rel(gWd, gW) < 1e-6 and _rel(gbd, gb) < 1e-6
+
+
+def test_conv_transpose_fwd_bwd():
+    tr = _tr()
+    g = torch.Generator().manual_seed(5)
+    B, Tin, Cin, Cout = 2, 19, 32, 24
+    x = torch.randn(B, Tin, Cin, generator=g, requires_grad=True)
+    W = torch.randn(Cin, Cout, 4, generator=g, requires_grad=True)
+    b = torch.randn(Cout, generator=g, requires_grad=True)
+    y = F.conv_transpose1d(x.transpose(1, 2), W, b, stride=2, padding=1).transpose(1, 2)
+    dy = torch.randn(y.shape, generator=g)
+    gx, gW, gb = torch.autograd.grad(y, (x, W, b), dy)
+    yd, ctx = tr.convT_fwd(x.detach().to(DEV).contiguous(), W.detach().to(DEV), b.detach().to(DEV), 2, 1)
+    gWd, gbd = torch.empty_like(W, device=DEV), torch.empty_like(b, device=DEV)
+    gxd = tr.convT_bwd(dy.to(DEV).contiguous(), ctx, W.detach().to(DEV), gWd, gbd)
+    assert yd.shape == y.shape
+    assert _rel(yd, y) < 1e-6 and _rel(gxd, gx) < 1e-6 and _rel(gWd, gW) < 1e-6 and _rel(gbd, gb) < 1e-6
+
+
+def test_groupnorm_layernorm_fwd_bwd():
+    tr = _tr()
+    g = torch.Generator().manual_seed(6)
+    B, T, C = 3, 29, 64
+    x = (torch.randn(B, T, C, generator=g) * 3 + 1).requires_grad_(True)
+    gam = torch.randn(C, generator=g, requires_grad=True)
+    bet = torch.randn(C, generator=g, requires_grad=True)
+    dy = torch.randn(B, T, C, generator=g)
+    y = F.group_norm(x.transpose(1, 2), 8, gam, bet, eps=1e-5).transpose(1, 2)
+    ref = torch.autograd.grad(y, (x, gam, bet), dy)
+    yd, ctx = tr.gn_fwd(x.detach().to(DEV).contiguous(), gam.detach().to(DEV), bet.detach().to(DEV))
+    gg, gb = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    dx = tr.gn_bwd(dy.to(DEV).contiguous(), ctx, gam.detach().to(DEV), gg, gb)
+    assert _rel(yd, y) < 1e-6
+    for a, b in zip((dx, gg, gb), ref):
+        assert _rel(a, b) < 1e-5
+    for eps in (1e-5, 1e-4):
+        y = F.layer_norm(x, (C,), gam, bet, eps=eps)
+        ref = torch.autograd.grad(y, (x, gam, bet), dy)
+        yd, ctx = tr.ln_fwd(x.detach().to(DEV).contiguous(), gam.detach().to(DEV), bet.detach().to(DEV), eps)
+        dx = tr.ln_bwd(dy.to(DEV).contiguous(), ctx, gam.detach().to(DEV), gg, gb)
+        assert _rel(yd, y) < 1e-6
+        for a, b in zip((dx, gg, gb), ref):
+            assert _rel(a, b) < 1e-5
+
+
+def test_snake_mish_silu_relu_bwd():
+    tr = _tr()
+    g = torch.Generator().manual_seed(7)
+    x = (torch.randn(50, 96, generator=g) * 2).requires_grad_(True)
+    la = (torch.randn(96, generator=g) * 0.3).requires_grad_(True)
+    lb = (torch.randn(96, generator=g) * 0.3).requires_grad_(True)
+    dy = torch.randn(50, 96, generator=g)
+    y = x + 1.0 / (torch.exp(lb) + 1e-9) * torch.sin(x * torch.exp(la)) ** 2  # model.py:600-609
+    ref = torch.autograd.grad(y, (x, la, lb), dy)
+    xd = x.detach().to(DEV).contiguous()
+    dx, ga, gb = torch.empty_like(xd), torch.empty_like(xd), torch.empty_like(xd)
+    yd = torch.empty_like(xd)
+    L = tr.lib()
+    tr.check(L.mtt_snake_fwd(xd.data_ptr(), la.detach().to(DEV).data_ptr(), lb.detach().to(DEV).data_ptr(), xd.numel(),
+                             96, yd.data_ptr(), tr._s(xd)))
+    la_d, lb_d = la.detach().to(DEV), lb.detach().to(DEV)
+    tr.check(L.mtt_snake_bwd(xd.data_ptr(), la_d.data_ptr(), lb_d.data_ptr(), dy.to(DEV).data_ptr(), xd.numel(), 96,
+                             dx.data_ptr(), ga.data_ptr(), gb.data_ptr(), tr._s(xd)))
+    assert _rel(yd, y) < 1e-6 and _rel(dx, ref[0]) < 1e-5
+    assert _rel(ga.sum(0), ref[1]) < 1e-5 and _rel(gb.sum(0), ref[2]) < 1e-5
+    for op, opb, fn in ((tr.MISH, tr.MISH_B, lambda v: v * torch.tanh(F.softplus(v))), (tr.SILU, tr.SILU_B, F.silu),
+                        (tr.RELU, tr.RELU_B, torch.relu)):
+        y = fn(x)
+        (gx,) = torch.autograd.grad(y, (x,), dy)
+        assert _rel(tr.act(op, xd), y) < 1e-6
+        assert _rel(tr.act_bwd(opb, xd, dy.to(DEV).contiguous()), gx) < 1e-5
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_masked_attention_fwd_bwd(mode):
+    """mode 0: decoder key mask filled with -finfo.min = +3.4e38 (model.py:697, padded queries and keys attend
+    uniformly to the padded keys); mode 1: encoder query x key mask filled with -1e4 (model.py:360) plus dropout
+    off. Reference math in fp64 autograd."""
+    tr = _tr()
+    g = torch.Generator().manual_seed(8 + mode)
+    B, T, H, dh = 3, 21, 2, 16
+    lens = torch.tensor([21, 15, 8])
+    m = (torch.arange(T)[None] < lens[:, None]).float()
+    q, k, v = (torch.randn(B, T, H * dh, generator=g, dtype=torch.float64, requires_grad=True) for _ in range(3))
+    scale = dh ** -0.5
+
+    def heads(z):
+        return z.view(B, T, H, dh).permute(0, 2, 1, 3)
+
+    s = torch.einsum("bhid,bhjd->bhij", heads(q), heads(k)) * scale
+    if mode == 0:
+        s = s.masked_fill(m[:, None, None, :] == 0, 3.4028234663852886e38)
+    else:
+        s = s.masked_fill((m[:, None, :, None] * m[:, None, None, :]) == 0, -1e4)
+    o = torch.einsum("bhij,bhjd->bhid", s.softmax(-1), heads(v)).permute(0, 2, 1, 3).reshape(B, T, H * dh)
+    do = torch.randn(o.shape, generator=g, dtype=torch.float64)
+    ref = torch.autograd.grad(o, (q, k, v), do)
+    md = m.to(DEV)
+    od, ctx = tr.attention_fwd(*(z.detach().float().to(DEV).contiguous() for z in (q, k, v)), md,
+                               md if mode == 1 else None, H, dh, scale, mode)
+    grads = tr.attention_bwd(do.float().to(DEV).contiguous(), ctx)
+    assert _rel(od, o) < 1e-5
+    for a, b in zip(grads, ref):
+        assert _rel(a, b) < 1e-4
+
+
+def test_rope_and_inverse():
+    import oracle.matcha_oracle as O
+    tr = _tr()
+    from matcha_hip import runtime as rt
+    g = torch.Generator().manual_seed(9)
+    B, T, H, dh = 2, 13, 2, 96
+    x = torch.randn(B, T, H * dh, generator=g)
+    d = int(dh * 0.5)
+    ref = O.rope(x.view(B, T, H, dh).permute(0, 2, 1, 3), d).permute(0, 2, 1, 3).reshape(B, T, H * dh)
+    xd = x.to(DEV).contiguous()
+    theta = rt.rope_theta(dh).to(DEV)
+    tr.rope_(xd, H, dh, d, theta)
+    assert _rel(xd, ref) < 1e-6
+    tr.rope_(xd, H, dh, d, theta, inverse=True)
+    assert _rel(xd, x) < 1e-6
+
+
+def test_embedding_dropout_sums():
+    tr = _tr()
+    g = torch.Generator().manual_seed(10)
+    V, C, B, T = 50, 24, 3, 17
+    ids = torch.randint(0, V, (B, T), generator=g)
+    dout = torch.randn(B * T, C, generator=g)
+    table = torch.randn(V, C, generator=g)
+    want = torch.zeros(V, C).index_add_(0, ids.view(-1), dout) * math.sqrt(C)
+    got = torch.empty(V, C, device=DEV)
+    tr.check(tr.lib().mtt_embed_bwd(ids.to(DEV).data_ptr(), B * T, dout.to(DEV).data_ptr(), V, C, math.sqrt(C),
+                                    got.data_ptr(), tr._s(got)))
+    assert _rel(got, want) < 1e-6
+    out = torch.empty(B * T, C, device=DEV)
+    tr.check(tr.lib().mtt_embed_fwd(ids.to(DEV).data_ptr(), B * T, table.to(DEV).data_ptr(), C, math.sqrt(C),
+                                    out.data_ptr(), tr._s(out)))
+    assert torch.equal(out.cpu(), table[ids.view(-1)] * math.sqrt(C))
+    # dropout: keep rate, scaling, same mask for the same seed, different mask for another seed
+    x = torch.ones(1 << 20, device=DEV)
+    a, b, c = tr.dropout(x, 0.3, 77), tr.dropout(x, 0.3, 77), tr.dropout(x, 0.3, 78)
+    assert torch.equal(a, b) and not torch.equal(a, c)
+    keep = (a != 0).float().mean().item()
+    assert abs(keep - 0.7) < 3e-3
+    assert torch.allclose(a[a != 0], torch.full_like(a[a != 0], 1 / 0.7))
+    # colsum (segmented) and full sum
+    y = torch.randn(300, 70, generator=g)
+    cs = tr.colsum(y.to(DEV), 70, torch.empty(3, 70, device=DEV), seg=100)
+    assert _rel(cs, y.view(3, 100, 70).sum(1)) < 1e-6
+    assert abs(tr.total(y.to(DEV)).item() - y.double().sum().item()) < 1e-3
+
+
+def test_adam_and_clip_match_torch():
+    """mtt_clip_factor + mtt_adam against torch.nn.utils.clip_grad_norm_(5.0) + torch.optim.Adam(lr) over 3 steps,
+    both the clipping (large gradients) and non-clipping regimes, and the world-2 averaging fold."""
+    tr = _tr()
+    g = torch.Generator().manual_seed(11)
+    n = 5000
+    p0 = torch.randn(n, generator=g)
+    for world, gscale in ((1, 0.01), (1, 1.0), (2, 1.0)):
+        p_ref = p0.clone().requires_grad_(True)
+        opt = torch.optim.Adam([p_ref], lr=1e-3)
+        p, m, v = p0.to(DEV), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+        for step in range(1, 4):
+            gr = torch.randn(n, generator=g) * gscale
+            p_ref.grad = gr.clone()
+            torch.nn.utils.clip_grad_norm_([p_ref], 5.0)
+            opt.step()
+            gsum = (gr * world).to(DEV)  # the flat buffer after a SUM all-reduce of identical rank gradients
+            sc = torch.empty(2, device=DEV)
+            tr.check(tr.lib().mtt_clip_factor(tr.total(gsum, gsum).data_ptr(), 5.0, 1.0 / world, sc.data_ptr(),
+                                              sc[1:].data_ptr(), tr._s(sc)))
+            tr.check(tr.lib().mtt_adam(p.data_ptr(), gsum.data_ptr(), m.data_ptr(), v.data_ptr(), n, sc.data_ptr(),
+                                       1e-3, 0.9, 0.999, 1e-8, step, tr._s(p)))
+            assert abs(sc[1].item() - gr.norm().item()) / gr.norm().item() < 1e-5
+        assert (p.cpu() - p_ref.detach()).abs().max().item() < 1e-6
+
+
+# ----------------------------------------------------------------------------------------- the step
+def _setup(seed=21, B=3, Tx=17, Ty=64, x_len=(17, 12, 9), y_len=(64, 50, 33)):
+    m = make_matcha(1, "fp32")
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(
+        [(k, tuple(v.shape)) for k, v in m.state_dict().items()], seed).items()}
+    g = torch.Generator().manual_seed(seed)
+    xl, yl = torch.tensor(x_len), torch.tensor(y_len)
+    x = torch.randint(1, 178, (B, Tx), generator=g) * (torch.arange(Tx)[None] < xl[:, None])
+    y = torch.randn(B, 80, Ty, generator=g) * 1.5 * (torch.arange(Ty)[None, None] < yl[:, None, None])
+    t = torch.rand(B, generator=g)
+    z = torch.randn(B, 80, Ty, generator=g)
+    return sd, x, xl, y, yl, t, z
+
+
+def _oracle_grads(sd, x, xl, y, yl, t, z):
+    import oracle.matcha_oracle as O
+    params = {k: v.clone().float().requires_grad_(True) for k, v in sd.items()
+              if k.startswith(("encoder.", "decoder.estimator."))}
+    dur, prior, cfm, attn, lp = O.training_losses(params, x, xl, y, yl, t, z, HP)
+    grads = torch.autograd.grad(dur + prior + cfm, list(params.values()), allow_unused=True)
+    return (dur, prior, cfm, attn, lp), {k: (gr if gr is not None else torch.zeros_like(p))
+                                         for (k, p), gr in zip(params.items(), grads)}
+
+
+def test_training_step_matches_autograd():
+    """Losses (rel 1e-4), the MAS path (exact), the log-prior (rel 1e-5) and every parameter gradient (relative
+    L2 error < 2e-3 per tensor, < 5e-4 over the whole flat gradient) of the fp32 GPU step against fp32 torch
+    autograd through the oracle on the CPU (the reference's arithmetic order for the time embedding and the
+    log-prior) on the same weights, batch, t and z (dropout off: eval-mode modules)."""
+    from matcha_hip.train import MatchaTrainer
+    sd, x, xl, y, yl, t, z = _setup()
+    (dur, prior, cfm, attn, lp), gref = _oracle_grads(sd, x, xl, y, yl, t, z)
+    tr = MatchaTrainer(sd, HP, DEV, dropout=False)
+    out = tr.forward_backward(x.to(DEV), xl.to(DEV), y.to(DEV), yl.to(DEV), t=t.to(DEV), z=z.to(DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(out["attn"].cpu(), attn.float())
+    assert _rel(out["log_prior"], lp) < 1e-5
+    for name, a, b in (("dur", out["dur_loss"], dur), ("prior", out["prior_loss"], prior), ("cfm", out["cfm_loss"], cfm)):
+        assert abs(a.item() - b.item()) <= 1e-4 * abs(b.item()), (name, a.item(), b.item())
+    got = tr.gradients()
+    # the encoder's key bias adds q.b to every score of a row: softmax is invariant to it, so its true gradient
+    # is 0 and both sides hold rounding noise; it is checked against the scale of the key weight's gradient
+    kb = [k for k in gref if k.endswith("conv_k.bias")]
+    for k in kb:
+        assert float((got[k].cpu() - gref[k]).norm()) <= 1e-3 * float(gref[k[:-4] + "weight"].norm()), k
+    worst = max((_rel(got[k], gref[k]), k) for k in gref if k not in kb)
+    assert worst[0] < 2e-3, worst
+    flat_ref = torch.cat([gref[n].reshape(-1) for n in tr.grads.names])
+    assert _rel(tr.grads.flat, flat_ref) < 5e-4
+    # the duration loss trains proj_w only (its input is detached, model.py:532)
+    assert all(gref[k].norm() > 0 for k in gref if k.startswith("encoder.proj_w."))
+
+
+def test_training_step_adam_update_matches_torch():
+    """optimizer_step on the GPU gradients vs clip_grad_norm_(5.0) + Adam(lr 1e-4) applied by torch to the SAME
+    gradients: the update is isolated from gradient rounding (max |dp| error 5e-7, a few ulp of the weights)."""
+    from matcha_hip.train import MatchaTrainer
+    sd, x, xl, y, yl, t, z = _setup(seed=22)
+    tr = MatchaTrainer(sd, HP, DEV, dropout=False)
+    tr.forward_backward(x.to(DEV), xl.to(DEV), y.to(DEV), yl.to(DEV), t=t.to(DEV), z=z.to(DEV))
+    g = {k: v.detach().cpu().clone() for k, v in tr.gradients().items()}
+    p0 = {k: v.detach().cpu().clone() for k, v in tr.parameters().items()}
+    tr.optimizer_step()
+    ref = {k: p0[k].clone().requires_grad_(True) for k in tr.grads.names}
+    for k, p in ref.items():
+        p.grad = g[k].clone()
+    norm = torch.nn.utils.clip_grad_norm_(list(ref.values()), 5.0)
+    torch.optim.Adam(list(ref.values()), lr=1e-4).step()
+    assert abs(tr.last["grad_norm"].item() - norm.item()) <= 1e-5 * norm.item()
+    err = max(float((tr.parameters()[k].cpu() - ref[k].detach()).abs().max()) for k in ref)
+    assert err < 5e-7
+
+
+def test_training_with_dropout_is_deterministic_and_learns():
+    """Dropout on (p = 0.1 encoder, 0.5 prenet, 0.1 duration predictor, 0.05 estimator): two trainers from the
+    same weights and seed produce bit-identical losses and parameters (no atomics anywhere), the dropout
+    masks change the loss against the eval-mode step, and 12 Adam steps on one batch lower the loss."""
+    from matcha_hip.train import MatchaTrainer
+    sd, x, xl, y, yl, t, z = _setup(seed=23)
+    args = (x.to(DEV), xl.to(DEV), y.to(DEV), yl.to(DEV))
+    a, b = MatchaTrainer(sd, HP, DEV, seed=5), MatchaTrainer(sd, HP, DEV, seed=5)
+    ev = MatchaTrainer(sd, HP, DEV, dropout=False).forward_backward(*args, t=t.to(DEV), z=z.to(DEV))["loss"].item()
+    losses = []
+    for step in range(12):
+        la = a.forward_backward(*args, t=t.to(DEV), z=z.to(DEV))["loss"].item()
+        a.optimizer_step()
+        if step < 2:
+            lb = b.forward_backward(*args, t=t.to(DEV), z=z.to(DEV))["loss"].item()
+            b.optimizer_step()
+            assert la == lb and torch.equal(a.params.flat, b.params.flat)
+        if step == 0:
+            assert la != ev and math.isfinite(la)
+        losses.append(la)
+    assert np.mean(losses[-3:]) < np.mean(losses[:3]), losses
