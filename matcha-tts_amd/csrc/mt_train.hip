@@ -28,80 +28,179 @@
 namespace mt {
 
 // ------------------------------------------------------------------------------------------------ gemm
+// 128 x 128 block tile, K staged through LDS 32 at a time (k-major: As[k][m], Bs[k][n]), 4 waves of 64 x 64,
+// each 2 x 2 v_mfma_f32_32x32x2_f32 accumulators (exact fp32: a k-ordered fma chain per output). The next
+// K chunk's global loads (16-byte along the operand's contiguous dimension when aligned) are issued before
+// the current chunk's MFMAs. Split-K (small M x N, long K: the weight gradients, K = frames) writes per-slice
+// partials that a second kernel sums in slice order — deterministic, no atomics.
 namespace {
-constexpr int GT = 64, GK = 16;  // tile rows / cols, K chunk
+constexpr int GBM = 128, GBK = 32, GLD = GBM + 4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+// v[j] = src[row][col + j] for the 4-wide group (0 outside [0, nrow) x [0, ncol))
+__device__ __forceinline__ f32x4 ld4(const float* __restrict__ base, int ld, int row, int col, int nrow, int ncol,
+                                     bool vec) {
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (row >= nrow) return v;
+  const float* p = base + (size_t)row * ld + col;
+  if (vec && col + 3 < ncol) return *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (col + j < ncol) v[j] = p[j];
+  return v;
+}
+}  // namespace
+
+// op(A) tile (128 m x 32 k) / op(B) tile (32 k x 128 n): 1024 groups of 4, 4 per thread
+template <int TA>
+__device__ __forceinline__ void gemm_load_a(const GemmF32& g, const float* A, int m0, int kb, int kend, bool vec,
+                                            f32x4 (&r)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    if (TA) r[i] = ld4(A, g.lda, kb + (e >> 5), m0 + (e & 31) * 4, kend, g.M, vec);  // stored [K][M]
+    else r[i] = ld4(A, g.lda, m0 + (e >> 3), kb + (e & 7) * 4, g.M, kend, vec);      // stored [M][K]
+  }
+}
+template <int TA>
+__device__ __forceinline__ void gemm_store_a(float (*As)[GLD], const f32x4 (&r)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    if (TA) {
+      *reinterpret_cast<f32x4*>(&As[e >> 5][(e & 31) * 4]) = r[i];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) As[(e & 7) * 4 + j][e >> 3] = r[i][j];
+    }
+  }
 }
 
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32 g) {
-  __shared__ float As[GK][GT + 4], Bs[GK][GT + 4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;  // 2 x 2 waves of 32 x 32
-  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT, z = blockIdx.z;
-  const float* A = g.A + (size_t)z * g.sA;
-  const float* B = g.B + (size_t)z * g.sB;
+template <int TA, int TB>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32 g, int kchunk, int split, bool va, bool vb) {
+  __shared__ float As[GBK][GLD], Bs[GBK][GLD];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBM, z = blockIdx.z;
+  const float* A = g.A + (split ? 0 : (size_t)z * g.sA);
+  const float* B = g.B + (split ? 0 : (size_t)z * g.sB);
   float* Cm = g.C + (size_t)z * g.sC;
-  f32x4 acc[2][2];
+  const int kbeg = split ? z * kchunk : 0, kend = split ? min(g.K, kbeg + kchunk) : g.K;
+  // B is loaded as op(B)^T's A-shaped case: TB == 1 means stored [N][K] (contiguous k) like TA == 0
+  GemmF32 gb = g;
+  gb.M = g.N;
+  gb.lda = g.ldb;
+  f32x16 acc[2][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < g.K; k0 += GK) {
-    // A tile: 64 (m) x 16 (k); B tile: 16 (k) x 64 (n); 4 elements per thread each, the contiguous
-    // global dimension mapped to consecutive threads
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + i * 256;
-      int m, k;
-      if (g.transA) { m = e % GT; k = e / GT; } else { k = e % GK; m = e / GK; }
-      const int gm = m0 + m, gk = k0 + k;
-      float v = 0.f;
-      if (gm < g.M && gk < g.K) v = g.transA ? A[(size_t)gk * g.lda + gm] : A[(size_t)gm * g.lda + gk];
-      As[k][m] = v;
-      int n, kb;
-      if (g.transB) { kb = e % GK; n = e / GK; } else { n = e % GT; kb = e / GT; }
-      const int gn = n0 + n, gkb = k0 + kb;
-      float w = 0.f;
-      if (gn < g.N && gkb < g.K) w = g.transB ? B[(size_t)gn * g.ldb + gkb] : B[(size_t)gkb * g.ldb + gn];
-      Bs[kb][n] = w;
-    }
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  f32x4 ra[4], rb[4];
+  gemm_load_a<TA>(g, A, m0, kbeg, kend, va, ra);
+  gemm_load_a<1 - TB>(gb, B, n0, kbeg, kend, vb, rb);
+  for (int kb = kbeg; kb < kend; kb += GBK) {
+    gemm_store_a<TA>(As, ra);
+    gemm_store_a<1 - TB>(Bs, rb);
     __syncthreads();
+    if (kb + GBK < kend) {
+      gemm_load_a<TA>(g, A, m0, kb + GBK, kend, va, ra);
+      gemm_load_a<1 - TB>(gb, B, n0, kb + GBK, kend, vb, rb);
+    }
 #pragma unroll
-    for (int kk = 0; kk < GK; kk += 4) {
-      const int kr = kk + (lane >> 4);
+    for (int kk = 0; kk < GBK; kk += 2) {
+      const int kr = kk + (lane >> 5);
       float a[2], b[2];
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
-        a[f] = As[kr][wm * 32 + f * 16 + (lane & 15)];
-        b[f] = Bs[kr][wn * 32 + f * 16 + (lane & 15)];
+        a[f] = As[kr][wm * 64 + f * 32 + (lane & 31)];
+        b[f] = Bs[kr][wn * 64 + f * 32 + (lane & 31)];
       }
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
         for (int fn = 0; fn < 2; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[fm], b[fn], acc[fm][fn], 0, 0, 0);
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[fm], b[fn], acc[fm][fn], 0, 0, 0);
     }
     __syncthreads();
   }
-  // D: lane holds rows 4 (lane >> 4) + r, column lane & 15 of each 16 x 16 fragment
+  // D of a 32 x 32 fragment: column lane & 31, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  const float alpha = split ? 1.f : g.alpha, beta = split ? 0.f : g.beta;
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
     for (int fn = 0; fn < 2; ++fn)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gm = m0 + wm * 32 + fm * 16 + 4 * (lane >> 4) + r;
-        const int gn = n0 + wn * 32 + fn * 16 + (lane & 15);
+      for (int r = 0; r < 16; ++r) {
+        const int gm = m0 + wm * 64 + fm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int gn = n0 + wn * 64 + fn * 32 + (lane & 31);
         if (gm >= g.M || gn >= g.N) continue;
-        float* c = Cm + (size_t)gm * g.ldc + gn;
-        float v = g.alpha * acc[fm][fn][r];
-        if (g.beta != 0.f) v += g.beta * *c;
+        float* c = Cm + (size_t)gm * (split ? g.N : g.ldc) + gn;
+        float v = alpha * acc[fm][fn][r];
+        if (beta != 0.f) v += beta * *c;
         *c = v;
       }
 }
 
+// C = alpha * sum_z P[z] + beta * C, slices in order
+__global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, int N, float alpha, float beta,
+                                     float* __restrict__ C, int ldc) {
+  const size_t mn = (size_t)M * N;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < mn; i += (size_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += P[z * mn + i];
+    float* c = C + (i / N) * ldc + i % N;
+    float v = alpha * s;
+    if (beta != 0.f) v += beta * *c;
+    *c = v;
+  }
+}
+
+namespace {
+float* g_splitk = nullptr;  // grow-only partial-sum scratch of the split-K path
+size_t g_splitk_cap = 0;
+bool vec_ok(const float* p, int ld, long long stride, int batch) {
+  return ((uintptr_t)p & 15) == 0 && ld % 4 == 0 && (batch == 1 || stride % 4 == 0);
+}
+}  // namespace
+
+static dim3 ew_grid(size_t n);
+
 int gemm_f32(const GemmF32& g, hipStream_t st) {
   MT_REQUIRE(g.M > 0 && g.N > 0 && g.K > 0 && g.batch > 0 && g.A && g.B && g.C, "gemm: shape / null");
-  dim3 grid((g.N + GT - 1) / GT, (g.M + GT - 1) / GT, g.batch);
-  MT_REQUIRE(grid.z <= 65535 && grid.y <= 65535, "gemm: grid too large");
-  hipLaunchKernelGGL(gemm_f32_kernel, grid, dim3(256), 0, st, g);
+  const int gx = (g.N + GBM - 1) / GBM, gy = (g.M + GBM - 1) / GBM;
+  MT_REQUIRE(gy <= 65535 && g.batch <= 65535, "gemm: grid too large");
+  const bool va = vec_ok(g.A, g.lda, g.sA, g.batch), vb = vec_ok(g.B, g.ldb, g.sB, g.batch);
+  int split = 0, kchunk = g.K, S = g.batch;
+  GemmF32 k = g;
+  if (g.batch == 1 && gx * gy < 128 && g.K >= 2048) {  // long-K, few tiles: split K over >= ~256 blocks
+    const int want = std::min((g.K + 511) / 512, (256 + gx * gy - 1) / (gx * gy));
+    kchunk = ((g.K + want - 1) / want + GBK - 1) / GBK * GBK;
+    S = (g.K + kchunk - 1) / kchunk;
+    if (S > 1) {
+      const size_t need = (size_t)S * g.M * g.N;
+      if (need > g_splitk_cap) {
+        if (g_splitk) MT_CHECK_HIP(hipFree(g_splitk));
+        g_splitk = nullptr;
+        MT_CHECK_HIP(hipMalloc(&g_splitk, need * sizeof(float)));
+        g_splitk_cap = need;
+      }
+      split = 1;
+      k.C = g_splitk;
+      k.sC = (long long)g.M * g.N;
+    } else {
+      kchunk = g.K;
+      S = 1;
+    }
+  }
+  dim3 grid(gx, gy, S);
+  auto kern = g.transA ? (g.transB ? gemm_f32_kernel<1, 1> : gemm_f32_kernel<1, 0>)
+                       : (g.transB ? gemm_f32_kernel<0, 1> : gemm_f32_kernel<0, 0>);
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, k, kchunk, split, va, vb);
+  if (split)
+    hipLaunchKernelGGL(splitk_reduce_kernel, ew_grid((size_t)g.M * g.N), dim3(256), 0, st, (const float*)g_splitk,
+                       S, g.M, g.N, g.alpha, g.beta, g.C, g.ldc);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -58,8 +58,9 @@ def mm(A, B, M, N, K, **kw):
     return gemm(A, B, M, N, K, empty(M, N, like=A), **kw)
 
 
-def ew(op, out, a=None, b=None, c=None, alpha=1.0, beta=0.0, bc=None, acc=False):
-    """out[i] (+)= op(a[i], b[bidx(i)], c[i]) (mtt_ew); bc = (d0, m0, s0, d1, m1, s1) broadcast of b."""
+def ew(op, out, a=None, b=None, c=None, alpha=1.0, beta=1.0, bc=None, acc=False):
+    """out[i] (+)= op(a[i], b[bidx(i)], c[i]) (mtt_ew; a missing operand reads 0); bc = (d0, m0, s0, d1, m1, s1)
+    broadcast of b. AXPBY defaults to a + b."""
     n = out.numel()
     d0, m0, s0, d1, m1, s1 = bc if bc is not None else (1, n, 1, 1, 1, 0)
     check(lib().mtt_ew(op, n, ptr(a), ptr(b), ptr(c), out.data_ptr(), float(alpha), float(beta), d0, m0, s0, d1, m1,
@@ -909,8 +910,8 @@ class MatchaTrainer:
         """gradient_clip_val 5.0 (norm of the world-averaged gradient) then torch.optim.Adam (lr, defaults)."""
         self.step_count += 1
         g = self.grads.flat
-        scale = empty(2, like=g)
-        check(lib().mtt_clip_factor(total(g, g).data_ptr(), float(self.clip), 1.0 / self.world, scale.data_ptr(),
+        scale, sumsq = empty(2, like=g), total(g, g)
+        check(lib().mtt_clip_factor(sumsq.data_ptr(), float(self.clip), 1.0 / self.world, scale.data_ptr(),
                                     scale[1:].data_ptr(), _s(g)), "clip_factor")
         check(lib().mtt_adam(self.params.flat.data_ptr(), g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), g.numel(),
                              scale.data_ptr(), float(self.lr), 0.9, 0.999, 1e-8, self.step_count, _s(g)), "adam")

@@ -30,8 +30,11 @@ def _rel(a, b):
 
 # ----------------------------------------------------------------------------------------- primitives
 @pytest.mark.parametrize("ta,tb,M,N,K,batch", [(0, 0, 70, 33, 19, 1), (1, 0, 64, 64, 100, 3), (0, 1, 5, 130, 64, 2),
-                                               (1, 1, 17, 9, 3, 1)])
+                                               (1, 1, 17, 9, 3, 1), (0, 0, 300, 260, 132, 2),
+                                               (1, 0, 40, 70, 5000, 1), (0, 1, 200, 96, 3001, 1)])
 def test_gemm_f32(ta, tb, M, N, K, batch):
+    """vector (aligned leading dimensions) and scalar loads, partial tiles, batch strides, and the split-K path
+    (the last two cases: few tiles, long K, per-slice partials summed in order)"""
     tr = _tr()
     g = torch.Generator().manual_seed(M * N + K)
     A = torch.randn(batch, *((K, M) if ta else (M, K)), generator=g)
@@ -119,10 +122,10 @@ def test_snake_mish_silu_relu_bwd():
     dx, ga, gb = torch.empty_like(xd), torch.empty_like(xd), torch.empty_like(xd)
     yd = torch.empty_like(xd)
     L = tr.lib()
-    tr.check(L.mtt_snake_fwd(xd.data_ptr(), la.detach().to(DEV).data_ptr(), lb.detach().to(DEV).data_ptr(), xd.numel(),
-                             96, yd.data_ptr(), tr._s(xd)))
-    la_d, lb_d = la.detach().to(DEV), lb.detach().to(DEV)
-    tr.check(L.mtt_snake_bwd(xd.data_ptr(), la_d.data_ptr(), lb_d.data_ptr(), dy.to(DEV).data_ptr(), xd.numel(), 96,
+    la_d, lb_d, dy_d = la.detach().to(DEV), lb.detach().to(DEV), dy.to(DEV)  # kept alive across the calls
+    tr.check(L.mtt_snake_fwd(xd.data_ptr(), la_d.data_ptr(), lb_d.data_ptr(), xd.numel(), 96, yd.data_ptr(),
+                             tr._s(xd)))
+    tr.check(L.mtt_snake_bwd(xd.data_ptr(), la_d.data_ptr(), lb_d.data_ptr(), dy_d.data_ptr(), xd.numel(), 96,
                              dx.data_ptr(), ga.data_ptr(), gb.data_ptr(), tr._s(xd)))
     assert _rel(yd, y) < 1e-6 and _rel(dx, ref[0]) < 1e-5
     assert _rel(ga.sum(0), ref[1]) < 1e-5 and _rel(gb.sum(0), ref[2]) < 1e-5
@@ -193,12 +196,13 @@ def test_embedding_dropout_sums():
     table = torch.randn(V, C, generator=g)
     want = torch.zeros(V, C).index_add_(0, ids.view(-1), dout) * math.sqrt(C)
     got = torch.empty(V, C, device=DEV)
-    tr.check(tr.lib().mtt_embed_bwd(ids.to(DEV).data_ptr(), B * T, dout.to(DEV).data_ptr(), V, C, math.sqrt(C),
-                                    got.data_ptr(), tr._s(got)))
+    ids_d, dout_d, table_d = ids.to(DEV), dout.to(DEV), table.to(DEV)
+    tr.check(tr.lib().mtt_embed_bwd(ids_d.data_ptr(), B * T, dout_d.data_ptr(), V, C, math.sqrt(C), got.data_ptr(),
+                                    tr._s(got)))
     assert _rel(got, want) < 1e-6
     out = torch.empty(B * T, C, device=DEV)
-    tr.check(tr.lib().mtt_embed_fwd(ids.to(DEV).data_ptr(), B * T, table.to(DEV).data_ptr(), C, math.sqrt(C),
-                                    out.data_ptr(), tr._s(out)))
+    tr.check(tr.lib().mtt_embed_fwd(ids_d.data_ptr(), B * T, table_d.data_ptr(), C, math.sqrt(C), out.data_ptr(),
+                                    tr._s(out)))
     assert torch.equal(out.cpu(), table[ids.view(-1)] * math.sqrt(C))
     # dropout: keep rate, scaling, same mask for the same seed, different mask for another seed
     x = torch.ones(1 << 20, device=DEV)
@@ -231,9 +235,9 @@ def test_adam_and_clip_match_torch():
             torch.nn.utils.clip_grad_norm_([p_ref], 5.0)
             opt.step()
             gsum = (gr * world).to(DEV)  # the flat buffer after a SUM all-reduce of identical rank gradients
-            sc = torch.empty(2, device=DEV)
-            tr.check(tr.lib().mtt_clip_factor(tr.total(gsum, gsum).data_ptr(), 5.0, 1.0 / world, sc.data_ptr(),
-                                              sc[1:].data_ptr(), tr._s(sc)))
+            sc, sumsq = torch.empty(2, device=DEV), tr.total(gsum, gsum)
+            tr.check(tr.lib().mtt_clip_factor(sumsq.data_ptr(), 5.0, 1.0 / world, sc.data_ptr(), sc[1:].data_ptr(),
+                                              tr._s(sc)))
             tr.check(tr.lib().mtt_adam(p.data_ptr(), gsum.data_ptr(), m.data_ptr(), v.data_ptr(), n, sc.data_ptr(),
                                        1e-3, 0.9, 0.999, 1e-8, step, tr._s(p)))
             assert abs(sc[1].item() - gr.norm().item()) / gr.norm().item() < 1e-5
