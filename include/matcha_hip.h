@@ -200,15 +200,23 @@ int mt_maximum_path(const float* neg_cent, const int32_t* t_xs, const int32_t* t
  * is built from, forward and backward (matcha_hip/train.py composes them). Activations are [rows][C]
  * row-major fp32 device buffers. No reduction uses atomics (bitwise reproducible).
  * ------------------------------------------------------------------------------------- */
-/* C[z] = alpha op(A[z]) op(B[z]) + beta C[z]; op(A) M x K, op(B) K x N; z < batch, strides in elements */
+/* C[z] = (alpha op(A[z]) op(B[z]) + beta C[z] + bias[n]) * row_mask[z][m]; op(A) M x K, op(B) K x N; z < batch,
+ * strides in elements; bias [N] and row_mask [batch][M] optional (NULL). Exact-fp32 MFMA (32x32x2 f32); a long K over
+ * few output tiles is split into slices whose partials (in the caller's workspace) are summed in slice order
+ * (deterministic). */
 int mtt_gemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda, long long sA,
-             const float* B, int ldb, long long sB, float beta, float* C, int ldc, long long sC, int batch, void* stream);
-/* conv1d columns: cols[(b*Tout+o)][c*k+tap] = x[b][o*stride-pad+tap*dil][c] (a torch Conv1d weight [Cout][Cin][k]
- * is then the GEMM operand as stored); col2im is its adjoint */
-int mtt_im2col(const float* x, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* cols,
-               void* stream);
-int mtt_col2im(const float* dcols, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* dx,
-               int accumulate, void* stream);
+             const float* B, int ldb, long long sB, float beta, float* C, int ldc, long long sC, int batch,
+             const float* bias, const float* row_mask, float* ws, size_t ws_bytes, void* stream);
+/* device workspace mtt_gemm uses to split a long K over slices (0: never splits this shape); with less, it runs
+ * unsplit */
+size_t mtt_gemm_workspace_bytes(int M, int N, int K, int batch);
+/* conv1d columns: cols[(b*Tout+o)][c*k+tap] = x[b][t][c] * mask[b][t], t = o*stride-pad+tap*dil (a torch Conv1d weight
+ * [Cout][Cin][k] is then the GEMM operand as stored; mask [B][T] optional: the reference's conv(x * mask)); col2im is
+ * its adjoint, dx[b][t][c] (+)= mask[b][t] * sum of the columns that read (b, t, c) */
+int mtt_im2col(const float* x, const float* mask, int B, int T, int C, int k, int stride, int pad, int dil, int Tout,
+               float* cols, void* stream);
+int mtt_col2im(const float* dcols, const float* mask, int B, int T, int C, int k, int stride, int pad, int dil,
+               int Tout, float* dx, int accumulate, void* stream);
 /* out[i] (+)= op(a[i], b[((i/d0)%m0)*s0 + ((i/d1)%m1)*s1], c[i]); op: 0 alpha a + beta b, 1 alpha a b,
  * 2 mish(a), 3 c mish'(a), 4 silu(a), 5 c silu'(a), 6 relu(a), 7 c [a>0], 8 exp(a), 9 (a-b)^2, 10 sin(a),
  * 11 cos(a), 12 log(alpha + a), 13 alpha / a */

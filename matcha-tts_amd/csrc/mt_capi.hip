@@ -361,17 +361,22 @@ int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes,
 
 // ---- training-step primitives (fp32) ----
 int mtt_gemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda, long long sA,
-             const float* B, int ldb, long long sB, float beta, float* C, int ldc, long long sC, int batch, void* stream) {
-  mt::GemmF32 g{transA, transB, M, N, K, alpha, beta, A, lda, sA, B, ldb, sB, C, ldc, sC, batch};
+             const float* B, int ldb, long long sB, float beta, float* C, int ldc, long long sC, int batch,
+             const float* bias, const float* row_mask, float* ws, size_t ws_bytes, void* stream) {
+  mt::GemmF32 g{transA, transB, M, N, K, alpha, beta, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, bias, row_mask, ws,
+                ws_bytes / sizeof(float)};
   return mt::gemm_f32(g, (hipStream_t)stream);
 }
-int mtt_im2col(const float* x, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* cols,
-               void* stream) {
-  return mt::im2col(x, B, T, C, k, stride, pad, dil, Tout, cols, (hipStream_t)stream);
+size_t mtt_gemm_workspace_bytes(int M, int N, int K, int batch) {
+  return mt::gemm_f32_workspace_floats(M, N, K, batch) * sizeof(float);
 }
-int mtt_col2im(const float* dcols, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* dx,
-               int accumulate, void* stream) {
-  return mt::col2im(dcols, B, T, C, k, stride, pad, dil, Tout, dx, accumulate, (hipStream_t)stream);
+int mtt_im2col(const float* x, const float* mask, int B, int T, int C, int k, int stride, int pad, int dil, int Tout,
+               float* cols, void* stream) {
+  return mt::im2col(x, mask, B, T, C, k, stride, pad, dil, Tout, cols, (hipStream_t)stream);
+}
+int mtt_col2im(const float* dcols, const float* mask, int B, int T, int C, int k, int stride, int pad, int dil,
+               int Tout, float* dx, int accumulate, void* stream) {
+  return mt::col2im(dcols, mask, B, T, C, k, stride, pad, dil, Tout, dx, accumulate, (hipStream_t)stream);
 }
 int mtt_ew(int op, size_t n, const float* a, const float* b, const float* c, float* out, float alpha, float beta,
            size_t d0, size_t m0, size_t s0, size_t d1, size_t m1, size_t s1, int accumulate, void* stream) {

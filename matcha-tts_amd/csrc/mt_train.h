@@ -19,13 +19,18 @@ struct GemmF32 {  // C[z] = alpha op(A[z]) op(B[z]) + beta C[z]; op(A) is M x K,
   int ldc;
   long long sC;
   int batch;
+  const float* bias;   // optional, per output column: C += bias[n] (after alpha / beta)
+  const float* rmask;  // optional, per output row of each batch [batch][M]: C *= rmask[m] (last)
+  float* ws;           // split-K partials (gemm_f32_workspace_floats); NULL: no split
+  size_t ws_floats;
 };
+size_t gemm_f32_workspace_floats(int M, int N, int K, int batch);
 int gemm_f32(const GemmF32& g, hipStream_t st);
 
-int im2col(const float* x, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* cols,
-           hipStream_t st);
-int col2im(const float* dcols, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* dx,
-           int accumulate, hipStream_t st);
+int im2col(const float* x, const float* mask, int B, int T, int C, int k, int stride, int pad, int dil, int Tout,
+           float* cols, hipStream_t st);
+int col2im(const float* dcols, const float* mask, int B, int T, int C, int k, int stride, int pad, int dil, int Tout,
+           float* dx, int accumulate, hipStream_t st);
 
 enum EwOp {
   EW_AXPBY = 0,     // alpha a + beta b

@@ -139,12 +139,15 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32 g, int kchunk, in
         float* c = Cm + (size_t)gm * (split ? g.N : g.ldc) + gn;
         float v = alpha * acc[fm][fn][r];
         if (beta != 0.f) v += beta * *c;
+        if (!split && g.bias) v += g.bias[gn];
+        if (!split && g.rmask) v *= g.rmask[(size_t)z * g.M + gm];
         *c = v;
       }
 }
 
 // C = alpha * sum_z P[z] + beta * C, slices in order
 __global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, int N, float alpha, float beta,
+                                     const float* __restrict__ bias, const float* __restrict__ rmask,
                                      float* __restrict__ C, int ldc) {
   const size_t mn = (size_t)M * N;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < mn; i += (size_t)gridDim.x * blockDim.x) {
@@ -153,17 +156,34 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, 
     float* c = C + (i / N) * ldc + i % N;
     float v = alpha * s;
     if (beta != 0.f) v += beta * *c;
+    if (bias) v += bias[i % N];
+    if (rmask) v *= rmask[i / N];
     *c = v;
   }
 }
 
 namespace {
-float* g_splitk = nullptr;  // grow-only partial-sum scratch of the split-K path
-size_t g_splitk_cap = 0;
 bool vec_ok(const float* p, int ld, long long stride, int batch) {
   return ((uintptr_t)p & 15) == 0 && ld % 4 == 0 && (batch == 1 || stride % 4 == 0);
 }
+// split-K plan: slices of kchunk (a multiple of GBK) when a single GEMM has few output tiles and a long K
+int splitk_plan(int M, int N, int K, int batch, int* kchunk) {
+  const int tiles = ((N + GBM - 1) / GBM) * ((M + GBM - 1) / GBM);
+  *kchunk = K;
+  if (batch != 1 || tiles >= 128 || K < 2048) return 1;
+  const int want = std::min((K + 511) / 512, (256 + tiles - 1) / tiles);
+  *kchunk = ((K + want - 1) / want + GBK - 1) / GBK * GBK;
+  const int S = (K + *kchunk - 1) / *kchunk;
+  if (S <= 1) *kchunk = K;
+  return S;
+}
 }  // namespace
+
+size_t gemm_f32_workspace_floats(int M, int N, int K, int batch) {
+  int kc;
+  const int S = splitk_plan(M, N, K, batch, &kc);
+  return S > 1 ? (size_t)S * M * N : 0;
+}
 
 static dim3 ew_grid(size_t n);
 
@@ -174,24 +194,15 @@ int gemm_f32(const GemmF32& g, hipStream_t st) {
   const bool va = vec_ok(g.A, g.lda, g.sA, g.batch), vb = vec_ok(g.B, g.ldb, g.sB, g.batch);
   int split = 0, kchunk = g.K, S = g.batch;
   GemmF32 k = g;
-  if (g.batch == 1 && gx * gy < 128 && g.K >= 2048) {  // long-K, few tiles: split K over >= ~256 blocks
-    const int want = std::min((g.K + 511) / 512, (256 + gx * gy - 1) / (gx * gy));
-    kchunk = ((g.K + want - 1) / want + GBK - 1) / GBK * GBK;
-    S = (g.K + kchunk - 1) / kchunk;
-    if (S > 1) {
-      const size_t need = (size_t)S * g.M * g.N;
-      if (need > g_splitk_cap) {
-        if (g_splitk) MT_CHECK_HIP(hipFree(g_splitk));
-        g_splitk = nullptr;
-        MT_CHECK_HIP(hipMalloc(&g_splitk, need * sizeof(float)));
-        g_splitk_cap = need;
-      }
+  if (g.batch == 1) {
+    const int s = splitk_plan(g.M, g.N, g.K, 1, &kchunk);
+    if (s > 1 && g.ws && g.ws_floats >= (size_t)s * g.M * g.N) {  // without the workspace: one unsplit pass
       split = 1;
-      k.C = g_splitk;
+      S = s;
+      k.C = g.ws;
       k.sC = (long long)g.M * g.N;
     } else {
       kchunk = g.K;
-      S = 1;
     }
   }
   dim3 grid(gx, gy, S);
@@ -199,8 +210,8 @@ int gemm_f32(const GemmF32& g, hipStream_t st) {
                        : (g.transB ? gemm_f32_kernel<0, 1> : gemm_f32_kernel<0, 0>);
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, k, kchunk, split, va, vb);
   if (split)
-    hipLaunchKernelGGL(splitk_reduce_kernel, ew_grid((size_t)g.M * g.N), dim3(256), 0, st, (const float*)g_splitk,
-                       S, g.M, g.N, g.alpha, g.beta, g.C, g.ldc);
+    hipLaunchKernelGGL(splitk_reduce_kernel, ew_grid((size_t)g.M * g.N), dim3(256), 0, st, (const float*)g.ws,
+                       S, g.M, g.N, g.alpha, g.beta, g.bias, g.rmask, g.C, g.ldc);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -209,8 +220,8 @@ int gemm_f32(const GemmF32& g, hipStream_t st) {
 // cols[(b*Tout + o)][c*k + tap] = x[b][o*stride - pad + tap*dil][c] (0 outside [0, T)): channel-major, tap
 // fastest, so a torch Conv1d weight [Cout][Cin][k] is the GEMM operand [Cout][Cin*k] as it lies in memory
 // (and a ConvTranspose1d weight [Cin][Cout][k] that of its adjoint conv)
-__global__ void im2col_kernel(const float* __restrict__ x, int B, int T, int C, int k, int stride, int pad, int dil,
-                              int Tout, float* __restrict__ cols) {
+__global__ void im2col_kernel(const float* __restrict__ x, const float* __restrict__ mask, int B, int T, int C, int k,
+                              int stride, int pad, int dil, int Tout, float* __restrict__ cols) {
   const size_t total = (size_t)B * Tout * C * k;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int tap = (int)(i % k);
@@ -220,13 +231,18 @@ __global__ void im2col_kernel(const float* __restrict__ x, int B, int T, int C, 
     const int o = (int)(r % Tout);
     const int b = (int)(r / Tout);
     const int t = o * stride - pad + tap * dil;
-    cols[i] = (t >= 0 && t < T) ? x[((size_t)b * T + t) * C + c] : 0.f;
+    float v = 0.f;
+    if (t >= 0 && t < T) {
+      v = x[((size_t)b * T + t) * C + c];
+      if (mask) v *= mask[(size_t)b * T + t];
+    }
+    cols[i] = v;
   }
 }
 
-// dx[b][t][c] (+)= sum over (o, tap) with o*stride - pad + tap*dil == t of dcols[(b*Tout + o)][c*k + tap]
-__global__ void col2im_kernel(const float* __restrict__ dcols, int B, int T, int C, int k, int stride, int pad,
-                              int dil, int Tout, float* __restrict__ dx, int accumulate) {
+// dx[b][t][c] (+)= mask[b][t] * sum over (o, tap) with o*stride - pad + tap*dil == t of dcols[(b*Tout + o)][c*k + tap]
+__global__ void col2im_kernel(const float* __restrict__ dcols, const float* __restrict__ mask, int B, int T, int C,
+                              int k, int stride, int pad, int dil, int Tout, float* __restrict__ dx, int accumulate) {
   const size_t total = (size_t)B * T * C;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
@@ -240,26 +256,27 @@ __global__ void col2im_kernel(const float* __restrict__ dcols, int B, int T, int
       if (o >= Tout) continue;
       s += dcols[((size_t)b * Tout + o) * C * k + (size_t)c * k + tap];
     }
+    if (mask) s *= mask[(size_t)b * T + t];
     dx[i] = accumulate ? dx[i] + s : s;
   }
 }
 
 static dim3 ew_grid(size_t n) { return dim3((unsigned)std::min<size_t>((n + 255) / 256, 65535u * 4)); }
 
-int im2col(const float* x, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* cols,
-           hipStream_t st) {
+int im2col(const float* x, const float* mask, int B, int T, int C, int k, int stride, int pad, int dil, int Tout,
+           float* cols, hipStream_t st) {
   MT_REQUIRE(x && cols && B > 0 && T > 0 && C > 0 && k > 0 && stride > 0 && dil > 0 && Tout > 0, "im2col: args");
-  hipLaunchKernelGGL(im2col_kernel, ew_grid((size_t)B * Tout * k * C), dim3(256), 0, st, x, B, T, C, k, stride, pad,
-                     dil, Tout, cols);
+  hipLaunchKernelGGL(im2col_kernel, ew_grid((size_t)B * Tout * k * C), dim3(256), 0, st, x, mask, B, T, C, k, stride,
+                     pad, dil, Tout, cols);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }
 
-int col2im(const float* dcols, int B, int T, int C, int k, int stride, int pad, int dil, int Tout, float* dx,
-           int accumulate, hipStream_t st) {
+int col2im(const float* dcols, const float* mask, int B, int T, int C, int k, int stride, int pad, int dil, int Tout,
+           float* dx, int accumulate, hipStream_t st) {
   MT_REQUIRE(dcols && dx && B > 0 && T > 0 && C > 0 && k > 0 && stride > 0 && dil > 0 && Tout > 0, "col2im: args");
-  hipLaunchKernelGGL(col2im_kernel, ew_grid((size_t)B * T * C), dim3(256), 0, st, dcols, B, T, C, k, stride, pad, dil,
-                     Tout, dx, accumulate);
+  hipLaunchKernelGGL(col2im_kernel, ew_grid((size_t)B * T * C), dim3(256), 0, st, dcols, mask, B, T, C, k, stride, pad,
+                     dil, Tout, dx, accumulate);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -354,29 +371,41 @@ int seq_mask(const long long* lengths, int B, int T, float* out, hipStream_t st)
 }
 
 // ---------------------------------------------------------------------------------------- column sums
-// out[s][c] (+)= sum_{r in segment s} a[r][c] * (b ? b[r][c] : 1), segments of `seg` rows. Two fixed-order
-// levels: partial sums over blocks of CS_ROWS rows (one thread per column, rows in order), then the partials
-// of each segment in order (deterministic, no atomics).
-constexpr int CS_ROWS = 128;
-__global__ void colsum_part_kernel(const float* __restrict__ a, const float* __restrict__ b, int rows, int C, int seg,
-                                   int nsub, float* __restrict__ part) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x, sb = blockIdx.y;  // sub-block sb of all segments
-  if (c >= C) return;
+// out[s][c] (+)= sum_{r in segment s} a[r][c] * (b ? b[r][c] : 1), segments of `seg` rows. Two fixed-order levels,
+// no atomics: partials over blocks of CS_ROWS rows (a 256-thread block = 64 columns x 4 row lanes, lanes combined
+// in lane order), then each segment's partials (4 threads per column over interleaved partials, combined in order).
+constexpr int CS_ROWS = 512;
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                          int rows, int C, int seg, int nsub, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, lr = threadIdx.x >> 6, c = blockIdx.x * 64 + cl, sb = blockIdx.y;
   const int s = sb / nsub, k = sb % nsub;
   const int r0 = s * seg + k * CS_ROWS, r1 = min(min(rows, (s + 1) * seg), r0 + CS_ROWS);
   float acc = 0.f;
-  for (int r = r0; r < r1; ++r) acc += b ? a[(size_t)r * C + c] * b[(size_t)r * C + c] : a[(size_t)r * C + c];
-  part[(size_t)sb * C + c] = acc;
+  if (c < C)
+    for (int r = r0 + lr; r < r1; r += 4) {
+      const size_t o = (size_t)r * C + c;
+      acc += b ? a[o] * b[o] : a[o];
+    }
+  red[lr][cl] = acc;
+  __syncthreads();
+  if (lr == 0 && c < C) part[(size_t)sb * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
 }
 
-__global__ void colsum_merge_kernel(const float* __restrict__ part, int C, int nsub, float* __restrict__ out,
-                                    int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x, s = blockIdx.y;
-  if (c >= C) return;
+__global__ __launch_bounds__(256) void colsum_merge_kernel(const float* __restrict__ part, int C, int nsub,
+                                                           float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, lr = threadIdx.x >> 6, c = blockIdx.x * 64 + cl, s = blockIdx.y;
   float acc = 0.f;
-  for (int k = 0; k < nsub; ++k) acc += part[((size_t)s * nsub + k) * C + c];
-  float* o = out + (size_t)s * C + c;
-  *o = accumulate ? *o + acc : acc;
+  if (c < C)
+    for (int k = lr; k < nsub; k += 4) acc += part[((size_t)s * nsub + k) * C + c];
+  red[lr][cl] = acc;
+  __syncthreads();
+  if (lr == 0 && c < C) {
+    float* o = out + (size_t)s * C + c;
+    const float v = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+    *o = accumulate ? *o + v : v;
+  }
 }
 
 size_t colsum_scratch_floats(int rows, int C, int seg) {
@@ -388,9 +417,10 @@ int colsum(const float* a, const float* b, int rows, int C, int seg, float* out,
            hipStream_t st) {
   MT_REQUIRE(a && out && scratch && rows > 0 && C > 0 && seg > 0, "colsum: args");
   const int nseg = (rows + seg - 1) / seg, nsub = (seg + CS_ROWS - 1) / CS_ROWS;
-  hipLaunchKernelGGL(colsum_part_kernel, dim3((C + 255) / 256, nseg * nsub), dim3(256), 0, st, a, b, rows, C, seg,
+  MT_REQUIRE((size_t)nseg * nsub <= 65535u * 64, "colsum: too many partial blocks");
+  hipLaunchKernelGGL(colsum_part_kernel, dim3((C + 63) / 64, nseg * nsub), dim3(256), 0, st, a, b, rows, C, seg,
                      nsub, scratch);
-  hipLaunchKernelGGL(colsum_merge_kernel, dim3((C + 255) / 256, nseg), dim3(256), 0, st, (const float*)scratch, C,
+  hipLaunchKernelGGL(colsum_merge_kernel, dim3((C + 63) / 64, nseg), dim3(256), 0, st, (const float*)scratch, C,
                      nsub, out, accumulate);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
@@ -520,17 +550,27 @@ __global__ __launch_bounds__(256) void gn_bwd_kernel(const float* __restrict__ d
     const float xh = (x[o] - m) * r;
     dx[o] = r * (gamma[c] * dy[o] - a1 - xh * a2);
   }
-  // per-(b, c) parameter-gradient partials: thread per channel of the group, frames in order
-  for (int cc = threadIdx.x; cc < cg; cc += 256) {
-    const int c = g * cg + cc;
-    float pg = 0.f, pb = 0.f;
-    for (int t = 0; t < T; ++t) {
-      const size_t o = ((size_t)b * T + t) * C + c;
+  // per-(b, c) parameter-gradient partials: 256 / cg frame lanes per channel, lanes combined in lane order
+  __syncthreads();
+  const int nl = 256 / cg, cc = threadIdx.x % cg, tl = threadIdx.x / cg;
+  float pg = 0.f, pb = 0.f;
+  if (tl < nl)
+    for (int t = tl; t < T; t += nl) {
+      const size_t o = ((size_t)b * T + t) * C + g * cg + cc;
       pg += dy[o] * (x[o] - m) * r;
       pb += dy[o];
     }
-    dgp[(size_t)b * C + c] = pg;
-    dbp[(size_t)b * C + c] = pb;
+  red[0][threadIdx.x] = pg;
+  red[1][threadIdx.x] = pb;
+  __syncthreads();
+  if (threadIdx.x < cg) {
+    float sg = 0.f, sbb = 0.f;
+    for (int l = 0; l < nl; ++l) {
+      sg += red[0][l * cg + threadIdx.x];
+      sbb += red[1][l * cg + threadIdx.x];
+    }
+    dgp[(size_t)b * C + g * cg + threadIdx.x] = sg;
+    dbp[(size_t)b * C + g * cg + threadIdx.x] = sbb;
   }
 }
 
@@ -544,7 +584,8 @@ int groupnorm_fwd(const float* x, const float* gamma, const float* beta, int B, 
 
 int groupnorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd, int B,
                   int T, int C, int G, float* dx, float* dgp, float* dbp, hipStream_t st) {
-  MT_REQUIRE(dy && x && gamma && mean && rstd && dx && dgp && dbp && C % G == 0, "groupnorm_bwd: args");
+  MT_REQUIRE(dy && x && gamma && mean && rstd && dx && dgp && dbp && C % G == 0 && C / G <= 256,
+             "groupnorm_bwd: args");
   hipLaunchKernelGGL(gn_bwd_kernel, dim3(G, B), dim3(256), 0, st, dy, x, gamma, mean, rstd, T, C, G, dx, dgp, dbp);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
@@ -762,15 +803,20 @@ __global__ void embed_fwd_kernel(const long long* __restrict__ ids, size_t ntok,
     out[i] = table[(size_t)ids[i / C] * C + i % C] * scale;
 }
 
-// dtable[v][c] = scale * sum over tokens with id v of dout[tok][c]: one thread per (v, c), tokens in order
-__global__ void embed_bwd_kernel(const long long* __restrict__ ids, size_t ntok, const float* __restrict__ dout,
-                                 int V, int C, float scale, float* __restrict__ dtable) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x, v = blockIdx.y;
-  if (c >= C) return;
+// dtable[v][c] = scale * sum over tokens with id v of dout[tok][c]: a 256-thread block per (v, 64 columns), 4 token
+// lanes per column, lanes combined in order (deterministic)
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const long long* __restrict__ ids, size_t ntok,
+                                                        const float* __restrict__ dout, int V, int C, float scale,
+                                                        float* __restrict__ dtable) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, lr = threadIdx.x >> 6, c = blockIdx.x * 64 + cl, v = blockIdx.y;
   float s = 0.f;
-  for (size_t t = 0; t < ntok; ++t)
-    if (ids[t] == v) s += dout[t * C + c];
-  dtable[(size_t)v * C + c] = s * scale;
+  if (c < C)
+    for (size_t t = lr; t < ntok; t += 4)
+      if (ids[t] == v) s += dout[t * C + c];
+  red[lr][cl] = s;
+  __syncthreads();
+  if (lr == 0 && c < C) dtable[(size_t)v * C + c] = (((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl]) * scale;
 }
 
 int embed_fwd(const long long* ids, size_t ntok, const float* table, int C, float scale, float* out, hipStream_t st) {
@@ -783,7 +829,7 @@ int embed_fwd(const long long* ids, size_t ntok, const float* table, int C, floa
 int embed_bwd(const long long* ids, size_t ntok, const float* dout, int V, int C, float scale, float* dtable,
               hipStream_t st) {
   MT_REQUIRE(ids && dout && dtable && V > 0, "embed_bwd: args");
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3((C + 63) / 64, V), dim3(64), 0, st, ids, ntok, dout, V, C, scale, dtable);
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3((C + 63) / 64, V), dim3(256), 0, st, ids, ntok, dout, V, C, scale, dtable);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }

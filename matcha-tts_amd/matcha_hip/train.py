@@ -42,15 +42,35 @@ def empty(*shape, like) -> torch.Tensor:
     return torch.empty(*shape, dtype=torch.float32, device=like.device)
 
 
+class _Scratch:
+    """grow-only stream-ordered scratch (column-sum partials)"""
+    buf: Optional[torch.Tensor] = None
+
+    @classmethod
+    def get(cls, n, like):
+        if cls.buf is None or cls.buf.numel() < n or cls.buf.device != like.device:
+            cls.buf = empty(max(n, 4096), like=like)
+        return cls.buf
+
+
+class _GemmWS(_Scratch):
+    """split-K partials of mtt_gemm"""
+    buf: Optional[torch.Tensor] = None
+
+
 def gemm(A, B, M, N, K, out, ta=0, tb=0, alpha=1.0, beta=0.0, lda=None, ldb=None, ldc=None, batch=1, sA=0, sB=0,
-         sC=0, a_off=0, b_off=0, c_off=0):
-    """out = alpha op(A) op(B) + beta out, row-major; op(A) M x K, op(B) K x N; offsets in elements."""
+         sC=0, a_off=0, b_off=0, c_off=0, bias=None, rmask=None):
+    """out = (alpha op(A) op(B) + beta out + bias[n]) * rmask[m], row-major; op(A) M x K, op(B) K x N; offsets in
+    elements. Long-K / few-tile shapes split K over slices in a workspace (summed in slice order)."""
     lda = lda if lda is not None else (M if ta else K)
     ldb = ldb if ldb is not None else (K if tb else N)
     ldc = ldc if ldc is not None else N
-    check(lib().mtt_gemm(int(ta), int(tb), M, N, K, float(alpha), A.data_ptr() + 4 * a_off, lda, sA,
-                         B.data_ptr() + 4 * b_off, ldb, sB, float(beta), out.data_ptr() + 4 * c_off, ldc, sC, batch,
-                         _s(out)), "gemm")
+    L = lib()
+    wsb = L.mtt_gemm_workspace_bytes(M, N, K, batch)
+    ws = _GemmWS.get(wsb // 4, out) if wsb else None
+    check(L.mtt_gemm(int(ta), int(tb), M, N, K, float(alpha), A.data_ptr() + 4 * a_off, lda, sA,
+                     B.data_ptr() + 4 * b_off, ldb, sB, float(beta), out.data_ptr() + 4 * c_off, ldc, sC, batch,
+                     ptr(bias), ptr(rmask), ptr(ws), wsb, _s(out)), "gemm")
     return out
 
 
@@ -150,16 +170,6 @@ def split_cols(d, Ca):
     return a, b
 
 
-class _Scratch:
-    buf: Optional[torch.Tensor] = None
-
-    @classmethod
-    def get(cls, n, like):
-        if cls.buf is None or cls.buf.numel() < n or cls.buf.device != like.device:
-            cls.buf = empty(max(n, 4096), like=like)
-        return cls.buf
-
-
 def colsum(a, C, out, b=None, seg=None, acc=False):
     rows = a.numel() // C
     seg = rows if seg is None else seg
@@ -194,14 +204,12 @@ def seq_mask(lengths, T, like):
 
 
 # ---------------------------------------------------------------------------------------- layer blocks
-def linear_fwd(x, W, b):
-    """x [N][I] -> x W^T + b [N][O] (nn.Linear, Conv1d k=1 with W [O][I][1])"""
+def linear_fwd(x, W, b, rmask=None):
+    """x [N][I] -> (x W^T + b) * rmask [N][O] (nn.Linear, Conv1d k=1 with W [O][I][1]; bias and the output row mask
+    in the GEMM epilogue)"""
     I = x.shape[-1]
     N, O = x.numel() // I, W.shape[0]
-    y = mm(x, W, N, O, I, tb=1)
-    if b is not None:
-        ew(AXPBY, y, y, b, bc=bc_col(O))
-    return y
+    return mm(x, W, N, O, I, tb=1, bias=b, rmask=rmask)
 
 
 def linear_bwd(dy, x, W, gW, gb, need_dx=True):
@@ -213,21 +221,22 @@ def linear_bwd(dy, x, W, gW, gb, need_dx=True):
     return mm(dy, W, N, I, O) if need_dx else None
 
 
-def conv_fwd(x, W, b, stride=1, pad=0, dil=1):
-    """Conv1d: x [B][T][Cin], W [Cout][Cin][k] -> [B][Tout][Cout]; ctx keeps the columns"""
+def conv_fwd(x, W, b, stride=1, pad=0, dil=1, mask=None, out_mask=None):
+    """Conv1d of (x * mask): x [B][T][Cin], W [Cout][Cin][k] -> (conv + b) * out_mask [B][Tout][Cout]; the input mask
+    is applied while building the columns, bias and output mask in the GEMM epilogue; ctx keeps the columns"""
     B, T, Cin = x.shape
     Cout, _, k = W.shape
     Tout = (T + 2 * pad - dil * (k - 1) - 1) // stride + 1
     cols = empty(B * Tout, Cin * k, like=x)
-    check(lib().mtt_im2col(x.data_ptr(), B, T, Cin, k, stride, pad, dil, Tout, cols.data_ptr(), _s(x)), "im2col")
-    y = mm(cols, W, B * Tout, Cout, Cin * k, tb=1).view(B, Tout, Cout)
-    if b is not None:
-        ew(AXPBY, y, y, b, bc=bc_col(Cout))
-    return y, (cols, B, T, Cin, k, stride, pad, dil, Tout)
+    check(lib().mtt_im2col(x.data_ptr(), ptr(mask), B, T, Cin, k, stride, pad, dil, Tout, cols.data_ptr(), _s(x)),
+          "im2col")
+    y = mm(cols, W, B * Tout, Cout, Cin * k, tb=1, bias=b, rmask=out_mask).view(B, Tout, Cout)
+    return y, (cols, B, T, Cin, k, stride, pad, dil, Tout, mask)
 
 
 def conv_bwd(dy, ctx, W, gW, gb, need_dx=True):
-    cols, B, T, Cin, k, stride, pad, dil, Tout = ctx
+    """-> d x (times the forward's input mask); weight / bias gradients into gW / gb"""
+    cols, B, T, Cin, k, stride, pad, dil, Tout, mask = ctx
     Cout = W.shape[0]
     gemm(dy, cols, Cout, Cin * k, B * Tout, gW, ta=1)
     if gb is not None:
@@ -236,7 +245,8 @@ def conv_bwd(dy, ctx, W, gW, gb, need_dx=True):
         return None
     dcols = mm(dy, W, B * Tout, Cin * k, Cout)
     dx = empty(B, T, Cin, like=dy)
-    check(lib().mtt_col2im(dcols.data_ptr(), B, T, Cin, k, stride, pad, dil, Tout, dx.data_ptr(), 0, _s(dy)), "col2im")
+    check(lib().mtt_col2im(dcols.data_ptr(), ptr(mask), B, T, Cin, k, stride, pad, dil, Tout, dx.data_ptr(), 0,
+                           _s(dy)), "col2im")
     return dx
 
 
@@ -248,7 +258,8 @@ def convT_fwd(x, W, b, stride, pad):
     Tout = (Tin - 1) * stride - 2 * pad + k
     dcols = mm(x, W, B * Tin, Cout * k, Cin)
     y = empty(B, Tout, Cout, like=x)
-    check(lib().mtt_col2im(dcols.data_ptr(), B, Tout, Cout, k, stride, pad, 1, Tin, y.data_ptr(), 0, _s(x)), "col2im")
+    check(lib().mtt_col2im(dcols.data_ptr(), None, B, Tout, Cout, k, stride, pad, 1, Tin, y.data_ptr(), 0, _s(x)),
+          "col2im")
     if b is not None:
         ew(AXPBY, y, y, b, bc=bc_col(Cout))
     return y, (x, B, Tin, Cin, Cout, k, stride, pad, Tout)
@@ -257,7 +268,8 @@ def convT_fwd(x, W, b, stride, pad):
 def convT_bwd(dy, ctx, W, gW, gb):
     x, B, Tin, Cin, Cout, k, stride, pad, Tout = ctx
     cols = empty(B * Tin, Cout * k, like=dy)
-    check(lib().mtt_im2col(dy.data_ptr(), B, Tout, Cout, k, stride, pad, 1, Tin, cols.data_ptr(), _s(dy)), "im2col")
+    check(lib().mtt_im2col(dy.data_ptr(), None, B, Tout, Cout, k, stride, pad, 1, Tin, cols.data_ptr(), _s(dy)),
+          "im2col")
     gemm(x, cols, Cin, Cout * k, B * Tin, gW, ta=1)
     if gb is not None:
         colsum(dy, Cout, gb)
@@ -462,7 +474,7 @@ class EstimatorTrainer:
 
     def block1d_fwd(self, p, x, m):  # model.py:764-775
         P = self.P
-        y, cc = conv_fwd(mul_rows(x, m), P[p + ".block.0.weight"], P[p + ".block.0.bias"], pad=1)
+        y, cc = conv_fwd(x, P[p + ".block.0.weight"], P[p + ".block.0.bias"], pad=1, mask=m)
         g, gc = gn_fwd(y, P[p + ".block.1.weight"], P[p + ".block.1.bias"])
         return mul_rows(act(MISH, g), m), (m, cc, gc, g)
 
@@ -473,7 +485,7 @@ class EstimatorTrainer:
         d = gn_bwd(d, gc, P[p + ".block.1.weight"], G.view[p + ".block.1.weight"], G.view[p + ".block.1.bias"])
         d = conv_bwd(d, cc, P[p + ".block.0.weight"], G.view[p + ".block.0.weight"], G.view[p + ".block.0.bias"])
         G.done(p + ".block.1.weight", p + ".block.1.bias", p + ".block.0.weight", p + ".block.0.bias")
-        return mul_rows(d, m)
+        return d
 
     def resnet_fwd(self, p, x, m, mtemb):  # model.py:777-790
         P = self.P
@@ -573,12 +585,12 @@ class EstimatorTrainer:
         h, c["d0r"] = self.resnet_fwd("down_blocks.0.0", h, m0, mtemb)
         h, c["d0t"] = self.tblock_fwd("down_blocks.0.1.0", h, m0, seed + 1)
         h0 = h
-        h, c["d0c"] = conv_fwd(mul_rows(h, m0), P["down_blocks.0.2.conv.weight"], P["down_blocks.0.2.conv.bias"],
-                               stride=2, pad=1)
+        h, c["d0c"] = conv_fwd(h, P["down_blocks.0.2.conv.weight"], P["down_blocks.0.2.conv.bias"], stride=2, pad=1,
+                               mask=m0)
         h, c["d1r"] = self.resnet_fwd("down_blocks.1.0", h, m1, mtemb)
         h, c["d1t"] = self.tblock_fwd("down_blocks.1.1.0", h, m1, seed + 3)
         hd1 = h
-        h, c["d1c"] = conv_fwd(mul_rows(h, m1), P["down_blocks.1.2.weight"], P["down_blocks.1.2.bias"], pad=1)
+        h, c["d1c"] = conv_fwd(h, P["down_blocks.1.2.weight"], P["down_blocks.1.2.bias"], pad=1, mask=m1)
         for i in range(self.n_mid):
             h, c[f"m{i}r"] = self.resnet_fwd(f"mid_blocks.{i}.0", h, m1, mtemb)
             h, c[f"m{i}t"] = self.tblock_fwd(f"mid_blocks.{i}.1.0", h, m1, seed + 5 + 2 * i)
@@ -589,11 +601,10 @@ class EstimatorTrainer:
         h = cat_cols(h, h0)
         h, c["u1r"] = self.resnet_fwd("up_blocks.1.0", h, m0, mtemb)
         h, c["u1t"] = self.tblock_fwd("up_blocks.1.1.0", h, m0, seed + 63)
-        h, c["u1c"] = conv_fwd(mul_rows(h, m0), P["up_blocks.1.2.weight"], P["up_blocks.1.2.bias"], pad=1)
+        h, c["u1c"] = conv_fwd(h, P["up_blocks.1.2.weight"], P["up_blocks.1.2.bias"], pad=1, mask=m0)
         h, c["fb"] = self.block1d_fwd("final_block", h, m0)
         c["fp_in"] = mul_rows(h, m0)
-        out = linear_fwd(c["fp_in"], P["final_proj.weight"], P["final_proj.bias"]).view(B, T, F)
-        return mul_rows(out, m0), c
+        return linear_fwd(c["fp_in"], P["final_proj.weight"], P["final_proj.bias"], rmask=m0).view(B, T, F), c
 
     def backward(self, dpred, c, G):
         """dpred [B][T][80] -> d mu [B][T][80]; parameter gradients into G (estimator-relative names)."""
@@ -605,8 +616,8 @@ class EstimatorTrainer:
                        G.view["final_proj.bias"])
         G.done("final_proj.weight", "final_proj.bias")
         d = self.block1d_bwd("final_block", mul_rows(d, m0).view(B, T, -1), c["fb"], G)
-        d = mul_rows(conv_bwd(d, c["u1c"], P["up_blocks.1.2.weight"], G.view["up_blocks.1.2.weight"],
-                              G.view["up_blocks.1.2.bias"]), m0)
+        d = conv_bwd(d, c["u1c"], P["up_blocks.1.2.weight"], G.view["up_blocks.1.2.weight"],
+                     G.view["up_blocks.1.2.bias"])
         G.done("up_blocks.1.2.weight", "up_blocks.1.2.bias")
         d = self.tblock_bwd("up_blocks.1.1.0", d, c["u1t"], G)
         d = self.resnet_bwd("up_blocks.1.0", d, c["u1r"], G, mtemb, dmtemb)
@@ -620,14 +631,14 @@ class EstimatorTrainer:
         for i in reversed(range(self.n_mid)):
             d = self.tblock_bwd(f"mid_blocks.{i}.1.0", d, c[f"m{i}t"], G)
             d = self.resnet_bwd(f"mid_blocks.{i}.0", d, c[f"m{i}r"], G, mtemb, dmtemb)
-        d = mul_rows(conv_bwd(d, c["d1c"], P["down_blocks.1.2.weight"], G.view["down_blocks.1.2.weight"],
-                              G.view["down_blocks.1.2.bias"]), m1)
+        d = conv_bwd(d, c["d1c"], P["down_blocks.1.2.weight"], G.view["down_blocks.1.2.weight"],
+                     G.view["down_blocks.1.2.bias"])
         G.done("down_blocks.1.2.weight", "down_blocks.1.2.bias")
         add(d, dhd1, out=d)
         d = self.tblock_bwd("down_blocks.1.1.0", d, c["d1t"], G)
         d = self.resnet_bwd("down_blocks.1.0", d, c["d1r"], G, mtemb, dmtemb)
-        d = mul_rows(conv_bwd(d, c["d0c"], P["down_blocks.0.2.conv.weight"], G.view["down_blocks.0.2.conv.weight"],
-                              G.view["down_blocks.0.2.conv.bias"]), m0)
+        d = conv_bwd(d, c["d0c"], P["down_blocks.0.2.conv.weight"], G.view["down_blocks.0.2.conv.weight"],
+                     G.view["down_blocks.0.2.conv.bias"])
         G.done("down_blocks.0.2.conv.weight", "down_blocks.0.2.conv.bias")
         add(d, dh0, out=d)
         d = self.tblock_bwd("down_blocks.0.1.0", d, c["d0t"], G)
@@ -680,7 +691,7 @@ class EncoderTrainer:
             org, pre = h, []
             for i in range(3):
                 W = P[f"prenet.conv_layers.{i}.weight"]
-                y, cc = conv_fwd(mul_rows(h, xm), W, P[f"prenet.conv_layers.{i}.bias"], pad=W.shape[-1] // 2)
+                y, cc = conv_fwd(h, W, P[f"prenet.conv_layers.{i}.bias"], pad=W.shape[-1] // 2, mask=xm)
                 n, lc = self.cln(y, f"prenet.norm_layers.{i}")
                 h = dropout(act(RELU, n), self.p_pre, seed + i)
                 pre.append((cc, lc, n))
@@ -699,23 +710,23 @@ class EncoderTrainer:
             y = linear_fwd(o, P[a + ".conv_o.weight"], P[a + ".conv_o.bias"]).view(B, Tx, C)
             h1, l1 = self.cln(add(hm, dropout(y, self.p, s + 1)), f"encoder.norm_layers_1.{i}")
             f = f"encoder.ffn_layers.{i}"
-            f1, c1 = conv_fwd(mul_rows(h1, xm), P[f + ".conv_1.weight"], P[f + ".conv_1.bias"], pad=self.k // 2)
+            f1, c1 = conv_fwd(h1, P[f + ".conv_1.weight"], P[f + ".conv_1.bias"], pad=self.k // 2, mask=xm)
             rd = dropout(act(RELU, f1), self.p, s + 2)
-            f2, c2 = conv_fwd(mul_rows(rd, xm), P[f + ".conv_2.weight"], P[f + ".conv_2.bias"], pad=self.k // 2)
-            f2 = mul_rows(f2, xm)
+            f2, c2 = conv_fwd(rd, P[f + ".conv_2.weight"], P[f + ".conv_2.bias"], pad=self.k // 2, mask=xm,
+                              out_mask=xm)
             h, l2 = self.cln(add(h1, dropout(f2, self.p, s + 3)), f"encoder.norm_layers_2.{i}")
             layers.append((hm, ac, o, l1, c1, f1, c2, l2))
         c["layers"] = layers
         hm = mul_rows(h, xm)
         c["hm"] = hm
-        mu = mul_rows(linear_fwd(hm, P["proj_m.weight"], P["proj_m.bias"]).view(B, Tx, -1), xm)
+        mu = linear_fwd(hm, P["proj_m.weight"], P["proj_m.bias"], rmask=xm).view(B, Tx, -1)
         d1, dc1 = conv_fwd(hm, P["proj_w.conv_1.weight"], P["proj_w.conv_1.bias"], pad=self.kd // 2)
         n1, dl1 = self.cln(act(RELU, d1), "proj_w.norm_1")
-        d2, dc2 = conv_fwd(mul_rows(dropout(n1, self.p_dp, seed + 50), xm), P["proj_w.conv_2.weight"],
-                           P["proj_w.conv_2.bias"], pad=self.kd // 2)
+        d2, dc2 = conv_fwd(dropout(n1, self.p_dp, seed + 50), P["proj_w.conv_2.weight"], P["proj_w.conv_2.bias"],
+                           pad=self.kd // 2, mask=xm)
         n2, dl2 = self.cln(act(RELU, d2), "proj_w.norm_2")
         n2m = mul_rows(dropout(n2, self.p_dp, seed + 51), xm)
-        logw = mul_rows(linear_fwd(n2m, P["proj_w.proj.weight"], P["proj_w.proj.bias"]), xm).view(B, Tx)
+        logw = linear_fwd(n2m, P["proj_w.proj.weight"], P["proj_w.proj.bias"], rmask=xm).view(B, Tx)
         c["dp"] = (d1, dc1, dl1, d2, dc2, dl2, n2m)
         return mu, logw, xm, c
 
@@ -730,8 +741,8 @@ class EncoderTrainer:
                           G.view["proj_w.proj.weight"], G.view["proj_w.proj.bias"]).view(B, Tx, -1)
         dn2 = dropout(mul_rows(dn2m, xm), self.p_dp, seed + 51)
         dd2 = act_bwd(RELU_B, d2, self.cln_bwd(dn2, dl2, "proj_w.norm_2", G))
-        dn1 = mul_rows(conv_bwd(dd2, dc2, P["proj_w.conv_2.weight"], G.view["proj_w.conv_2.weight"],
-                                G.view["proj_w.conv_2.bias"]), xm)
+        dn1 = conv_bwd(dd2, dc2, P["proj_w.conv_2.weight"], G.view["proj_w.conv_2.weight"],
+                       G.view["proj_w.conv_2.bias"])
         dd1 = act_bwd(RELU_B, d1, self.cln_bwd(dropout(dn1, self.p_dp, seed + 50), dl1, "proj_w.norm_1", G))
         conv_bwd(dd1, dc1, P["proj_w.conv_1.weight"], G.view["proj_w.conv_1.weight"], G.view["proj_w.conv_1.bias"],
                  need_dx=False)
@@ -745,11 +756,10 @@ class EncoderTrainer:
             hm, ac, o, l1, c1, f1, c2, l2 = c["layers"][i]
             ds = self.cln_bwd(dh, l2, f"encoder.norm_layers_2.{i}", G)  # d(h1 + drop(ffn))
             df2 = mul_rows(dropout(ds, self.p, s + 3), xm)
-            drd = mul_rows(conv_bwd(df2, c2, P[f + ".conv_2.weight"], G.view[f + ".conv_2.weight"],
-                                    G.view[f + ".conv_2.bias"]), xm)
+            drd = conv_bwd(df2, c2, P[f + ".conv_2.weight"], G.view[f + ".conv_2.weight"], G.view[f + ".conv_2.bias"])
             df1 = act_bwd(RELU_B, f1, dropout(drd, self.p, s + 2))
-            dh1 = add(ds, mul_rows(conv_bwd(df1, c1, P[f + ".conv_1.weight"], G.view[f + ".conv_1.weight"],
-                                            G.view[f + ".conv_1.bias"]), xm))
+            dh1 = add(ds, conv_bwd(df1, c1, P[f + ".conv_1.weight"], G.view[f + ".conv_1.weight"],
+                                   G.view[f + ".conv_1.bias"]))
             ds1 = self.cln_bwd(dh1, l1, f"encoder.norm_layers_1.{i}", G)  # d(hm + drop(attn))
             do = linear_bwd(dropout(ds1, self.p, s + 1), o, P[a + ".conv_o.weight"], G.view[a + ".conv_o.weight"],
                             G.view[a + ".conv_o.bias"]).view(B, Tx, C)
@@ -770,9 +780,8 @@ class EncoderTrainer:
                 cc, lc, n = c["pre"][i]
                 dn = act_bwd(RELU_B, n, dropout(drd, self.p_pre, seed + i))
                 dy = self.cln_bwd(dn, lc, f"prenet.norm_layers.{i}", G)
-                drd = mul_rows(conv_bwd(dy, cc, P[f"prenet.conv_layers.{i}.weight"],
-                                        G.view[f"prenet.conv_layers.{i}.weight"],
-                                        G.view[f"prenet.conv_layers.{i}.bias"]), xm)
+                drd = conv_bwd(dy, cc, P[f"prenet.conv_layers.{i}.weight"], G.view[f"prenet.conv_layers.{i}.weight"],
+                               G.view[f"prenet.conv_layers.{i}.bias"])
             dh = add(dorg, drd)
             G.done_prefix("prenet.")
         check(lib().mtt_embed_bwd(c["ids"].data_ptr(), B * Tx, dh.data_ptr(), P["emb.weight"].shape[0], C,
