@@ -831,12 +831,21 @@ class MatchaTrainer:
         enc_P = {k[len("encoder."):]: v for k, v in self.params.view.items() if k.startswith("encoder.")}
         est_P = {k[len("decoder.estimator."):]: v for k, v in self.params.view.items()
                  if k.startswith("decoder.estimator.")}
-        on = 1.0 if dropout else 0.0
-        self.enc = EncoderTrainer(enc_P, int(hp["n_layers"]), int(hp["n_heads"]), 0.1 * on, 0.5 * on, 0.1 * on)
-        self.est = EstimatorTrainer(est_P, heads, 0.05 * on)
+        self.enc = EncoderTrainer(enc_P, int(hp["n_layers"]), int(hp["n_heads"]))
+        self.est = EstimatorTrainer(est_P, heads)
+        self.set_dropout(dropout)
         self.lr, self.sigma_min, self.prior, self.clip = lr, sigma_min, prior_loss, grad_clip
         self.step_count, self.seed = 0, seed
         self.last: Dict[str, torch.Tensor] = {}
+
+    def set_dropout(self, enabled: bool):
+        """train (True: p = 0.1 encoder / 0.5 prenet / 0.1 duration predictor / 0.05 estimator, train_standalone.py:
+        775-800, model.py:481) or eval (False: identity) dropout"""
+        on = 1.0 if enabled else 0.0
+        self.enc.p, self.enc.p_pre, self.enc.p_dp = 0.1 * on, 0.5 * on, 0.1 * on
+        self.est.p_drop = 0.05 * on
+        self.dropout = bool(enabled)
+        return self
 
     def parameters(self) -> Dict[str, torch.Tensor]:
         return dict(self.params.view)
@@ -845,11 +854,12 @@ class MatchaTrainer:
         return dict(self.grads.view)
 
     def forward_backward(self, x, x_lengths, y, y_lengths, t: Optional[torch.Tensor] = None,
-                         z: Optional[torch.Tensor] = None):
+                         z: Optional[torch.Tensor] = None, backward: bool = True):
         """train_standalone.py:623-667 + the backward of dur + prior + cfm. x int64 [B][Tx], y [B][80][Ty]
         (Ty % 4 == 0, the collate's fix_len_compatibility), lengths int64 [B]; t [B] / z [B][80][Ty] default to
         the reference's draws (torch.rand, torch.randn_like). Leaves the all-reduced (summed over ranks)
-        gradients in the flat buffer; returns the losses as device scalars."""
+        gradients in the flat buffer; returns the losses as device scalars. backward=False: losses only
+        (validation_step)."""
         rt.require_gpu(x, y, what="MatchaTrainer")
         B, Tx = x.shape
         F, Ty = y.shape[1], y.shape[2]
@@ -902,6 +912,11 @@ class MatchaTrainer:
         inv_nx = ew(RECIP, empty(1, like=y), total(xm), alpha=1.0)
         dur = mul_scalar(total(dl, dl), inv_nx)
         dlogw = mul_scalar(dl, inv_nx, alpha=2.0)
+        if not backward:
+            loss = add(add(dur, prior), cfm)
+            self.last = {"loss": loss, "dur_loss": dur, "prior_loss": prior, "cfm_loss": cfm, "attn": attn,
+                         "log_prior": lp}
+            return self.last
         # ---- backward
         dmu_y = self.est.backward(dpred, dctx, Grads(self.grads, "decoder.estimator.", self.buckets))
         if self.prior:

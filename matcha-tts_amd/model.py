@@ -439,8 +439,8 @@ class BASECFM(nn.Module):
     def compute_loss(self, x1, mask, mu, spks=None, cond=None):
         """model.py:1147-1162 -> (loss, y_t, pred, u_t): t ~ U(0,1) and z ~ N(0,1) per utterance on the
         device, one batched estimator evaluation with a time per utterance (mt_decoder_step_times).
-        Forward only: the estimator has no backward kernels yet, so the loss carries no gradient
-        (validation-loss use; training is the rest of SURVEY.md §8f row 3)."""
+        Forward only (bf16 / fp32 inference estimator, no autograd graph): the training step with its
+        hand-written backward is matcha_hip.train.MatchaTrainer (train_standalone.MatchaLightningModule)."""
         b = mu.shape[0]
         t = torch.rand([b, 1, 1], device=mu.device, dtype=mu.dtype)
         z = torch.randn_like(x1)
@@ -492,7 +492,11 @@ class MatchaTTS(nn.Module):
         return self
 
     def forward(self, x, x_lengths, y, y_lengths, spks=None):
-        raise NotImplementedError("the training forward (model.py:1234-1262) is outside this round's hot path")
+        # The reference's MatchaTTS.forward (model.py:1234-1262) is a placeholder: it feeds text-length mu and the
+        # text mask to CFM.compute_loss against mel-length y (model.py:1254-1260). The reference trains through
+        # MatchaLightningModule.forward (train_standalone.py:623-667) instead, whose drop-in runs on the GPU.
+        raise NotImplementedError("train through train_standalone.MatchaLightningModule (the reference's training "
+                                  "path, train_standalone.py:580-707); MatchaTTS.forward is a placeholder upstream")
 
     @torch.inference_mode()
     def synthesize(self, x, x_lengths, n_timesteps, temperature=1.0, spks=None, length_scale=1.0):

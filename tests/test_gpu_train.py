@@ -33,19 +33,23 @@ def _rel(a, b):
                                                (1, 1, 17, 9, 3, 1), (0, 0, 300, 260, 132, 2),
                                                (1, 0, 40, 70, 5000, 1), (0, 1, 200, 96, 3001, 1)])
 def test_gemm_f32(ta, tb, M, N, K, batch):
-    """vector (aligned leading dimensions) and scalar loads, partial tiles, batch strides, and the split-K path
-    (the last two cases: few tiles, long K, per-slice partials summed in order)"""
+    """vector (aligned leading dimensions) and scalar loads, partial tiles, batch strides, the bias / row-mask
+    epilogue, and the split-K path (the last two cases: few tiles, long K, per-slice partials summed in order,
+    epilogue in the reduction)"""
     tr = _tr()
     g = torch.Generator().manual_seed(M * N + K)
     A = torch.randn(batch, *((K, M) if ta else (M, K)), generator=g)
     B = torch.randn(batch, *((N, K) if tb else (K, N)), generator=g)
     C0 = torch.randn(batch, M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    rmask = (torch.rand(batch, M, generator=g) > 0.3).float()
     out = C0.clone().to(DEV)
+    bias_d, rmask_d = bias.to(DEV), rmask.to(DEV)
     tr.gemm(A.to(DEV), B.to(DEV), M, N, K, out, ta=ta, tb=tb, alpha=0.5, beta=-1.0, batch=batch,
-            sA=A[0].numel(), sB=B[0].numel(), sC=M * N)
+            sA=A[0].numel(), sB=B[0].numel(), sC=M * N, bias=bias_d, rmask=rmask_d)
     Ad = A.double().transpose(1, 2) if ta else A.double()
     Bd = B.double().transpose(1, 2) if tb else B.double()
-    ref = 0.5 * Ad @ Bd - C0.double()
+    ref = (0.5 * Ad @ Bd - C0.double() + bias.double()) * rmask.double()[:, :, None]
     assert _rel(out, ref) < 2e-6
 
 
@@ -338,3 +342,37 @@ def test_training_with_dropout_is_deterministic_and_learns():
             assert la != ev and math.isfinite(la)
         losses.append(la)
     assert np.mean(losses[-3:]) < np.mean(losses[:3]), losses
+
+
+def test_lightning_module_drop_in():
+    """train_standalone.MatchaLightningModule (the drop-in for train_standalone.py:580-707): validation_step draws
+    t and z exactly as the reference does (torch.rand, then torch.randn_like on the device RNG) and matches the
+    oracle's losses for those draws; training_step + optimizer.step() update model.MatchaTTS's own parameters."""
+    from types import SimpleNamespace
+
+    import train_standalone as TS
+    from conftest import DEC, DP, ENC
+    sd, x, xl, y, yl, _, _ = _setup(seed=24)
+    mod = TS.MatchaLightningModule(178, 1, 64, SimpleNamespace(**ENC), SimpleNamespace(**DEC),
+                                   {"solver": "euler", "sigma_min": 1e-4}, SimpleNamespace(**DP),
+                                   {"mel_mean": 0.0, "mel_std": 1.0})
+    mod.model.load_state_dict(sd)
+    mod.to(DEV)
+    batch = {"x": x.to(DEV), "x_lengths": xl.to(DEV), "y": y.to(DEV), "y_lengths": yl.to(DEV)}
+    torch.manual_seed(99)
+    t = torch.rand([3, 1, 1], device=DEV)
+    z = torch.randn_like(batch["y"])
+    torch.manual_seed(99)
+    val = mod.validation_step(batch, 0).item()
+    (dur, prior, cfm, _, _), _ = _oracle_grads(sd, x, xl, y, yl, t.view(3).cpu(), z.cpu())
+    ref = (dur + prior + cfm).item()
+    assert abs(val - ref) <= 1e-4 * abs(ref), (val, ref)
+    opt = mod.configure_optimizers()
+    w0 = mod.model.state_dict()["decoder.estimator.final_proj.weight"].clone()
+    loss = mod.training_step(batch, 0)
+    assert math.isfinite(loss.item()) and set(mod.logged) >= {"train/loss", "val/loss"}
+    opt.step()
+    opt.zero_grad()
+    w1 = mod.model.state_dict()["decoder.estimator.final_proj.weight"]
+    assert not torch.equal(w0, w1)
+    assert torch.equal(w1, mod.trainer().parameters()["decoder.estimator.final_proj.weight"])
