@@ -48,10 +48,13 @@ def parse():
     p.add_argument("--cpu-utterances", type=int, default=3, help="CPU baseline sample size (batch 1)")
     p.add_argument("--no-north-star", action="store_true", help="skip the B=256 single-GPU record")
     p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--model", default="lj", choices=["lj", "vctk"],
+                   help="lj: single speaker (configs[1..2]); vctk: 109 speakers with the speaker-embedding "
+                        "condition (configs[3]: B=128 over 8 GPUs = 16/GPU, 20 ODE steps)")
     return p.parse_args()
 
 
-def build_models(device, precision, seed):
+def build_models(device, precision, seed, n_spks=1):
     from types import SimpleNamespace
 
     import model
@@ -66,7 +69,7 @@ def build_models(device, precision, seed):
     dec = SimpleNamespace(channels=(256, 256), dropout=0.05, attention_head_dim=64, n_blocks=1, num_mid_blocks=2,
                           num_heads=2, act_fn="snakebeta")
     dp = SimpleNamespace(filter_channels_dp=256, kernel_size=3, p_dropout=0.1)
-    m = model.MatchaTTS(178, 1, 64, enc, dec, {"solver": "euler", "sigma_min": 1e-4}, dp, precision=precision)
+    m = model.MatchaTTS(178, n_spks, 64, enc, dec, {"solver": "euler", "sigma_min": 1e-4}, dp, precision=precision)
     sd = synthetic.make_state_dict([(k, tuple(v.shape)) for k, v in m.state_dict().items()], seed,
                                    force_log_duration=math.log(2.5))
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
@@ -90,6 +93,12 @@ def shard_inputs(rank, world, batch, seed):
     return torch.from_numpy(np.ascontiguousarray(x)), torch.from_numpy(np.ascontiguousarray(xl))
 
 
+def shard_speakers(rank, world, batch, seed, n_spks=109):
+    """speaker ids of the shard's utterances (VCTK), drawn from the same global synthetic set"""
+    ids = np.random.RandomState(seed + 17).randint(0, n_spks, size=batch * world)
+    return torch.from_numpy(ids[rank * batch:(rank + 1) * batch].astype(np.int64))
+
+
 def reduce_over_ranks(elapsed, frames, dist, device):
     """Job time = MAX of the ranks' timed regions; job work = SUM of their useful frames."""
     if dist is None:
@@ -101,8 +110,9 @@ def reduce_over_ranks(elapsed, frames, dist, device):
     return float(t.item()), int(f.item())
 
 
-def step(m, g, den, x, xl, n_ts, denoise):
-    mel, yl, attn = m.synthesize(x, xl, n_timesteps=n_ts, temperature=0.667, length_scale=1.0)
+def step(m, g, den, x, xl, n_ts, denoise, spk=None):
+    spks = m.spk_emb(spk) if spk is not None else None  # main.py: the speaker embedding of the requested ids
+    mel, yl, attn = m.synthesize(x, xl, n_timesteps=n_ts, temperature=0.667, spks=spks, length_scale=1.0)
     wav = g(mel).clamp(-1, 1)
     if denoise:
         wav = den(wav.squeeze(1), strength=0.00025)
@@ -296,17 +306,19 @@ def main():
     torch.cuda.set_device(device)
     torch.manual_seed(a.seed + rank)
 
-    m, g, den, msd, gsd = build_models(device, a.precision, a.seed)
+    vctk = a.model == "vctk"
+    m, g, den, msd, gsd = build_models(device, a.precision, a.seed, n_spks=109 if vctk else 1)
     x_cpu, xl_cpu = shard_inputs(rank, world, a.batch, a.seed)
     x, xl = x_cpu.to(device), xl_cpu.to(device)
+    spk = shard_speakers(rank, world, a.batch, a.seed).to(device) if vctk else None
     denoise = not a.no_denoise
 
     for _ in range(a.warmup):
-        step(m, g, den, x, xl, a.n_timesteps, denoise)
+        step(m, g, den, x, xl, a.n_timesteps, denoise, spk)
     torch.cuda.synchronize()
 
     # useful frames per step on this rank (deterministic durations), outside the timed region
-    _, yl, wav = step(m, g, den, x, xl, a.n_timesteps, denoise)
+    _, yl, wav = step(m, g, den, x, xl, a.n_timesteps, denoise, spk)
     yls = [int(v) for v in yl.cpu()]
     frames = int(yl.sum())
     t_y = int(yl.max())
@@ -322,7 +334,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        step(m, g, den, x, xl, a.n_timesteps, denoise)
+        step(m, g, den, x, xl, a.n_timesteps, denoise, spk)
     barrier()
     el = time.perf_counter() - t0
     probe = rt.probe_stop()
@@ -333,12 +345,14 @@ def main():
     ms_per_step = el / a.steps * 1e3
     audio_s = tot_frames * HOP / SR
     out = {
-        "metric": "mel-frames/sec + RTF, text->wav @10 ODE steps, LJSpeech model, 1/2/4/8 GPU",
+        "metric": "mel-frames/sec + RTF, text->wav @10 ODE steps, LJSpeech model, 1/2/4/8 GPU" if not vctk else
+                  f"mel-frames/sec + RTF, text->wav @{a.n_timesteps} ODE steps, VCTK 109-speaker model",
         "value": round(value, 2), "unit": "mel-frames/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": a.precision,
         "data": "synthetic (random-init weights, LJSpeech-shaped text; duration head forced to 3 frames/token)",
-        "config": {"workload": "text->wav: synthesize(10-step Euler CFM) + HiFi-GAN v1 + denoiser",
+        "config": {"workload": f"text->wav: synthesize({a.n_timesteps}-step Euler CFM) + HiFi-GAN v1 + denoiser"
+                               + (" (VCTK, speaker-embedding condition)" if vctk else ""),
                    "global_batch": a.batch * world, "batch_per_gpu": a.batch, "n_timesteps": a.n_timesteps,
                    "seq_len": t_pad, "frames_per_step": tot_frames, "parallelism": f"dp{world} (utterance shards)",
                    "denoiser": denoise},
@@ -346,12 +360,13 @@ def main():
     }
     if rank == 0:
         if world == 1:
-            default = (a.batch, a.n_timesteps, a.seed, a.no_denoise, a.precision) == (32, 10, 1234, False, "bf16")
+            default = (a.batch, a.n_timesteps, a.seed, a.no_denoise, a.precision, a.model) == \
+                (32, 10, 1234, False, "bf16", "lj")
             out["roofline"] = roofline(probe, default_workload=default)
             out["path_roofline"] = path_roofline(el / a.steps, yls, t_pad, a.n_timesteps)
-            if not a.no_north_star and a.batch != 256 and a.precision == "bf16":
+            if not a.no_north_star and a.batch != 256 and a.precision == "bf16" and not vctk:
                 out["north_star"] = north_star(m, g, den, 256, a.seed, a.n_timesteps, denoise)
-            if not a.no_cpu_baseline:
+            if not a.no_cpu_baseline and not vctk:
                 out["cpu_baseline"] = cpu_baseline(msd, gsd, x_cpu, xl_cpu, a.n_timesteps, a.cpu_utterances)
         print(json.dumps(out), flush=True)
     if dist is not None:

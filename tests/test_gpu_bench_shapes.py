@@ -137,13 +137,16 @@ def test_generator_bf16_bench_length_vs_oracle():
 
 
 # ------------------------------------------------------------------------------- (c) bench step
-def _bench_rows_vs_oracle(batch, rows, tag):
+def _bench_rows_vs_oracle(batch, rows, tag, rank=0, world=1, vctk=False, n_ts=10):
     from hifigan.config import v1
     from matcha_hip import runtime as rt
     from oracle import matcha_oracle as O
     bench = _bench()
-    m, g, den, msd, gsd = bench.build_models(torch.device(DEV), "bf16", 1234)
-    x, xl = bench.shard_inputs(0, 1, batch, 1234)
+    n_spks = 109 if vctk else 1
+    m, g, den, msd, gsd = bench.build_models(torch.device(DEV), "bf16", 1234, n_spks=n_spks)
+    x, xl = bench.shard_inputs(rank, world, batch, 1234)
+    spk = bench.shard_speakers(rank, world, batch, 1234).to(DEV) if vctk else None
+    torch.manual_seed(1234 + rank)  # bench.main's per-rank noise seed
     real = torch.randn_like
     zs = []
 
@@ -154,7 +157,7 @@ def _bench_rows_vs_oracle(batch, rows, tag):
     torch.randn_like = noise
     try:
         rt.vconv_log_start()
-        mel, yl, wav = bench.step(m, g, den, x.to(DEV), xl.to(DEV), 10, True)
+        mel, yl, wav = bench.step(m, g, den, x.to(DEV), xl.to(DEV), n_ts, True, spk)
         torch.cuda.synchronize()
         LOGS[tag] = rt.vconv_log_stop()
     finally:
@@ -167,15 +170,16 @@ def _bench_rows_vs_oracle(batch, rows, tag):
     assert z.shape[-1] == t_pad and mel.shape[-1] == t_y
     rows = sorted(set(r % batch for r in rows) | {int(yl.argmax())})
     sd = {k: v.detach().cpu() for k, v in msd.items()}
-    hp = dict(n_channels=192, n_layers=6, n_heads=2, kernel_size=3, dp_kernel_size=3, n_spks=1)
+    hp = dict(n_channels=192, n_layers=6, n_heads=2, kernel_size=3, dp_kernel_size=3, n_spks=n_spks)
+    spks = sd["spk_emb.weight"][spk.cpu()[rows]] if vctk else None
     with torch.inference_mode():
-        mu, logw, x_mask = O.text_encoder(O.sub(sd, "encoder"), x[rows], xl[rows], hp)
+        mu, logw, x_mask = O.text_encoder(O.sub(sd, "encoder"), x[rows], xl[rows], hp, spks)
         w_ceil, y_ref = O.durations(logw, x_mask)
         assert torch.equal(y_ref, yl[rows]), "duration path must be exact (forced duration head)"
         y_mask = O.sequence_mask(y_ref, t_pad).unsqueeze(1).float()
         attn = O.generate_path(w_ceil.squeeze(1), (x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)).squeeze(1))
         mu_y = torch.matmul(attn.transpose(1, 2), mu.transpose(1, 2)).transpose(1, 2)
-        zr = O.cfm_solve(O.sub(sd, "decoder.estimator"), mu_y, y_mask, 10, z[rows])
+        zr = O.cfm_solve(O.sub(sd, "decoder.estimator"), mu_y, y_mask, n_ts, z[rows], spks)
         mel_ref = O.denormalize(zr, sd["mel_mean"], sd["mel_std"])[:, :, :t_y]
         gs = {k: v.detach().cpu() for k, v in gsd.items()}
         wav_ref = O.generator_forward(gs, mel_ref, v1).clamp(-1, 1)
@@ -184,11 +188,13 @@ def _bench_rows_vs_oracle(batch, rows, tag):
     mel_r = mel.cpu()[rows]
     e_mel = rel_rms((mel_r - mean) / std, (mel_ref - mean) / std)
     e_wav = rel_rms(wav.cpu()[rows], den_ref)
-    print(f"bench step B={batch} rows {rows}: mel rel-RMS {e_mel:.3e}, denoised wav rel-RMS {e_wav:.3e}")
+    print(f"bench step {'vctk' if vctk else 'lj'} B={batch} n={n_ts} rows {rows}: mel rel-RMS {e_mel:.3e}, "
+          f"denoised wav rel-RMS {e_wav:.3e}")
     for i, r in enumerate(rows):  # every row inside its useful length, and silence-free
         n = int(yl[r]) * 256
         assert rel_rms(wav.cpu()[r, :n], den_ref[i, :n]) < 2e-2
     assert e_mel < 2e-2 and e_wav < 2e-2, (e_mel, e_wav)
+    return t_pad
 
 
 def test_bench_step_rows_vs_oracle_b32():
@@ -199,6 +205,24 @@ def test_bench_step_rows_vs_oracle_b32():
 def test_bench_step_rows_vs_oracle_b256():
     """The north-star point (B=256 on one GPU): same check on rows across the whole batch."""
     _bench_rows_vs_oracle(256, [0, 129, 255], "bench256")
+
+
+def test_bench_shard_parity_rank1_of_2():
+    """Multi-GPU per-shard parity: rank 1 of a world-2 bench job synthesises
+    utterances [32, 64) of the global set at ITS OWN padded length with its own noise seed; those rows equal the
+    oracle run on the same utterances at that T_pad. Results depend only on the shard, never on the other rank
+    (no data-path collective), so this is the whole multi-GPU parity claim; rank 0 is the B=32 test above."""
+    t1 = _bench_rows_vs_oracle(32, [1, 17, 30], "bench32_rank1", rank=1, world=2)
+    bench = _bench()
+    _, xl0 = bench.shard_inputs(0, 2, 32, 1234)
+    _, xl1 = bench.shard_inputs(1, 2, 32, 1234)
+    assert not torch.equal(xl0, xl1) and t1 % 4 == 0
+
+
+def test_bench_step_rows_vs_oracle_vctk_config4():
+    """BASELINE configs[3] per GPU: VCTK 109-speaker model with the speaker-embedding condition (the encoder and
+    the estimator both read spks), 16 utterances (= 128 over 8 GPUs), 20 ODE steps, bench step rows vs oracle."""
+    _bench_rows_vs_oracle(16, [0, 7, 15], "bench_vctk16", vctk=True, n_ts=20)
 
 
 # ------------------------------------------------------------------------------- (d) fp32 10 steps

@@ -4,8 +4,9 @@
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of wide
 coalesced reads, so it is doubled; WRITE_SIZE is exact for 16-B stores. Both are in KiB.
 Usage: python tools_pmc_traffic.py FETCH_CSV WRITE_CSV KERNEL_REGEX OUT_JSON "command"
-Only the launches with the largest grid are used (the bench workload, not the denoiser's
-bias-spectrum run on a 1 x 80 x 88 zero mel)."""
+Per kernel name, only the launches with that kernel's largest grid are used (the bench workload, not the
+denoiser's bias-spectrum run on a 1 x 80 x 88 zero mel); the per-launch figure averages over all of them, so a
+family of kernels (vconv + vpair) is weighted by its launch mix."""
 import csv
 import json
 import re
@@ -14,14 +15,18 @@ import sys
 
 def per_launch(path, sub, counter):
     rows = [r for r in csv.DictReader(open(path)) if re.search(sub, r["Kernel_Name"]) and r["Counter_Name"] == counter]
-    g = max(int(r["Grid_Size"]) for r in rows)
-    vals = [float(r["Counter_Value"]) for r in rows if int(r["Grid_Size"]) == g]
-    return sum(vals) / len(vals), len(vals), g, rows[0]["Kernel_Name"]
+    gmax = {}
+    for r in rows:
+        gmax[r["Kernel_Name"]] = max(gmax.get(r["Kernel_Name"], 0), int(r["Grid_Size"]))
+    keep = [r for r in rows if int(r["Grid_Size"]) == gmax[r["Kernel_Name"]]]
+    vals = [float(r["Counter_Value"]) for r in keep]
+    names = sorted({r["Kernel_Name"][:60] for r in keep})
+    return sum(vals) / len(vals), len(vals), sorted(set(gmax.values())), names
 
 
 fetch, nf, grid, name = per_launch(sys.argv[1], sys.argv[3], "FETCH_SIZE")
 write, nw, _, _ = per_launch(sys.argv[2], sys.argv[3], "WRITE_SIZE")
-out = {"kernel": name, "grid_size": grid, "launches_fetch_pass": nf, "launches_write_pass": nw,
+out = {"kernels": name, "grid_sizes": grid, "launches_fetch_pass": nf, "launches_write_pass": nw,
        "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
        "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024)),
        "correction": "2 x FETCH_SIZE (gfx950 reports half of wide coalesced reads) + WRITE_SIZE, KiB -> B",
