@@ -86,9 +86,10 @@ int mt_decoder_num_params(const mt_decoder* d);
 int mt_decoder_param_name(const mt_decoder* d, int i, char* buf, int buflen);
 int mt_decoder_param_shape(const mt_decoder* d, int i, int64_t* shape, int maxdim); /* -> ndim */
 /* bf16: 1 (default) runs the ResnetBlock1D convs, the stride-1 down/up convs and the final block
- * conv on the LDS-DMA persistent conv (mt_vconv; producers keep those inputs masked, GroupNorm+Mish
- * applied by a separate pass); 0 = generic conv kernel with the GN/mask prologues. Same math as
- * mt_decoder_step / mt_cfm_solve (model.py ResnetBlock1D, Block1D, Decoder.forward) either way. */
+ * conv on the LDS-DMA persistent conv (mt_vconv; producers keep those inputs masked, block 1's
+ * GroupNorm+Mish applied by a separate pass, block 2's inside the res conv's epilogue); 2 = the same with
+ * block 2's GroupNorm+Mish as a separate pass too; 0 = generic conv kernel with the GN/mask prologues.
+ * Same math as mt_decoder_step / mt_cfm_solve (model.py ResnetBlock1D, Block1D, Decoder.forward). */
 int mt_decoder_set_vconv(mt_decoder* d, int enable);
 size_t mt_decoder_packed_bytes(const mt_decoder* d);
 /* params[i]: device fp32 tensor in reference layout for parameter i. */
@@ -100,6 +101,19 @@ size_t mt_cfm_workspace_bytes(const mt_decoder* d, int B, int T, int n_timesteps
 int mt_cfm_solve(const mt_decoder* d, const void* packed, const float* z_noise, float temperature,
                  const float* mu_y, const float* mask, const float* spks, int B, int T,
                  int n_timesteps, int solver, float* z_out, void* ws, size_t ws_bytes, void* stream);
+
+/* The same solve with the caller's bound on valid frames: max_valid = the most mask = 1 frames of any utterance
+ * (model.py:1278's y_max; 0 = unknown). When max_valid < T every utterance has padded frames at full resolution
+ * (and at max_valid <= T - 2 also at half resolution, mask[:, ::2]); the reference then fills every masked key
+ * with +3.4e38 (model.py:697), so each utterance's attention is the same row for all queries — the uniform
+ * mean of its masked V rows — and those transformer blocks skip Q / K / the per-frame softmax and
+ * out-projection (a masked mean + two GEMVs per utterance). Same results as mt_cfm_solve up to rounding. */
+int mt_cfm_solve_bounded(const mt_decoder* d, const void* packed, const float* z_noise, float temperature,
+                         const float* mu_y, const float* mask, const float* spks, int B, int T, int max_valid,
+                         int n_timesteps, int solver, float* z_out, void* ws, size_t ws_bytes, void* stream);
+/* 1 (default): mt_cfm_solve_bounded takes the query-independent attention path where max_valid allows it;
+ * 0: always the general Q.K^T path (A/B, tests) */
+int mt_decoder_set_uniform_attention(mt_decoder* d, int enable);
 
 size_t mt_decoder_step_workspace_bytes(const mt_decoder* d, int B, int T);
 /* one estimator evaluation: out = Decoder.forward(x, mask, mu_y, t, spks) [B,80,T] */

@@ -306,6 +306,156 @@ size_t attention_part_bytes(int B, int T, int heads) {
   return NS <= 1 ? 0 : (size_t)B * heads * ((T + 63) / 64) * NS * 64 * 66 * sizeof(float);
 }
 
+// ------------------------------------------------------------------------------------------------------
+// Query-independent attention of utterances WITH padding (bf16 decoder, C = 256, heads x 64 = 128).
+// The reference fills masked keys with +3.4e38 (model.py:697), so every query of such an utterance attends
+// uniformly to its masked keys: attn1's output is the same row for every frame,
+//     o = W_o (mean_{j masked} V_j) + b_o,   V_j = W_v LN1(x_j) + b_v = W'_v xhat_j + b'_v
+// (LN1's gamma / beta are folded into the packed QKV image W' / bias b'; xhat_j = (x_j - mu_j) rstd_j). So the
+// block needs neither Q, K, V of every frame nor the per-frame out-projection: one masked mean of xhat per
+// utterance and two 256-wide GEMVs. BasicTransformerBlock's x + attn1(...) (model.py:733-737) becomes x_j += o.
+// part: grid (S, B), slice s of utterance b -> part[b][s][0..255] = sum over masked frames of xhat, [256] = count
+// apply: grid (S, B), merges the S partials (slice order), the GEMVs (every block, redundantly: 2 x 32 K MACs),
+//   then x_j = bf16(x_j + o) for the slice's frames + the (mean, M2) per 64-channel slab of the stored row
+//   (the LayerNorm partials LN3 reads, VE_ROWSTATS format). Rounding as the GEMM path: V averaged in fp32,
+//   o rounded to bf16 (the attention output was stored bf16), x + (W_o o + b_o) in fp32, stored bf16.
+constexpr int UNI_C = 256, UNI_PART = UNI_C + 4;
+
+__global__ __launch_bounds__(256) void attn_uni_part_kernel(const bf16* __restrict__ x, const float* __restrict__ mask,
+                                                            int T, float* __restrict__ part) {
+  __shared__ float red[8][UNI_C + 1];
+  const int S = gridDim.x, s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int fr = tid >> 5, cl = tid & 31, c = cl * 8;
+  const int f0 = (int)((long)s * T / S), f1 = (int)((long)(s + 1) * T / S);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, n = 0.f;
+  for (int j = f0 + fr; j < f1; j += 8) {
+    if (mask[(size_t)b * T + j] != 0.f) continue;  // the 32 lanes of a frame agree
+    const u32x4 w = *reinterpret_cast<const u32x4*>(x + ((size_t)b * T + j) * UNI_C + c);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[2 * e] = __uint_as_float(w[e] << 16);
+      v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+    }
+    float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) sm += __shfl_xor(sm, o, 64);
+    const float mu = sm * (1.f / UNI_C);
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q += (v[e] - mu) * (v[e] - mu);
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);
+    const float rs = rsqrtf(q * (1.f / UNI_C) + 1e-5f);  // nn.LayerNorm eps (BasicTransformerBlock.norm1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += (v[e] - mu) * rs;
+    n += 1.f;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[fr][c + e] = acc[e];
+  if (cl == 0) red[fr][UNI_C] = n;
+  __syncthreads();
+  for (int i = tid; i <= UNI_C; i += 256) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][i];
+    part[((size_t)b * S + s) * UNI_PART + i] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ x, int T, const float* __restrict__ part,
+                                                             const bf16* __restrict__ wqkv, int mq, const float* __restrict__ bqkv,
+                                                             const bf16* __restrict__ wout, const float* __restrict__ bout,
+                                                             float* __restrict__ row_out) {
+  __shared__ float zb[UNI_C], vb[128], ob[UNI_C];
+  const int S = gridDim.x, s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  {  // merge the utterance's slices in order
+    float z = 0.f, n = 0.f;
+    for (int k = 0; k < S; ++k) {
+      z += part[((size_t)b * S + k) * UNI_PART + tid];
+      n += part[((size_t)b * S + k) * UNI_PART + UNI_C];
+    }
+    zb[tid] = z / n;
+  }
+  __syncthreads();
+  if (tid < 128) {  // V row 256 + tid of the LN-folded QKV image [4 chunks][mq rows][64]
+    const int m = 256 + tid;
+    float v = bqkv[m];
+    for (int ck = 0; ck < 4; ++ck) {
+      const bf16* wr = wqkv + ((size_t)ck * mq + m) * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const u32x4 w = *reinterpret_cast<const u32x4*>(wr + 8 * i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v += __uint_as_float(w[e] << 16) * zb[ck * 64 + 8 * i + 2 * e];
+          v += __uint_as_float(w[e] & 0xffff0000u) * zb[ck * 64 + 8 * i + 2 * e + 1];
+        }
+      }
+    }
+    vb[tid] = (float)(bf16)v;
+  }
+  __syncthreads();
+  {  // out-projection row tid of the [2 chunks][256 rows][64] image
+    float o = bout[tid];
+    for (int ck = 0; ck < 2; ++ck) {
+      const bf16* wr = wout + ((size_t)ck * UNI_C + tid) * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const u32x4 w = *reinterpret_cast<const u32x4*>(wr + 8 * i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o += __uint_as_float(w[e] << 16) * vb[ck * 64 + 8 * i + 2 * e];
+          o += __uint_as_float(w[e] & 0xffff0000u) * vb[ck * 64 + 8 * i + 2 * e + 1];
+        }
+      }
+    }
+    ob[tid] = o;
+  }
+  __syncthreads();
+  const int fr = tid >> 5, cl = tid & 31, c = cl * 8;
+  const int f0 = (int)((long)s * T / S), f1 = (int)((long)(s + 1) * T / S);
+  for (int j = f0 + fr; j < f1; j += 8) {
+    bf16* xr = x + ((size_t)b * T + j) * UNI_C + c;
+    u32x4 w = *reinterpret_cast<const u32x4*>(xr);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bf16 lo = (bf16)(__uint_as_float(w[e] << 16) + ob[c + 2 * e]);
+      const bf16 hi = (bf16)(__uint_as_float(w[e] & 0xffff0000u) + ob[c + 2 * e + 1]);
+      v[2 * e] = (float)lo;
+      v[2 * e + 1] = (float)hi;
+      w[e] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+    }
+    *reinterpret_cast<u32x4*>(xr) = w;
+    // (mean, M2) of the 64-channel slab (8 lanes x 8 channels), two-pass over the stored values
+    float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) sm += __shfl_xor(sm, o, 64);
+    const float mu = sm * (1.f / 64.f);
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q += (v[e] - mu) * (v[e] - mu);
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) q += __shfl_xor(q, o, 64);
+    if ((cl & 7) == 0) *reinterpret_cast<float2*>(row_out + 2 * (((size_t)b * T + j) * 4 + (cl >> 3))) = float2{mu, q};
+  }
+}
+
+int uniform_attention_slices(int T) { return std::max(1, std::min(8, T / 64)); }
+
+int launch_uniform_attention(void* x, const float* mask, int B, int T, const void* wqkv, int mq, const float* bqkv,
+                             const void* wout, const float* bout, float* part, float* row_out, hipStream_t st) {
+  MT_REQUIRE(x && mask && wqkv && bqkv && wout && bout && part && row_out && B > 0 && T > 0 && mq == 384,
+             "uniform attention: arguments (C = 256, 2 heads x 64)");
+  const int S = uniform_attention_slices(T);
+  hipLaunchKernelGGL(attn_uni_part_kernel, dim3(S, B), dim3(256), 0, st, (const bf16*)x, mask, T, part);
+  hipLaunchKernelGGL(attn_uni_apply_kernel, dim3(S, B), dim3(256), 0, st, (bf16*)x, T, (const float*)part,
+                     (const bf16*)wqkv, mq, bqkv, (const bf16*)wout, bout, row_out);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 int launch_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T,
                      int heads, hipStream_t stream, float* part) {
   MT_REQUIRE(B > 0 && T > 0 && heads > 0, "attention: empty geometry");

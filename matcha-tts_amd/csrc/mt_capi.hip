@@ -113,7 +113,9 @@ int mt_decoder_param_shape(const mt_decoder* d, int i, int64_t* shape, int maxdi
 }
 int mt_decoder_set_vconv(mt_decoder* d, int enable) {
   MT_REQUIRE(d, "null decoder");
+  MT_REQUIRE(enable >= 0 && enable <= 2, "decoder_set_vconv: mode %d", enable);
   d->d.vconv = enable ? 1 : 0;
+  d->d.gnres = enable == 1 ? 1 : 0;
   return 0;
 }
 size_t mt_decoder_packed_bytes(const mt_decoder* d) { return d ? d->d.packed_bytes : 0; }
@@ -131,6 +133,18 @@ int mt_cfm_solve(const mt_decoder* d, const void* packed, const float* z_noise, 
   MT_REQUIRE(d && packed && z_noise && mu_y && mask && z_out && ws, "cfm_solve: null argument");
   return d->d.solve(packed, z_noise, temperature, mu_y, mask, spks, B, T, n_timesteps, solver, z_out, ws,
                     ws_bytes, (hipStream_t)stream);
+}
+int mt_cfm_solve_bounded(const mt_decoder* d, const void* packed, const float* z_noise, float temperature,
+                         const float* mu_y, const float* mask, const float* spks, int B, int T, int max_valid,
+                         int n_timesteps, int solver, float* z_out, void* ws, size_t ws_bytes, void* stream) {
+  MT_REQUIRE(d && packed && z_noise && mu_y && mask && z_out && ws, "cfm_solve: null argument");
+  return d->d.solve(packed, z_noise, temperature, mu_y, mask, spks, B, T, n_timesteps, solver, z_out, ws,
+                    ws_bytes, (hipStream_t)stream, max_valid);
+}
+int mt_decoder_set_uniform_attention(mt_decoder* d, int enable) {
+  MT_REQUIRE(d, "null decoder");
+  d->d.uniform_attn = enable ? 1 : 0;
+  return 0;
 }
 size_t mt_decoder_step_workspace_bytes(const mt_decoder* d, int B, int T) {
   return d ? d->d.workspace_bytes(B, T, 1) : 0;

@@ -403,6 +403,7 @@ size_t Decoder::workspace_bytes(int B, int T, int S) const {
   n += 4096;                                          // trash (vconv stores past the last frame)
   n += align256(attention_part_bytes(B, T, heads));   // attention key-split slots
   n += align256(BT * (C / 64) * 2 * 4);               // lnp
+  n += align256((size_t)B * 8 * 260 * 4);             // upart
   return n;
 }
 
@@ -442,6 +443,7 @@ Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
   w.tb_ld = 0;
   w.apart = (float*)take(attention_part_bytes(B, T, heads));
   w.lnp = (float*)take(BT * (C / 64) * 2 * 4);
+  w.upart = (float*)take((size_t)B * 8 * 260 * 4);
   w.m0 = nullptr;
   return w;
 }
@@ -548,14 +550,27 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
   }
   // residual 1x1 + block output
   if (x_masked && vc(R.res)) {
-    if ((rc = gn_apply(yb2, B, Tl, C, w.gn2, nt2, g2, g2 + C, 1e-5f, nullptr, 0, mask, w.y2, st))) return rc;
     VConvArgs c = vargs(R.res, P, w, x0, B, Tl, out);
     c.x1 = (const bf16*)x1;
     c.c0 = c0;
     c.cin = cin;
-    c.resid = (const bf16*)w.y2;
     c.row_out = w.lnp;  // the LayerNorm partials of the transformer block that reads `out`
     *row_stats = true;
+    if (vc(R.c2) && gnres && Tl >= vconv_gnres_min_frames()) {
+      // block 2's GroupNorm + Mish + mask applied in this conv's epilogue to the raw conv output (no gn_apply)
+      c.resid = (const bf16*)yb2;
+      c.gn_in = w.gn2;
+      c.gn_in_parts = nt2;
+      c.gn_T = Tl;
+      c.gn_B = B;
+      c.gn_gamma = g2;
+      c.gn_beta = g2 + C;
+      c.gn_eps = 1e-5f;
+      c.emask = mask;
+      return launch_vconv(VE_RESID | VE_ROWSTATS | VE_GNRES, c, st);
+    }
+    if ((rc = gn_apply(yb2, B, Tl, C, w.gn2, nt2, g2, g2 + C, 1e-5f, nullptr, 0, mask, w.y2, st))) return rc;
+    c.resid = (const bf16*)w.y2;
     return launch_vconv(VE_RESID | VE_ROWSTATS, c, st);
   }
   ConvArgs c = gemm_args(R.res, P, B, Tl);
@@ -577,12 +592,29 @@ int Decoder::resnet(const char* P, const Work& w, const Res& R, const void* x0, 
 
 template <class E>
 int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, bool mask_out,
-                    bool row_stats, int B, int Tl, hipStream_t st) const {
+                    bool row_stats, bool uni, int B, int Tl, hipStream_t st) const {
   int rc;
   if constexpr (std::is_same<E, bf16>::value) {
     if (t.qkv.vc && t.out.vc && t.ff1.vc && t.ff2.vc) {
       // bf16: the four GEMMs on mt_vconv's 1x1 pipeline; LayerNorm folded into the QKV / FF1 epilogues
       auto vargs = [&](const GemmW& g, const void* xin, void* y) { return this->vargs(g, P, w, xin, B, Tl, y); };
+      if (uni && heads == 2 && t.qkv.cout == 384 && t.qkv.cin == C && t.out.cout == C && t.out.cin == 128) {
+        // every utterance is padded at this level: attention is query-independent (model.py:697) -> x += o_b
+        // with o_b from a masked mean and two GEMVs; no QKV GEMM, no attention, no per-frame out-projection
+        if ((rc = launch_uniform_attention(x, mask, B, Tl, P + t.qkv.v_off, t.qkv.cout, (const float*)(P + t.qkv.b_off),
+                                           P + t.out.v_off, (const float*)(P + t.out.b_off), w.upart, w.lnp, st)))
+          return rc;
+        VConvArgs f1 = vargs(t.ff1, x, w.ff);
+        f1.ln_stats = w.lnp;
+        f1.wsum = (const float*)(P + t.wsf_off);
+        f1.snake_alpha = (const float*)(P + t.snake_off);
+        f1.snake_ibeta = (const float*)(P + t.snake_off) + TE;
+        if ((rc = launch_vconv(VE_LN | VE_LNP | VE_SNAKE, f1, st))) return rc;
+        VConvArgs f2 = vargs(t.ff2, w.ff, x);
+        f2.resid = (const bf16*)x;
+        f2.emask = mask;
+        return launch_vconv(mask_out ? VE_RESID | VE_MASK : VE_RESID, f2, st);
+      }
       // LayerNorm statistics: per-slab partials from the producing conv's epilogue (VE_ROWSTATS) when it
       // wrote them, else a row-statistics pass
       VConvArgs q = vargs(t.qkv, x, w.qkv);
@@ -656,8 +688,9 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   bool rs = false;  // the last resnet's output conv wrote the LayerNorm partials of its output
   auto tblocks = [&](int r, void* x, const float* m, int Tl) -> int {
     const int nb = (int)tbs[r].size();
+    const bool uni = uniform_attn && (Tl == T ? w.uni0 : w.uni1);
     for (int j = 0; j < nb; ++j) {
-      int e = tblock<E>(P, w, tbs[r][j], x, m, mio && j == nb - 1, rs && j == 0, B, Tl, st);
+      int e = tblock<E>(P, w, tbs[r][j], x, m, mio && j == nb - 1, rs && j == 0, uni, B, Tl, st);
       if (e) return e;
     }
     return 0;
@@ -799,7 +832,7 @@ static int check_geom(int B, int T) {
 
 int Decoder::solve(const void* packed, const float* z_noise, float temperature, const float* mu_y,
                    const float* mask, const float* spks, int B, int T, int n_steps, int solver, float* z_out,
-                   void* ws, size_t ws_bytes, hipStream_t st) const {
+                   void* ws, size_t ws_bytes, hipStream_t st, int max_valid) const {
   int rc;
   if ((rc = check_geom(B, T))) return rc;
   MT_REQUIRE(n_steps >= 1, "cfm: n_timesteps must be >= 1");
@@ -811,6 +844,11 @@ int Decoder::solve(const void* packed, const float* z_noise, float temperature, 
   const char* P = (const char*)packed;
   Work w = carve(ws, B, T, S);
   w.m0 = mask;
+  // the caller's bound on valid frames (model.py's y_max): below T every utterance is padded at full resolution,
+  // at <= T - 2 also at half resolution (mask[:, ::2] keeps frame T - 2)
+  MT_REQUIRE(max_valid >= 0 && max_valid <= T, "cfm: max_valid %d outside [0, T=%d]", max_valid, T);
+  w.uni0 = max_valid > 0 && max_valid < T;
+  w.uni1 = max_valid > 0 && max_valid <= T - 2;
   // evaluation times exactly as the reference forms them in fp32 (model.py:1086-1104)
   TimeSched ts{};
   const float dt = (float)(1.0 / (double)n_steps);

@@ -56,5 +56,12 @@ int maximum_path(const float* value, const int* t_xs, const int* t_ys, int B, in
 int launch_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                      hipStream_t stream, float* part = nullptr);
 size_t attention_part_bytes(int B, int T, int heads);
+// query-independent attention + out-projection + residual of utterances that ALL have padded frames at this
+// level (the reference's mask fill, model.py:697; mt_attn.hip): x [B][T][256] bf16 updated in place to x + attn1(x),
+// row_out [B*T][4][2] the per-slab (mean, M2) of the result; wqkv / bqkv the LN-folded QKV vconv image (mq = 384
+// rows) and bias, wout / bout the out-projection image and bias; part: B * uniform_attention_slices(T) * 260 floats
+int uniform_attention_slices(int T);
+int launch_uniform_attention(void* x, const float* mask, int B, int T, const void* wqkv, int mq, const float* bqkv,
+                             const void* wout, const float* bout, float* part, float* row_out, hipStream_t st);
 
 }  // namespace mt

@@ -83,6 +83,9 @@ struct Decoder {
   // bf16: 1 = the ResnetBlock convs, down1 / up1 and the final block conv also run on mt_vconv (their
   // inputs are then kept masked by their producers), 0 = generic conv kernel for those (A/B, tests)
   int vconv = 1;
+  // vconv path: block 2's GroupNorm + Mish + mask folded into the res conv's epilogue (VE_GNRES); 0: a separate
+  // gn_apply pass (mt_decoder_set_vconv mode 2, A/B and tests)
+  int gnres = 1;
   std::vector<Res> res;                // down0, down1, mid..., up0, up1
   std::vector<std::vector<TB>> tbs;    // per resnet
   GemmW down0, down1, up0, up1, fconv, fproj;
@@ -99,8 +102,12 @@ struct Decoder {
     double *gn1, *gn2;
     float* apart;  // attention key-split slots
     float* lnp;    // per frame, per 64-channel slab (sum, sum of squares): LayerNorm partials (vconv VE_ROWSTATS)
+    float* upart;  // query-independent attention: per (utterance, slice) masked sums of the normalised rows
     int tb_ld;     // 0: one time bias per evaluation; n_res * C: one per utterance (step_times)
     const float* m0;
+    // every utterance has padded frames at the full- / half-resolution level (the caller's max_valid < T /
+    // <= T - 2): the transformer blocks there take the query-independent attention path
+    bool uni0 = false, uni1 = false;
   };
   Work carve(void* ws, int B, int T, int S) const;
   int time_embed(const char* P, const Work& w, const TimeSched& ts, int S, hipStream_t st,
@@ -118,8 +125,9 @@ struct Decoder {
              hipStream_t st) const;
   // row_stats: w.lnp already holds the LayerNorm partials of x (written by the producing conv)
   template <class E>
+  // uni: the query-independent attention path (every utterance padded at this level)
   int tblock(const char* P, const Work& w, const TB& t, void* x, const float* mask, bool mask_out, bool row_stats,
-             int B, int Tl, hipStream_t st) const;
+             bool uni, int B, int Tl, hipStream_t st) const;
   bool vc(const GemmW& g) const { return vconv && g.vc; }
   // decoder input row stride: zero-padded to a multiple of 64 channels (and stored masked) on the vconv path
   int xld() const { return (vconv && dtype == BF16) ? (c_cond + 63) / 64 * 64 : c_cond; }
@@ -127,9 +135,13 @@ struct Decoder {
 
   int init_inputs(const Work& w, const float* z, float temperature, const float* mu_y, const float* spks,
                   int B, int T, hipStream_t st) const;
+  // max_valid: the most valid (mask = 1) frames of any utterance (0: unknown)
   int solve(const void* packed, const float* z_noise, float temperature, const float* mu_y,
             const float* mask, const float* spks, int B, int T, int n_steps, int solver, float* z_out,
-            void* ws, size_t ws_bytes, hipStream_t st) const;
+            void* ws, size_t ws_bytes, hipStream_t st, int max_valid = 0) const;
+  // 1 (default): the query-independent attention path when the caller's max_valid allows it; 0: always the
+  // general Q.K^T path (A/B, tests)
+  int uniform_attn = 1;
   int step(const void* packed, const float* x, const float* mu_y, const float* mask, const float* spks,
            float t, int B, int T, float* out, void* ws, size_t ws_bytes, hipStream_t st) const;
   int step_times(const void* packed, const float* x, const float* mu_y, const float* mask, const float* spks,

@@ -26,6 +26,10 @@ enum : int {
   VE_LNP = 1024,     // with VE_LN: ln_stats holds VE_ROWSTATS partials [frames][cin/64] instead of (mean, rstd)
   VE_RELU = 2048,    // max(v, 0) after the bias (text-encoder FFN, model.py:119-130)
   VE_PMASK = 4096,   // placed output: v * emask[output frame], frame = element / mask_div
+  VE_GNRES = 8192,   // 1x1 only, with VE_RESID: the residual is the RAW input of a GroupNorm(M/32) + Mish + mask,
+                     // applied here: resid := bf16(mish(GN(resid)) * emask[frame]) with the statistics merged
+                     // per tile from the producer's VE_GNSTATS partials (ResnetBlock1D block2 -> + res(x),
+                     // model.py:777-790; replaces a separate gn_apply pass)
 };
 
 struct VConvArgs {
@@ -61,6 +65,12 @@ struct VConvArgs {
   int mask_div;        // VE_PMASK: output elements per frame
   int gn_parts;        // VE_GNSTATS: partial slots the consumer will merge (0: unchecked); must equal
                        // what this launch writes
+  // VE_GNRES: the residual's GroupNorm
+  const double* gn_in;       // [gn_B][M/32][gn_in_parts][2] (sum, sum of squares) of the raw residual
+  int gn_in_parts, gn_T, gn_B;  // partial slots per (utterance, group), frames per utterance, utterances
+  const float* gn_gamma;     // [M]
+  const float* gn_beta;      // [M]
+  float gn_eps;
 };
 
 // LayerNorm (mean, rstd) of a 256-channel frame from its 4 slab partials (mean_i, M2_i), 64 values each,
@@ -76,6 +86,8 @@ __device__ __forceinline__ float2 ln_merge4(f32x4 p01, f32x4 p23, float eps) {
 int vconv_gn_parts(int B, int L, int M);
 // an upper bound of vconv_gn_parts over B (workspace sizing)
 int vconv_gn_parts_max(int L);
+// shortest utterance VE_GNRES accepts (shorter: run gn_apply, then a plain VE_RESID conv)
+int vconv_gnres_min_frames();
 
 bool vconv_supported(int cin, int cout, int k, int dil, int stride);
 // packed bytes of the [cin/64][taps][Mpad][64] image

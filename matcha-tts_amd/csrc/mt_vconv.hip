@@ -94,8 +94,8 @@ __device__ __forceinline__ void raw_barrier() {
 }
 
 template <int EF>
-constexpr int vc_npar() {
-  return 1 + ((EF & VE_LN) ? 1 : 0) + ((EF & VE_SNAKE) ? 2 : 0);
+constexpr int vc_npar() {  // per-channel LDS tables (MMAX floats each); VE_GNRES: gamma, beta + the GN table
+  return 1 + ((EF & VE_LN) ? 1 : 0) + ((EF & VE_SNAKE) ? 2 : 0) + ((EF & VE_GNRES) ? 3 : 0);
 }
 
 template <int EF, int BMT, bool K1, int BNT = BN>
@@ -107,6 +107,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   constexpr int BIAS_OFF = TT::PAR_OFF;
   constexpr int WSUM_OFF = BIAS_OFF + MMAX * 4;
   constexpr int SNAKE_OFF = WSUM_OFF + ((EF & VE_LN) ? MMAX * 4 : 0);
+  constexpr int GNP_OFF = SNAKE_OFF + ((EF & VE_SNAKE) ? 2 * MMAX * 4 : 0);  // gamma, beta, then per-wave GN table
   __shared__ __attribute__((aligned(1024))) char smem[TT::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -129,6 +130,10 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     if constexpr ((EF & VE_SNAKE) != 0) {
       reinterpret_cast<float*>(smem + SNAKE_OFF)[i] = a.snake_alpha[i];
       reinterpret_cast<float*>(smem + SNAKE_OFF)[MMAX + i] = a.snake_ibeta[i];
+    }
+    if constexpr ((EF & VE_GNRES) != 0) {
+      reinterpret_cast<float*>(smem + GNP_OFF)[i] = a.gn_gamma[i];
+      reinterpret_cast<float*>(smem + GNP_OFF)[MMAX + i] = a.gn_beta[i];
     }
   }
   __syncthreads();
@@ -219,7 +224,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
             lnr[fn][0] = pp[0];
             lnr[fn][1] = pp[1];
           }
-        if constexpr ((EF & VE_MASK) != 0)
+        if constexpr ((EF & (VE_MASK | VE_GNRES)) != 0)
           if (fp == 0) mk[fn] = a.emask[rowbase + n];
       }
   };
@@ -240,6 +245,45 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     if constexpr ((EF & VE_LNP) != 0) {
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) lns[fn] = ln_merge4(lnr[fn][0], lnr[fn][1], a.ln_eps);
+    }
+    // VE_GNRES: (mean, rstd) of the residual's GroupNorm for the utterances this wave's frames span and its
+    // two 32-channel groups, merged from the producer's partials into a wave-private LDS table (4 lanes per
+    // (utterance, group) pair, fp64 as gn_apply merges them); read back by the same wave, no barrier
+    int gu0 = 0;
+    int gun[FN];
+    const float* gtab = reinterpret_cast<const float*>(smem + GNP_OFF + 2 * MMAX * 4) + wave * 32;
+    if constexpr ((EF & VE_GNRES) != 0) {
+      const int nlo = n0 + wn * WNC, nhi = min(nlo + WNC, L) - 1;
+      gu0 = nlo / a.gn_T;
+      const int nu = min(nhi / a.gn_T, a.gn_B - 1) - gu0 + 1;  // <= 8 (host check)
+      const int pair = lane >> 2, sub = lane & 3, pu = pair >> 1;
+      const int G = a.M >> 5, grp = ((m0 + wm * 64) >> 5) + (pair & 1);
+      double s1 = 0.0, s2 = 0.0;
+      if (pu < nu) {
+        const double* p = a.gn_in + ((size_t)(gu0 + pu) * G + grp) * a.gn_in_parts * 2;
+        for (int k = sub; k < a.gn_in_parts; k += 4) {
+          s1 += p[2 * k];
+          s2 += p[2 * k + 1];
+        }
+      }
+      s1 += __shfl_xor(s1, 1, 64);
+      s2 += __shfl_xor(s2, 1, 64);
+      s1 += __shfl_xor(s1, 2, 64);
+      s2 += __shfl_xor(s2, 2, 64);
+      if (sub == 0 && pu < nu) {
+        const double cnt = 32.0 * (double)a.gn_T, mean = s1 / cnt;
+        double var = s2 / cnt - mean * mean;
+        var = var < 0.0 ? 0.0 : var;
+        float* wt = reinterpret_cast<float*>(smem + GNP_OFF + 2 * MMAX * 4) + wave * 32;
+        wt[2 * pair] = (float)mean;
+        wt[2 * pair + 1] = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int n = min(n0 + wn * WNC + fn * 16 + l16, L - 1);
+        gun[fn] = min(n / a.gn_T, a.gn_B - 1) - gu0;
+      }
     }
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
@@ -277,6 +321,15 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
             ib4 = *reinterpret_cast<const f32x4*>(smem + SNAKE_OFF + 4 * (MMAX + m));
           }
           const uint32_t rr[2] = {h ? ry0 : rx0, h ? ry1 : rx1};
+          float gga = 0.f, ggs = 0.f;  // VE_GNRES: this (utterance, group)'s mean and rstd
+          f32x4 gam4, bet4;
+          if constexpr ((EF & VE_GNRES) != 0) {
+            const float2 mr = *reinterpret_cast<const float2*>(gtab + 2 * (2 * gun[fn] + fp));
+            gga = mr.x;
+            ggs = mr.y;
+            gam4 = *reinterpret_cast<const f32x4*>(smem + GNP_OFF + 4 * m);
+            bet4 = *reinterpret_cast<const f32x4*>(smem + GNP_OFF + 4 * (MMAX + m));
+          }
           const uint32_t yy[2] = {h ? yy0 : yx0, h ? yy1 : yx1};
           bf16 ob[4], ab[4];
 #pragma unroll
@@ -289,7 +342,14 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
               v = v + ib4[r] * (sn * sn);
             }
             if constexpr ((EF & VE_RELU) != 0) v = fmaxf(v, 0.f);
-            if constexpr ((EF & VE_RESID) != 0) v = v + bf2(rr[r >> 1], r & 1);
+            if constexpr ((EF & VE_GNRES) != 0) {
+              // gn_apply's arithmetic: scale = rstd * gamma, shift = -scale * mean + beta, mish, * mask, bf16
+              const float sc = ggs * gam4[r], sh = -sc * gga + bet4[r];
+              const float hv = mish_f(bf2(rr[r >> 1], r & 1) * sc + sh) * mk[fn];
+              v = v + (float)(bf16)hv;
+            } else if constexpr ((EF & VE_RESID) != 0) {
+              v = v + bf2(rr[r >> 1], r & 1);
+            }
             if constexpr ((EF & VE_ACCUM) != 0) v = bf2(yy[r >> 1], r & 1) + v;
             if constexpr ((EF & VE_DIV) != 0) v = v / a.div;
             if constexpr ((EF & VE_GNSTATS) != 0) {
@@ -298,7 +358,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
                 gq[fp] += (double)v * (double)v;
               }
             }
-            if constexpr ((EF & VE_MASK) != 0) v = v * mk[fn];
+            if constexpr ((EF & VE_MASK) != 0 && (EF & VE_GNRES) == 0) v = v * mk[fn];
             if constexpr ((EF & VE_PMASK) != 0) v = v * pmk;
             const bf16 rb = (bf16)v;
             if constexpr ((EF & VE_ROWSTATS) != 0) {  // Welford over the lane's values (k-th value: 1/k)
@@ -621,6 +681,9 @@ int vconv_gn_parts(int B, int L, int M) {
 
 int vconv_gn_parts_max(int L) { return (L + 127) / 128 * 4; }
 
+// VE_GNRES: a wave's 64 (or 32) frames must span at most 8 utterances (its GN table holds 16 pairs)
+int vconv_gnres_min_frames() { return 10; }
+
 int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(a0.x && a0.w && a0.bias && a0.y && a0.zero && a0.trash, "vconv: null pointer");
   MT_REQUIRE(a0.B > 0 && a0.L > 0 && a0.cin % 64 == 0 && a0.M % 64 == 0 && a0.Mpad == a0.M && a0.M <= MMAX,
@@ -636,6 +699,10 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(!(ef & VE_SNAKE) || (a0.snake_alpha && a0.snake_ibeta), "vconv: snake params");
   MT_REQUIRE(!(ef & VE_MASK) || a0.emask, "vconv: mask");
   MT_REQUIRE(!(ef & VE_GNSTATS) || (a0.gn_out && a0.taps > 1 && a0.M % 32 == 0), "vconv: GN statistics");
+  MT_REQUIRE(!(ef & VE_GNRES) || ((ef & VE_RESID) && !(ef & VE_MASK) && a0.taps == 1 && a0.gn_in && a0.gn_gamma &&
+                                  a0.gn_beta && a0.emask && a0.gn_in_parts > 0 && a0.gn_B == a0.B &&
+                                  a0.gn_T == a0.L && a0.gn_T >= vconv_gnres_min_frames() && a0.M % 64 == 0),
+             "vconv: residual GroupNorm (1x1, resid, partials, gamma / beta, mask, T >= %d)", vconv_gnres_min_frames());
   VConvArgs a = a0;
   if (a.c0 == 0) a.c0 = a.cin;  // one source
   MT_REQUIRE(a.c0 == a.cin || (a.x1 && a.c0 % 64 == 0 && a.c0 > 0 && a.c0 < a.cin), "vconv: channel split %d/%d",
@@ -739,6 +806,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE1(VE_RESID)
       MT_VCASE1(VE_RESID | VE_MASK)
       MT_VCASE1(VE_RESID | VE_ROWSTATS)
+      MT_VCASE1(VE_RESID | VE_ROWSTATS | VE_GNRES)
       MT_VCASE1(VE_LN | VE_LNP)
       MT_VCASE1(VE_LN | VE_LNP | VE_SNAKE)
       MT_VCASE1(0)

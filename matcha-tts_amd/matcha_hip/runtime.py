@@ -250,12 +250,19 @@ class DecoderEngine:
         self._packed, self._fp = packed, fp
         return packed
 
-    def set_vconv(self, enable) -> None:
-        """bf16: 1 (default) ResnetBlock / down / up / final convs on mt_vconv, 0 generic conv kernel."""
-        check(lib().mt_decoder_set_vconv(self.h, int(bool(enable))), "decoder_set_vconv")
+    def set_vconv(self, mode) -> None:
+        """bf16: 1 (default) ResnetBlock / down / up / final convs on mt_vconv with block 2's GroupNorm + Mish
+        in the res conv's epilogue; 2 the same with that GroupNorm as a separate pass; 0 generic conv kernel.
+        True / False map to 1 / 0."""
+        check(lib().mt_decoder_set_vconv(self.h, int(mode)), "decoder_set_vconv")
+
+    def set_uniform_attention(self, enable) -> None:
+        """1 (default): query-independent attention where the caller's max_valid proves every utterance padded."""
+        check(lib().mt_decoder_set_uniform_attention(self.h, int(bool(enable))), "decoder_set_uniform_attention")
 
     def solve(self, packed, z_noise, temperature, mu_y, mask, spks, n_timesteps, solver="euler",
-              out=None):
+              out=None, max_valid: int = 0):
+        """max_valid: the most valid frames of any utterance (synthesize's y_max), 0 when unknown."""
         B, C, T = mu_y.shape
         s = SOLVER_EULER if solver == "euler" else SOLVER_MIDPOINT if solver == "midpoint" else None
         if s is None:
@@ -264,9 +271,9 @@ class DecoderEngine:
         L = lib()
         nbytes = L.mt_cfm_workspace_bytes(self.h, B, T, n_timesteps, s)
         ws = _Workspace.get(nbytes, mu_y.device)
-        check(L.mt_cfm_solve(self.h, packed.data_ptr(), ptr(z_noise), float(temperature), ptr(mu_y),
-                             ptr(mask), ptr(spks), B, T, int(n_timesteps), s, ptr(out), ws.data_ptr(),
-                             ws.numel(), stream_handle(mu_y.device)), "cfm_solve")
+        check(L.mt_cfm_solve_bounded(self.h, packed.data_ptr(), ptr(z_noise), float(temperature), ptr(mu_y),
+                                     ptr(mask), ptr(spks), B, T, int(max_valid), int(n_timesteps), s, ptr(out),
+                                     ws.data_ptr(), ws.numel(), stream_handle(mu_y.device)), "cfm_solve")
         return out
 
     def step(self, packed, x, mu_y, mask, spks, t: float, out=None):

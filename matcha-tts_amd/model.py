@@ -427,14 +427,16 @@ class BASECFM(nn.Module):
         self.estimator = None
 
     @torch.inference_mode()
-    def forward(self, mu, mask, n_timesteps, temperature=1.0, spks=None, cond=None):
-        """z = randn_like(mu)*temperature, then the Euler/midpoint loop — one HIP call."""
+    def forward(self, mu, mask, n_timesteps, temperature=1.0, spks=None, cond=None, max_valid=None):
+        """z = randn_like(mu)*temperature, then the Euler/midpoint loop — one HIP call. max_valid (extension, not
+        in the reference signature): the most valid frames of any utterance when the caller knows it (synthesize's
+        y_max); it lets the solver prove every utterance padded and use the query-independent attention."""
         rt.require_gpu(mu, mask, spks, what="CFM.forward")
         mu, mask, spks = rt.f32c(mu), rt.f32c(mask), rt.f32c(spks)
         z = torch.randn_like(mu)
         est = self.estimator
         return est.engine().solve(est.packed(mu.device), z, temperature, mu, mask, spks, int(n_timesteps),
-                                  self.solver, out=z)
+                                  self.solver, out=z, max_valid=int(max_valid or 0))
 
     def compute_loss(self, x1, mask, mu, spks=None, cond=None):
         """model.py:1147-1162 -> (loss, y_t, pred, u_t): t ~ U(0,1) and z ~ N(0,1) per utterance on the
@@ -513,7 +515,7 @@ class MatchaTTS(nn.Module):
             y_max = int(y_lengths.max())                 # the reference's host sync (model.py:1278-1281)
             t_pad = fix_len_compatibility(y_max)
             attn, mu_y, y_mask = rt.alignment(cum, y_lengths, t_pad, mu)
-            z = self.decoder(mu_y, y_mask, n_timesteps, temperature, spks, cond=None)
+            z = self.decoder(mu_y, y_mask, n_timesteps, temperature, spks, cond=None, max_valid=y_max)
         finally:
             est._pk.untrust()
         mel = rt.denorm_crop(z, self.mel_mean, self.mel_std, y_max)
