@@ -328,28 +328,39 @@ __global__ __launch_bounds__(256) void attn_uni_part_kernel(const bf16* __restri
   const int fr = tid >> 5, cl = tid & 31, c = cl * 8;
   const int f0 = (int)((long)s * T / S), f1 = (int)((long)(s + 1) * T / S);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, n = 0.f;
-  for (int j = f0 + fr; j < f1; j += 8) {
-    if (mask[(size_t)b * T + j] != 0.f) continue;  // the 32 lanes of a frame agree
-    const u32x4 w = *reinterpret_cast<const u32x4*>(x + ((size_t)b * T + j) * UNI_C + c);
-    float v[8];
+  constexpr int FB = 4;  // frames per thread per round: their loads are issued together
+  for (int jb = f0 + fr; jb < f1; jb += 8 * FB) {
+    u32x4 wv[FB];
+    bool use[FB];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[2 * e] = __uint_as_float(w[e] << 16);
-      v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+    for (int i = 0; i < FB; ++i) {
+      const int j = jb + 8 * i;
+      use[i] = j < f1 && mask[(size_t)b * T + min(j, f1 - 1)] == 0.f;  // the 32 lanes of a frame agree
+      wv[i] = use[i] ? *reinterpret_cast<const u32x4*>(x + ((size_t)b * T + j) * UNI_C + c) : u32x4{0u, 0u, 0u, 0u};
     }
-    float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) sm += __shfl_xor(sm, o, 64);
-    const float mu = sm * (1.f / UNI_C);
-    float q = 0.f;
+    for (int i = 0; i < FB; ++i) {
+      if (!use[i]) continue;
+      float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) q += (v[e] - mu) * (v[e] - mu);
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] = __uint_as_float(wv[i][e] << 16);
+        v[2 * e + 1] = __uint_as_float(wv[i][e] & 0xffff0000u);
+      }
+      float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);
-    const float rs = rsqrtf(q * (1.f / UNI_C) + 1e-5f);  // nn.LayerNorm eps (BasicTransformerBlock.norm1)
+      for (int o = 1; o < 32; o <<= 1) sm += __shfl_xor(sm, o, 64);
+      const float mu = sm * (1.f / UNI_C);
+      float q = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] += (v[e] - mu) * rs;
-    n += 1.f;
+      for (int e = 0; e < 8; ++e) q += (v[e] - mu) * (v[e] - mu);
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);
+      const float rs = rsqrtf(q * (1.f / UNI_C) + 1e-5f);  // nn.LayerNorm eps (BasicTransformerBlock.norm1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += (v[e] - mu) * rs;
+      n += 1.f;
+    }
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[fr][c + e] = acc[e];
@@ -378,67 +389,88 @@ __global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ 
     zb[tid] = z / n;
   }
   __syncthreads();
-  if (tid < 128) {  // V row 256 + tid of the LN-folded QKV image [4 chunks][mq rows][64]
-    const int m = 256 + tid;
-    float v = bqkv[m];
-    for (int ck = 0; ck < 4; ++ck) {
-      const bf16* wr = wqkv + ((size_t)ck * mq + m) * 64;
+  // GEMVs: 4 lanes per output row, each a quarter of K with all its 16-byte weight loads independent (issued
+  // together), combined by two lane shuffles
+  const int q4 = tid & 3, rq = tid >> 2;  // 64 row slots per pass
+  auto dot8 = [](u32x4 w, const float* z) {
+    float acc = 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const u32x4 w = *reinterpret_cast<const u32x4*>(wr + 8 * i);
+    for (int e = 0; e < 4; ++e)
+      acc += __uint_as_float(w[e] << 16) * z[2 * e] + __uint_as_float(w[e] & 0xffff0000u) * z[2 * e + 1];
+    return acc;
+  };
+  {  // V rows 256 .. 383 of the LN-folded QKV image [4 chunks][mq rows][64]; lane quarter q4 = chunk q4
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v += __uint_as_float(w[e] << 16) * zb[ck * 64 + 8 * i + 2 * e];
-          v += __uint_as_float(w[e] & 0xffff0000u) * zb[ck * 64 + 8 * i + 2 * e + 1];
-        }
-      }
+    for (int pass = 0; pass < 2; ++pass) {
+      const int r = rq + 64 * pass;
+      const bf16* wr = wqkv + ((size_t)q4 * mq + 256 + r) * 64;
+      u32x4 w[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w[i] = *reinterpret_cast<const u32x4*>(wr + 8 * i);
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v += dot8(w[i], zb + q4 * 64 + 8 * i);
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      if (q4 == 0) vb[r] = (float)(bf16)(v + bqkv[256 + r]);
     }
-    vb[tid] = (float)(bf16)v;
   }
   __syncthreads();
-  {  // out-projection row tid of the [2 chunks][256 rows][64] image
-    float o = bout[tid];
-    for (int ck = 0; ck < 2; ++ck) {
-      const bf16* wr = wout + ((size_t)ck * UNI_C + tid) * 64;
+  {  // out-projection [2 chunks][256 rows][64]: quarter q4 = chunk q4 / 2, half (q4 & 1) of its 64 elements
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const u32x4 w = *reinterpret_cast<const u32x4*>(wr + 8 * i);
+    for (int pass = 0; pass < 4; ++pass) {
+      const int r = rq + 64 * pass;
+      const int ck = q4 >> 1, k0 = (q4 & 1) * 32;
+      const bf16* wr = wout + ((size_t)ck * UNI_C + r) * 64 + k0;
+      u32x4 w[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o += __uint_as_float(w[e] << 16) * vb[ck * 64 + 8 * i + 2 * e];
-          o += __uint_as_float(w[e] & 0xffff0000u) * vb[ck * 64 + 8 * i + 2 * e + 1];
-        }
-      }
+      for (int i = 0; i < 4; ++i) w[i] = *reinterpret_cast<const u32x4*>(wr + 8 * i);
+      float o = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o += dot8(w[i], vb + ck * 64 + k0 + 8 * i);
+      o += __shfl_xor(o, 1, 64);
+      o += __shfl_xor(o, 2, 64);
+      if (q4 == 0) ob[r] = o + bout[r];
     }
-    ob[tid] = o;
   }
   __syncthreads();
   const int fr = tid >> 5, cl = tid & 31, c = cl * 8;
   const int f0 = (int)((long)s * T / S), f1 = (int)((long)(s + 1) * T / S);
-  for (int j = f0 + fr; j < f1; j += 8) {
-    bf16* xr = x + ((size_t)b * T + j) * UNI_C + c;
-    u32x4 w = *reinterpret_cast<const u32x4*>(xr);
-    float v[8];
+  constexpr int FB = 4;  // frames per thread per round: loads issued together, then the stores
+  for (int jb = f0 + fr; jb < f1; jb += 8 * FB) {
+    u32x4 wv[FB];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const bf16 lo = (bf16)(__uint_as_float(w[e] << 16) + ob[c + 2 * e]);
-      const bf16 hi = (bf16)(__uint_as_float(w[e] & 0xffff0000u) + ob[c + 2 * e + 1]);
-      v[2 * e] = (float)lo;
-      v[2 * e + 1] = (float)hi;
-      w[e] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+    for (int i = 0; i < FB; ++i) {
+      const int j = min(jb + 8 * i, f1 - 1);
+      wv[i] = *reinterpret_cast<const u32x4*>(x + ((size_t)b * T + j) * UNI_C + c);
     }
-    *reinterpret_cast<u32x4*>(xr) = w;
-    // (mean, M2) of the 64-channel slab (8 lanes x 8 channels), two-pass over the stored values
-    float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) sm += __shfl_xor(sm, o, 64);
-    const float mu = sm * (1.f / 64.f);
-    float q = 0.f;
+    for (int i = 0; i < FB; ++i) {
+      const int j = jb + 8 * i;
+      if (j >= f1) break;
+      u32x4 w = wv[i];
+      float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) q += (v[e] - mu) * (v[e] - mu);
+      for (int e = 0; e < 4; ++e) {
+        const bf16 lo = (bf16)(__uint_as_float(w[e] << 16) + ob[c + 2 * e]);
+        const bf16 hi = (bf16)(__uint_as_float(w[e] & 0xffff0000u) + ob[c + 2 * e + 1]);
+        v[2 * e] = (float)lo;
+        v[2 * e + 1] = (float)hi;
+        w[e] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+      }
+      *reinterpret_cast<u32x4*>(x + ((size_t)b * T + j) * UNI_C + c) = w;
+      // (mean, M2) of the 64-channel slab (8 lanes x 8 channels), two-pass over the stored values
+      float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1) q += __shfl_xor(q, o, 64);
-    if ((cl & 7) == 0) *reinterpret_cast<float2*>(row_out + 2 * (((size_t)b * T + j) * 4 + (cl >> 3))) = float2{mu, q};
+      for (int o = 1; o < 8; o <<= 1) sm += __shfl_xor(sm, o, 64);
+      const float mu = sm * (1.f / 64.f);
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q += (v[e] - mu) * (v[e] - mu);
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) q += __shfl_xor(q, o, 64);
+      if ((cl & 7) == 0) *reinterpret_cast<float2*>(row_out + 2 * (((size_t)b * T + j) * 4 + (cl >> 3))) = float2{mu, q};
+    }
   }
 }
 
