@@ -194,7 +194,8 @@ struct Vocoder {
   int resblock = 1, dtype = BF16, esize = 2;
   int fuse = 1;  // fused ResBlock stages (mt_rbfuse) where supported
   int vconv = 2; // LDS-DMA persistent convs (mt_vconv): 1 = C >= 128 stages, 2 = also C = 64 (per layer)
-  int pair = 1;  // the 64-channel stage's ResBlock pairs as one launch each (mt_vpair; needs vconv >= 2)
+  // the 64- and 32-channel stages' ResBlock pairs as one launch each (mt_vpair / mt_vpair32; needs vconv >= 2)
+  int pair = 1;
   size_t zero_off = 0;  // 256 zero bytes in the packed buffer (vconv padding rows)
   bool any_vc = false;
   std::vector<int> up_rates, up_kernels, rb_kernels;
@@ -212,6 +213,10 @@ struct Vocoder {
   int pack(const float* const* p, void* packed, hipStream_t st) const;
   bool stage_vc(int i) const;  // stage i runs its ResBlock convs through mt_vconv
   bool stage_vp(int i) const;  // ... as fused pairs (mt_vpair): its input needs no activated copy
+  bool stage_vp32(int i) const;  // a 32-channel stage as fused pairs (mt_vpair32, generic weight packing)
+  // stage i's ResBlocks as one fused-pair launch per pair: X -> XS (+ lrelu(XS) in RA when act_out)
+  int pair_chain(const char* P, int i, int B, int L, const char* X, char* XS, char* Tb, char* R, char* RA,
+                 char* trash, bool act_out, hipStream_t st) const;
   size_t frame_elems() const;  // max over stages of (samples per mel frame) x channels
   size_t workspace_bytes(int B, int T) const;
   int forward(const void* packed, const float* mel, int B, int T, float* wav, void* ws, size_t ws_bytes,

@@ -233,6 +233,68 @@ bool Vocoder::stage_vp(int i) const {
   return true;
 }
 
+bool Vocoder::stage_vp32(int i) const {
+  const int nk = (int)rb_kernels.size();
+  // (needs the zero rows and the trash area of a vconv model)
+  if (!pair || !fuse || vconv < 2 || !any_vc || dtype != BF16 || resblock != 1 || rb1[(size_t)i * nk].empty()) return false;
+  for (int j = 0; j < nk; ++j)
+    for (size_t q = 0; q < rb1[(size_t)i * nk + j].size(); ++q) {
+      const GemmW& a = rb1[(size_t)i * nk + j][q];
+      const GemmW& b = rb2[(size_t)i * nk + j][q];
+      for (const GemmW* g : {&a, &b})
+        if (g->cin != 32 || g->cout != 32 || g->Mpad != 32 || g->cin_pad != 32 || g->taps != g->k) return false;
+      if (!vpair32_supported(a.k, a.dil) || b.k != a.k || b.dil != 1) return false;
+    }
+  return true;
+}
+
+// One launch per pair (mt_vpair / mt_vpair32); the chain state ping-pongs between R and Tb (a pair reads its
+// input's halo, so it cannot write in place); the inputs' activations are applied in LDS.
+int Vocoder::pair_chain(const char* P, int i, int B, int L, const char* X, char* XS, char* Tb, char* R, char* RA,
+                        char* trash, bool act_out, hipStream_t st) const {
+  const int nk = (int)rb_kernels.size();
+  const bool c32 = rb1[(size_t)i * nk][0].cout == 32;
+  int rc;
+  for (int j = 0; j < nk; ++j) {
+    const std::vector<GemmW>& c1 = rb1[(size_t)i * nk + j];
+    const std::vector<GemmW>& c2 = rb2[(size_t)i * nk + j];
+    const int np = (int)c1.size();
+    const char* state = X;
+    for (int q = 0; q < np; ++q) {
+      const bool last = q == np - 1;
+      VPairArgs a{};
+      a.x = (const bf16*)state;
+      a.B = B;
+      a.L = L;
+      a.w1 = (const bf16*)(P + (c32 ? c1[q].w_off : c1[q].v_off));
+      a.b1 = (const float*)(P + c1[q].b_off);
+      a.w2 = (const bf16*)(P + (c32 ? c2[q].w_off : c2[q].v_off));
+      a.b2 = (const float*)(P + c2[q].b_off);
+      a.taps = c1[q].k;
+      a.dil = c1[q].dil;
+      a.div = (float)nk;
+      a.slope = 0.1f;
+      a.zero = (const bf16*)(P + zero_off);
+      a.trash = (bf16*)trash;
+      int ef = 0;
+      if (!last) {
+        a.y = (bf16*)((q & 1) ? Tb : R);
+      } else {
+        a.y = (bf16*)XS;
+        if (j > 0) ef |= VE_ACCUM;
+        if (j == nk - 1) ef |= VE_DIV;
+        if (j == nk - 1 && act_out) {  // lrelu(xs) for the next upsampler
+          a.y2 = (bf16*)RA;
+          ef |= VE_DUAL;
+        }
+      }
+      if ((rc = c32 ? launch_vpair32(ef, a, st) : launch_vpair(ef, a, st))) return rc;
+      state = (const char*)a.y;
+    }
+  }
+  return 0;
+}
+
 bool Vocoder::ups_vc(int i) const {
   return vconv && dtype == BF16 && ups[(size_t)i].vc && (i == 0 || stage_vc(i - 1));
 }
@@ -294,48 +356,7 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
   const int nk = (int)rb_kernels.size();
   const bf16* zero = (const bf16*)(P + zero_off);
   int rc;
-  if (stage_vp(i)) {
-    // one launch per pair; the chain state ping-pongs between R and Tb (a pair reads its input's halo, so it
-    // cannot write in place); activations of the inputs are applied in LDS
-    for (int j = 0; j < nk; ++j) {
-      const std::vector<GemmW>& c1 = rb1[(size_t)i * nk + j];
-      const std::vector<GemmW>& c2 = rb2[(size_t)i * nk + j];
-      const int np = (int)c1.size();
-      const char* state = X;
-      for (int q = 0; q < np; ++q) {
-        const bool last = q == np - 1;
-        VPairArgs a{};
-        a.x = (const bf16*)state;
-        a.B = B;
-        a.L = L;
-        a.w1 = (const bf16*)(P + c1[q].v_off);
-        a.b1 = (const float*)(P + c1[q].b_off);
-        a.w2 = (const bf16*)(P + c2[q].v_off);
-        a.b2 = (const float*)(P + c2[q].b_off);
-        a.taps = c1[q].k;
-        a.dil = c1[q].dil;
-        a.div = (float)nk;
-        a.slope = 0.1f;
-        a.zero = zero;
-        a.trash = (bf16*)trash;
-        int ef = 0;
-        if (!last) {
-          a.y = (bf16*)((q & 1) ? Tb : R);
-        } else {
-          a.y = (bf16*)XS;
-          if (j > 0) ef |= VE_ACCUM;
-          if (j == nk - 1) ef |= VE_DIV;
-          if (j == nk - 1 && act_out) {  // lrelu(xs) for the next upsampler
-            a.y2 = (bf16*)RA;
-            ef |= VE_DUAL;
-          }
-        }
-        if ((rc = launch_vpair(ef, a, st))) return rc;
-        state = (const char*)a.y;
-      }
-    }
-    return 0;
-  }
+  if (stage_vp(i)) return pair_chain(P, i, B, L, X, XS, Tb, R, RA, trash, act_out, st);
   for (int j = 0; j < nk; ++j) {
     const std::vector<GemmW>& c1 = rb1[(size_t)i * nk + j];
     const std::vector<GemmW>& c2 = rb2[(size_t)i * nk + j];
@@ -450,6 +471,13 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     }
     if (!done_up && (rc = launch_conv<E, PF_LRELU, 0>(u, st))) return rc;
     L = u.Tout;
+    if constexpr (std::is_same<E, bf16>::value) {
+      if (stage_vp32((int)i)) {
+        const bool act_out = i + 1 < ups.size() && ups_vc((int)i + 1);
+        if ((rc = pair_chain(P, (int)i, B, L, X, XS, Tb, R, RA, trash, act_out, st))) return rc;
+        continue;
+      }
+    }
     bool uniform = true;
     for (const auto& dl : rb_dils) uniform = uniform && dl.size() == rb_dils[0].size();
     if (fuse && resblock == 1 && nk <= 3 && rbfuse_supported(dtype, C) && uniform && rb_dils[0].size() <= 3) {

@@ -1,20 +1,20 @@
-// Fused HiFi-GAN ResBlock1 pair (conv_{k,d} -> lrelu -> conv_{k,1} -> + x) for the 64-channel stage, bf16:
-// the intermediate stays in LDS and the input's activation is applied on chip (see mt_vpair.hip).
+// Fused HiFi-GAN ResBlock1 pair (conv_{k,d} -> lrelu -> conv_{k,1} -> + x) for the 64- and 32-channel stages,
+// bf16: the intermediate stays in LDS and the input's activation is applied on chip (mt_vpair.hip, mt_vpair32.hip).
 #pragma once
 #include "mt_vconv.h"
 
 namespace mt {
 
 struct VPairArgs {
-  const bf16* x;        // [B][L][64] pair input (raw chain state; also the residual)
+  const bf16* x;        // [B][L][C] pair input (raw chain state; also the residual)
   int B, L;
-  const bf16* w1;       // mt_vconv image [1][taps][64][64] of convs1[q] (dilation dil)
-  const float* b1;      // [64]
+  const bf16* w1;       // C = 64: mt_vconv image [1][taps][64][64]; C = 32: generic packing [32][taps][32]
+  const float* b1;      // [C]
   const bf16* w2;       // image of convs2[q] (dilation 1)
-  const float* b2;      // [64]
+  const float* b2;      // [C]
   int taps, dil;
-  bf16* y;              // [B][L][64] output (must not alias x); VE_ACCUM: also read (xs += ...)
-  bf16* y2;             // [B][L][64] lrelu(y) (VE_DUAL: the next upsampler's input)
+  bf16* y;              // [B][L][C] output (must not alias x); VE_ACCUM: also read (xs += ...)
+  bf16* y2;             // [B][L][C] lrelu(y) (VE_DUAL: the next upsampler's input)
   float div, slope;     // VE_DIV divisor (nk), lrelu slope (0.1)
   const bf16* zero;     // >= 128 zero bytes
   bf16* trash;          // >= 1 KiB
@@ -23,5 +23,8 @@ struct VPairArgs {
 // epilogue flags: 0 | VE_ACCUM | VE_DIV | VE_DUAL combinations (mt_vconv.h values)
 bool vpair_supported(int C, int k, int d);
 int launch_vpair(int ef, const VPairArgs& a, hipStream_t st);
+// the 32-channel kernel (weights in the generic conv packing)
+bool vpair32_supported(int k, int d);
+int launch_vpair32(int ef, const VPairArgs& a, hipStream_t st);
 
 }  // namespace mt

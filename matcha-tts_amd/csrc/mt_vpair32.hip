@@ -1,0 +1,368 @@
+// Fused HiFi-GAN ResBlock1 PAIR for the 32-channel (last) stage, bf16, gfx950 — the 32-channel sibling of
+// mt_vpair.hip:
+//
+//   t = conv_{k, d}(lrelu(x)) ;  y = conv_{k, 1}(lrelu(t)) + x          (hifigan/models.py:90-97)
+//   (the last pair of resblock j: xs = [xs +] y [/ nk], models.py:187-192)
+//
+// One persistent 512-thread workgroup per CU walks tiles of 752 output frames of one utterance. Per tile:
+//   1. the RAW input rows (768 conv1 frames + the conv1 halo, <= 896 rows x 32 channels = 64 B) land in LDS by
+//      global_load_lds_dwordx4 (issued during the previous tile's second conv); one in-place VALU pass turns
+//      them into lrelu(rows);
+//   2. conv1: 32 rows x 768 frames over k taps; epilogue lrelu(round(acc + b1)), zero outside [0, L) -> T;
+//   3. conv2: 32 rows x 752 frames over k taps of T; epilogue + b2 + x [+ xs, / nk] -> y.
+// A tap is one K = 32 MFMA slice, so a step carries FOUR taps (8 KiB of weights, read straight from the generic
+// [32 rows][k][32] packing) and a wave covers 96 frames (6 fragments) x both 16-row fragments: 48 MFMAs per
+// wave between barriers, as in the 64-channel kernel.
+// LDS rows are 64 bytes (four 16-byte chunks); chunk c of row r lives in slot c ^ ((r >> 1) & 2). With the
+// ds_read_b128 lane groups ({0-3,12-15,20-27}, ...; MI355X_MICROARCH.md §LDS) every B-fragment read (16
+// consecutive rows from any start row, chunk g4) and every A-fragment read is conflict-free, and so are the
+// 8-lane groups of the epilogue's ds_write_b128 (checked exhaustively over start rows when the layout was chosen).
+// Rounding points and the per-output accumulation order (taps ascending, one K = 32 slice per tap) equal the
+// generic per-layer conv path's (mt_conv.hip: 32-channel chunks, taps in order), so the results are the same bits.
+#include <algorithm>
+
+#include "mt_probe.h"
+#include "mt_vpair.h"
+
+namespace mt {
+
+namespace {
+constexpr int NT = 512, C = 32;
+constexpr int FN = 6;                // 16-frame fragments per wave (8 waves along frames, both row fragments)
+constexpr int WNC = 16 * FN;         // frames per wave
+constexpr int NF1 = 8 * WNC;         // conv1 frames per tile: n0 - HALO2 .. n0 - HALO2 + 767
+constexpr int HALO2 = 8;             // >= (k - 1) / 2 of conv2
+constexpr int BN = NF1 - 2 * HALO2;  // output frames per tile (752)
+constexpr int RB = C * 2;            // bytes per LDS row
+constexpr int XROWS = NF1 + 128;     // staged input rows >= NF1 + 2 * h1, h1 = d (k - 1) / 2 <= 64
+constexpr int XBUF = XROWS * RB;
+constexpr int TROWS = NF1 + 16;      // conv2's last (discarded) fragment reads up to row NF1 - 1 + 16
+constexpr int TBUF = TROWS * RB;
+constexpr int TAPS = 4;              // taps per step
+constexpr int TAPW = C * RB;         // one tap: 32 output rows x 32 input channels (2 KiB)
+constexpr int WSLOT = TAPS * TAPW;
+constexpr int NWS = 3;
+constexpr int T_OFF = XBUF, W_OFF = T_OFF + TBUF, PAR_OFF = W_OFF + NWS * WSLOT;
+constexpr int LDS_BYTES = PAR_OFF + 2 * C * 4;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+static_assert(XROWS % 128 == 0 && WSLOT == 8 * 1024, "one 1 KiB DMA per wave per weight step");
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 2; }
+
+__device__ __forceinline__ void glds16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  if (n < 7) {
+    if (n < 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (n < 4) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else if (n < 15) {
+    if (n < 10) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  } else {
+    if (n < 23) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+    else if (n < 31) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(31)" ::: "memory");
+  }
+}
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+}  // namespace
+
+template <int EF>
+__global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g4 = lane >> 4, l16 = lane & 15, lrow = lane >> 2, lp = lane & 3;
+  const int k = a.taps, d = a.dil, L = a.L;
+  const int h1 = d * (k - 1) / 2, h2 = (k - 1) / 2;
+  const int ntn = (L + BN - 1) / BN, ntiles = a.B * ntn;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
+  const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
+  if (nmine == 0) return;
+  for (int i = tid; i < C; i += NT) {
+    reinterpret_cast<float*>(smem + PAR_OFF)[i] = a.b1[i];
+    reinterpret_cast<float*>(smem + PAR_OFF)[C + i] = a.b2[i];
+  }
+  __syncthreads();
+
+  int issued = 0, xmk = 0;
+  int wmk[NWS] = {};
+  const int ns = (k + TAPS - 1) / TAPS;  // steps per conv
+  const int S = nmine * 2 * ns;          // weight steps of this workgroup
+  auto tile_of = [&](int ti, int& b, int& n0) {
+    const int tile = gl + ti * G;
+    b = tile / ntn;
+    n0 = (tile - b * ntn) * BN;
+  };
+  // taps 4m .. 4m+3 (clamped to k-1) of conv1 or conv2 from the generic packing [32 rows][k][32]: wave w moves
+  // tap w / 2, rows (w & 1) * 16 .. + 15
+  auto stage_w = [&](int s) {
+    const int r2 = s % (2 * ns);
+    const int m = r2 < ns ? r2 : r2 - ns;
+    const bf16* w = r2 < ns ? a.w1 : a.w2;
+    const int u = wave >> 1, r = (wave & 1) * 16 + lrow;
+    const int t = min(TAPS * m + u, k - 1);
+    glds16(w + ((size_t)r * k + t) * C + (lp ^ swz(r)) * 8,
+           smem + W_OFF + (s % NWS) * WSLOT + u * TAPW + (wave & 1) * 1024);
+    issued += 1;
+    wmk[s % NWS] = issued;
+  };
+  auto stage_x = [&](int ti) {  // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r
+    int b, n0;
+    tile_of(ti, b, n0);
+    const bf16* xb = a.x + (size_t)b * L * C;
+    const int f0 = n0 - HALO2 - h1, R1 = NF1 + 2 * h1;
+#pragma unroll
+    for (int i = 0; i < XROWS / 128; ++i) {
+      const int j = wave + 8 * i;
+      const int r = 16 * j + lrow;
+      const int q = lp ^ swz(r);
+      const int f = f0 + r;
+      const bool ok = r < R1 && f >= 0 && f < L;
+      glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + j * 1024);
+    }
+    issued += XROWS / 128;
+    xmk = issued;
+  };
+
+  auto swap16 = [](uint32_t& x, uint32_t& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+  };
+  auto bf2 = [](uint32_t w, int i) -> float { return __uint_as_float(i ? (w & 0xffff0000u) : (w << 16)); };
+  auto pack2 = [](bf16 lo, bf16 hi) -> uint32_t {
+    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+  };
+
+  f32x4 acc[2][FN];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  struct Frag {
+    bf16x8 A[2], B[FN];
+  };
+  // tap u of a step: A = the slot's 2 row fragments of that tap, B = FN frame fragments at rows rb0 + 16 fn
+  auto read_frag = [&](Frag& F, int slot, int u, const char* src, int rb0) {
+    const char* pa = smem + W_OFF + slot * WSLOT + u * TAPW + l16 * RB + ((g4 ^ swz(l16)) * 16);
+#pragma unroll
+    for (int f = 0; f < 2; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 16 * RB);
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int rb = rb0 + fn * 16;
+      F.B[fn] = *reinterpret_cast<const bf16x8*>(src + rb * RB + ((g4 ^ swz(rb)) * 16));
+    }
+  };
+  // 2 x FN MFMAs of one tap with the reads of another tap interleaved, one per MFMA issue slot
+  auto mma_tap = [&](const Frag& F) {
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+    constexpr int NR = 2 + FN, NMF = 2 * FN;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF - NR, 0);
+  };
+  // one conv over `src`: ns steps of up to four taps (row of tap t for this lane's first fragment:
+  // rb0 + t * tstride); each tap's fragments are read under the previous tap's MFMAs, the next step's first
+  // tap under this step's last (a full step has an even tap count, so it always lands in F[0])
+  Frag F[2];
+  int s = 0;
+  auto conv = [&](const char* src, int rb0, int tstride, auto&& at_first_step) {
+    for (int m = 0; m < ns; ++m, ++s) {
+      const bool more = m + 1 < ns;
+      const int t0 = TAPS * m, nt = min(TAPS, k - t0);
+      wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);  // this step's weights and the next step's
+      barrier();
+      if (s + NWS - 1 < S) stage_w(s + NWS - 1);
+      const int sl = s % NWS;
+      if (m == 0) {
+        at_first_step();
+        read_frag(F[0], sl, 0, src, rb0);
+      }
+#pragma unroll
+      for (int u = 0; u < TAPS; ++u) {
+        if (u + 1 < nt) read_frag(F[(u + 1) & 1], sl, u + 1, src, rb0 + (t0 + u + 1) * tstride);
+        else if (u + 1 == TAPS && more) read_frag(F[0], (s + 1) % NWS, 0, src, rb0 + (t0 + TAPS) * tstride);
+        if (u < nt) mma_tap(F[u & 1]);
+      }
+    }
+  };
+
+  // ---- prologue ----
+  stage_x(0);
+#pragma unroll
+  for (int p = 0; p < NWS - 1; ++p)
+    if (p < S) stage_w(p);
+
+  const float* par = reinterpret_cast<const float*>(smem + PAR_OFF);
+  const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;  // this lane's 8 channels after the fragment swap
+  const int qc = (g4 & 1) * 2 + (g4 >> 1);         // ... as a 16-byte chunk index
+  for (int ti = 0; ti < nmine; ++ti) {
+    int b, n0;
+    tile_of(ti, b, n0);
+    // ---- 1. in-place lrelu of the landed raw rows ----
+    wait_vmcnt(issued - xmk);
+    barrier();
+#pragma unroll
+    for (int i = 0; i < XBUF / 16 / NT; ++i) {
+      const int e = tid + i * NT;
+      u32x4 v = *reinterpret_cast<const u32x4*>(smem + e * 16);
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        v[w] = pack2((bf16)lrelu_f(bf2(v[w], 0), a.slope), (bf16)lrelu_f(bf2(v[w], 1), a.slope));
+      *reinterpret_cast<u32x4*>(smem + e * 16) = v;
+    }
+    // ---- 2. conv1 (published by its first step's barrier) ----
+    zero_acc();
+    u32x4 rv[FN], yv[FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
+    conv(smem, wave * WNC + l16, d, [&] {
+      // the residual / old-xs rows of this tile's outputs: loaded now, consumed after conv2
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int i = min(n0 + wave * WNC + fn * 16 + l16, L - 1);
+        const size_t o = ((size_t)b * L + i) * C + ch16;
+        rv[fn] = *reinterpret_cast<const u32x4*>(a.x + o);
+        if constexpr ((EF & VE_ACCUM) != 0) yv[fn] = *reinterpret_cast<const u32x4*>(a.y + o);
+      }
+      issued += FN * ((EF & VE_ACCUM) ? 2 : 1);
+    });
+    // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - HALO2 + j), zero outside [0, L)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int j = wave * WNC + fn * 16 + l16;
+      const int f = n0 - HALO2 + j;
+      const bool ok = f >= 0 && f < L;
+      uint32_t o[2][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + h * 16 + 4 * g4);
+        bf16 ob[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bf16 rb = (bf16)(acc[h][fn][r] + b4[r]);
+          ob[r] = ok ? (bf16)lrelu_f((float)rb, a.slope) : (bf16)0.f;
+        }
+        o[h][0] = pack2(ob[0], ob[1]);
+        o[h][1] = pack2(ob[2], ob[3]);
+      }
+      swap16(o[0][0], o[1][0]);
+      swap16(o[0][1], o[1][1]);
+      *reinterpret_cast<u32x4*>(smem + T_OFF + j * RB + ((qc ^ swz(j)) * 16)) = u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
+    }
+    // ---- 3. conv2 ----
+    zero_acc();
+    conv(smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, [&] {
+      // every wave is past conv1's reads of the row buffer: stage the next tile's raw rows into it
+      if (ti + 1 < nmine) stage_x(ti + 1);
+    });
+    // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int i = wave * WNC + fn * 16 + l16;  // output frame n0 + i
+      uint32_t rx0 = rv[fn][0], rx1 = rv[fn][1], ry0 = rv[fn][2], ry1 = rv[fn][3];
+      swap16(rx0, ry0);  // back to the accumulator layout
+      swap16(rx1, ry1);
+      uint32_t yx0 = 0, yx1 = 0, yy0 = 0, yy1 = 0;
+      if constexpr ((EF & VE_ACCUM) != 0) {
+        yx0 = yv[fn][0], yx1 = yv[fn][1], yy0 = yv[fn][2], yy1 = yv[fn][3];
+        swap16(yx0, yy0);
+        swap16(yx1, yy1);
+      }
+      uint32_t o1[2][2], o2[2][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + C + h * 16 + 4 * g4);
+        const uint32_t rr[2] = {h ? ry0 : rx0, h ? ry1 : rx1};
+        const uint32_t yy[2] = {h ? yy0 : yx0, h ? yy1 : yx1};
+        bf16 ob[4], ab[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[h][fn][r] + b4[r];
+          v = v + bf2(rr[r >> 1], r & 1);
+          if constexpr ((EF & VE_ACCUM) != 0) v = bf2(yy[r >> 1], r & 1) + v;
+          if constexpr ((EF & VE_DIV) != 0) v = v / a.div;
+          ob[r] = (bf16)v;
+          ab[r] = (bf16)lrelu_f((float)ob[r], a.slope);
+        }
+        o1[h][0] = pack2(ob[0], ob[1]);
+        o1[h][1] = pack2(ob[2], ob[3]);
+        o2[h][0] = pack2(ab[0], ab[1]);
+        o2[h][1] = pack2(ab[2], ab[3]);
+      }
+      swap16(o1[0][0], o1[1][0]);
+      swap16(o1[0][1], o1[1][1]);
+      const bool ok = i < BN && n0 + i < L;
+      const size_t o = ((size_t)b * L + n0 + i) * C + ch16;
+      *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
+      if constexpr ((EF & VE_DUAL) != 0) {
+        swap16(o2[0][0], o2[1][0]);
+        swap16(o2[0][1], o2[1][1]);
+        *reinterpret_cast<u32x4*>(ok ? a.y2 + o : a.trash + 8 * lane) = u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]};
+      }
+    }
+    issued += FN * ((EF & VE_DUAL) ? 2 : 1);
+  }
+}
+
+bool vpair32_supported(int k, int d) { return k >= 2 && (k - 1) / 2 <= HALO2 && NF1 + d * (k - 1) <= XROWS; }
+
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+int launch_vpair32(int ef, const VPairArgs& a, hipStream_t st) {
+  MT_REQUIRE(a.x && a.w1 && a.w2 && a.b1 && a.b2 && a.y && a.zero && a.trash && a.B > 0 && a.L > 0,
+             "vpair32: null argument / empty");
+  MT_REQUIRE(vpair32_supported(a.taps, a.dil) && a.taps % 2 == 1, "vpair32: k %d d %d", a.taps, a.dil);
+  MT_REQUIRE(!(ef & VE_DUAL) || a.y2, "vpair32: y2");
+  MT_REQUIRE(a.y != a.x, "vpair32: y must not alias x (neighbour tiles read x's halo)");
+  const long ntiles = (long)a.B * ((a.L + BN - 1) / BN);
+  const int G = (int)std::min<long>(ntiles, cu_count());
+  const double flops = 2.0 * 2.0 * C * C * a.taps * (double)a.B * a.L;
+  const double bytes = 2.0 * (2.0 * 2.0 * C * (double)a.B * a.L) + 2.0 * 2.0 * C * C * a.taps;
+  probe_begin(PROBE_VCONV, st);
+  switch (ef) {
+    case 0: hipLaunchKernelGGL((vpair32_kernel<0>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_ACCUM: hipLaunchKernelGGL((vpair32_kernel<VE_ACCUM>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_ACCUM | VE_DIV: hipLaunchKernelGGL((vpair32_kernel<VE_ACCUM | VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_ACCUM | VE_DIV | VE_DUAL:
+      hipLaunchKernelGGL((vpair32_kernel<VE_ACCUM | VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a);
+      break;
+    case VE_DIV: hipLaunchKernelGGL((vpair32_kernel<VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_DIV | VE_DUAL: hipLaunchKernelGGL((vpair32_kernel<VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a); break;
+    default: set_error("vpair32: epilogue %d not compiled in", ef); return -1;
+  }
+  MT_CHECK_HIP(hipGetLastError());
+  probe_end(PROBE_VCONV, st, flops, bytes);
+  const int rec[VCLOG_FIELDS] = {ef | 0x10000, C, BN, 0, (int)ntiles, G, a.taps, C, C, a.B, a.L};
+  vclog_record(rec);
+  return 0;
+}
+
+}  // namespace mt

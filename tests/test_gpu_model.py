@@ -172,9 +172,11 @@ def test_vconv_stages_match_generic_per_layer(T):
 
 @pytest.mark.parametrize("B,T", [(2, 37), (3, 200)])
 def test_fused_pair_stage_bit_identical_to_per_layer(B, T):
-    """bf16: the 64-channel stage as fused ResBlock pairs (mt_vpair: intermediate in LDS, input activation
-    applied on chip, ping-pong chain state) reproduces the per-layer mt_vconv path bit for bit (same rounding
-    points, same MFMA accumulation order), including tile edges and utterance ends."""
+    """bf16: the 64- and 32-channel stages as fused ResBlock pairs (mt_vpair / mt_vpair32: intermediate in LDS,
+    input activation applied on chip, ping-pong chain state) reproduce the per-layer paths bit for bit (same
+    rounding points, same MFMA accumulation order), including tile edges and utterance ends. References: pair 0
+    (64-channel stage per layer on mt_vconv, 32-channel stage on the fused-stage kernel mt_rbfuse) and fusion 0
+    (32-channel stage on the generic per-layer conv kernel)."""
     g, gen = _gen("bf16", True)
     mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(7 + T)) * 2 - 5
     mel = mel.to(DEV)
@@ -182,9 +184,13 @@ def test_fused_pair_stage_bit_identical_to_per_layer(B, T):
     eng.set_pair(0)
     a = gen(mel)
     eng.set_pair(1)
+    eng.set_fusion(0)
+    c = gen(mel)
+    eng.set_fusion(1)
     b = gen(mel)
     assert torch.isfinite(b).all()
     assert torch.equal(a, b), (a - b).abs().max().item()
+    assert torch.equal(c, b), (c - b).abs().max().item()
 
 
 def test_packed_weights_follow_weight_updates():
@@ -388,7 +394,7 @@ def test_launch_probe_times_fused_stage():
 
 def test_launch_probe_times_vconv_launches():
     """PROBE_VCONV: events around every ResBlock-conv launch of the default vocoder (stages 1-2: 3
-    resblocks x 3 pairs x 2 per-layer convs; stage 3: 3 x 3 fused pairs), their algorithmic FLOPs summed."""
+    resblocks x 3 pairs x 2 per-layer convs; stages 3-4: 3 x 3 fused pairs each), their algorithmic FLOPs summed."""
     from matcha_hip import runtime as rt
     g, gen = _gen("bf16", True)
     mel = t(g["mel"], DEV)
@@ -397,8 +403,8 @@ def test_launch_probe_times_vconv_launches():
     gen(mel)
     p = rt.probe_stop()
     B, T = mel.shape[0], mel.shape[2]
-    assert p["launches"] == 36 + 9 and p["ms"] > 0
-    want = sum(2.0 * 6 * C * C * 21 * B * T * r for C, r in ((256, 8), (128, 64), (64, 128)))
+    assert p["launches"] == 36 + 18 and p["ms"] > 0
+    want = sum(2.0 * 6 * C * C * 21 * B * T * r for C, r in ((256, 8), (128, 64), (64, 128), (32, 256)))
     assert abs(p["flops"] - want) <= 1e-9 * want
 
 
