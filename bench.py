@@ -166,7 +166,7 @@ def roofline(probe, default_workload=True):
     x 2 convs; C = 256/128 on B x 8/64 * T_y frames) and stages 3-4 as fused conv pairs on mt_vpair /
     mt_vpair32 (2 x 9 launches, C = 64/32 on B x 128/256 * T_y frames; a pair launch is priced as its two
     convs); k = 3/7/11. Timed by HIP events recorded on
-    its launch stream around each of its launches INSIDE the timed region (mt_probe_*, site
+    its launch stream around each of its launches in the LAST step of the timed region (mt_probe_*, site
     PROBE_VCONV). Per launch (SURVEY.md §8d): algorithmic FLOPs = 2 * C_out * C_in * k * B * L;
     algorithmic bytes = layer-boundary bytes 2 * B * L * (C_in + C_out) (bf16 input read once, output
     written once) + weights. The family's intensity decides the bound against the bf16 ridge (2.5 PFLOP/s /
@@ -332,10 +332,15 @@ def main():
         torch.cuda.synchronize()
 
     from matcha_hip import runtime as rt
-    rt.probe_start(rt.PROBE_VCONV, 64 * a.steps)
+    # the probe brackets the family's launches of the LAST timed step only: each event pair leaves a few
+    # microseconds of idle before its launch, so the other timed steps run unprobed
+    rt.probe_start(rt.PROBE_VCONV, 64)
+    rt.probe_pause(True)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
+        if i == a.steps - 1:
+            rt.probe_pause(False)
         step(m, g, den, x, xl, a.n_timesteps, denoise, spk)
     barrier()
     el = time.perf_counter() - t0

@@ -315,17 +315,22 @@ int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, in
  * Launch probe (measurement only; no reference counterpart). Arms HIP events around every
  * launch of one kernel site, on the stream the kernel is launched on, so a benchmark can time
  * that kernel inside its own timed region. Sites: 1 = fused 64-channel HiFi-GAN ResBlock stage,
- * 2 = fused 32-channel stage, 3 = every mt_vconv launch of the HiFi-GAN ResBlock convs, 4 = the
+ * 2 = fused 32-channel stage, 3 = every HiFi-GAN ResBlock conv launch on mt_vconv and every fused conv-pair
+ * launch (mt_vpair / mt_vpair32, priced as its two convs), 4 = the
  * decoder's k >= 2 mt_vconv launches. mt_probe_stop synchronizes the recorded events and returns the
  * number of launches, their summed duration, the algorithmic FLOPs and layer-boundary bytes they did
  * (every conv reads its input once and writes its output once, + its weights), and
  * roof_ms = sum over launches of max(FLOPs / peak_flops, bytes / peak_bw) (peaks in FLOP/s, B/s).
+ * mt_probe_pause(1) stops recording (launches run unprobed) until mt_probe_pause(0); mt_probe_start
+ * arms the probe unpaused. A benchmark probes a sample of its timed steps this way, since each event
+ * pair adds a few microseconds of idle before the launch it brackets.
  * ------------------------------------------------------------------------------------- */
 #define MT_PROBE_RBFUSE_C64 1
 #define MT_PROBE_RBFUSE_C32 2
 #define MT_PROBE_VCONV 3
 #define MT_PROBE_VCONV_DEC 4
 int mt_probe_start(int site, int max_launches);
+int mt_probe_pause(int paused);
 int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes, double peak_flops, double peak_bw,
                   double* roof_ms);
 

@@ -13,6 +13,7 @@ int g_n = 0, g_cap = 0;
 double g_flops = 0, g_bytes = 0;
 std::vector<double> g_lf, g_lb;  // per launch: algorithmic FLOPs, bytes
 bool g_open = false;
+bool g_paused = false;
 
 void release() {
   for (hipEvent_t e : g_ev) (void)hipEventDestroy(e);
@@ -23,6 +24,7 @@ void release() {
   g_lb.clear();
   g_site = PROBE_NONE;
   g_open = false;
+  g_paused = false;
 }
 }  // namespace
 
@@ -31,7 +33,7 @@ bool probe_armed(int site) { return g_site != PROBE_NONE && g_site == site; }
 void probe_begin(int site, hipStream_t st) {
   if (!probe_armed(site)) return;
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_n >= g_cap || g_open) return;
+  if (g_n >= g_cap || g_open || g_paused) return;
   (void)hipEventRecord(g_ev[2 * g_n], st);
   g_open = true;
 }
@@ -58,6 +60,12 @@ int probe_start(int site, int max_launches) {
   for (hipEvent_t& e : g_ev) MT_CHECK_HIP(hipEventCreate(&e));
   g_cap = max_launches;
   g_site = site;
+  return 0;
+}
+
+int probe_pause(bool paused) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_paused = paused;
   return 0;
 }
 

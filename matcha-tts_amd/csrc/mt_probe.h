@@ -18,6 +18,7 @@ bool probe_armed(int site);
 void probe_begin(int site, hipStream_t st);
 void probe_end(int site, hipStream_t st, double flops, double bytes);
 int probe_start(int site, int max_launches);
+int probe_pause(bool paused);
 // roof_ms: sum over launches of max(flops / peak_flops, bytes / peak_bw) in ms (the roofline time)
 int probe_stop(int* launches, double* total_ms, double* flops, double* bytes, double peak_flops, double peak_bw,
                double* roof_ms);

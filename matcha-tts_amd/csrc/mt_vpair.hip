@@ -9,14 +9,13 @@
 //      turns them into lrelu(rows), so no producer has to store an activated copy;
 //   2. conv1: 64 rows x 384 frames (frames n0-8 .. n0+375) over k taps, B = the activated rows shifted by
 //      t*d; epilogue lrelu(round(acc + b1)), zero outside [0, L) (conv2's zero padding) -> T in LDS;
-//   3. conv2: 64 rows x 368 frames over k taps of T; epilogue + b2 + x (residual rows loaded from L2/HBM
-//      at conv1's first step) [+ xs, / nk] -> y (+ lrelu(y)).
+//   3. conv2: 64 rows x 368 frames over k taps of T; epilogue + b2 + x (the residual rows, read from the
+//      staged raw rows before step 1's in-place pass) [+ xs, / nk] -> y (+ lrelu(y)).
 // Waves: 8 along frames (48 frames = 3 fragments each), all 64 rows. Weights stream two taps (16 KiB) per
 // step (48 MFMAs per wave between barriers) through a 3-slot LDS ring; each step's wait covers the next
 // step's weights too, so the next step's first K-slice fragments are read under this step's MFMAs (the mt_vconv pipeline: counted vmcnt, one
 // s_barrier per step, XOR-swizzled 128-byte rows).
-// HBM traffic per pair: x read once (+ halo) and y written once (+ x re-read for the residual, mostly from
-// L2), instead of the per-layer path's x_act read, t written and read back, x read, y and y_act written.
+// HBM traffic per pair: x read once (+ halo) and y written once, instead of the per-layer path's x_act read, t written and read back, x read, y and y_act written.
 // Rounding points are the per-layer path's (every stored tensor rounded to bf16, lrelu of the rounded value)
 // and the MFMA accumulation order per output is the same (taps ascending, one 64-channel chunk, two K-slices),
 // so the results are the same bits.
@@ -219,8 +218,19 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   for (int ti = 0; ti < nmine; ++ti) {
     int b, n0;
     tile_of(ti, b, n0);
-    // ---- 1. in-place lrelu of the landed raw rows ----
+    // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + HALO2 + h1), then
+    // the in-place lrelu of the landed raw rows ----
     vp_wait_vmcnt(issued - xmk);
+    vp_barrier();
+    u32x4 rv[2][FN], yv[2][FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int r = wave * WNC + fn * 16 + l16 + HALO2 + h1;
+        const int q = fp * 4 + (g4 & 1) * 2 + (g4 >> 1);
+        rv[fp][fn] = *reinterpret_cast<const u32x4*>(smem + r * 128 + ((q ^ (r & 6)) * 16));
+      }
     vp_barrier();
 #pragma unroll
     for (int i = 0; i < XROWS * 8 / NT; ++i) {
@@ -233,19 +243,25 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     }
     // ---- 2. conv1 (published by its first step's barrier) ----
     zero_acc();
-    u32x4 rv[2][FN], yv[2][FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
+    int ymk = 0;
     conv(smem, wave * WNC + l16, d, [&] {
-      // the residual / old-xs rows of this tile's outputs: loaded now, consumed after conv2
+      // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2. Issued as asm so
+      // that the counted wait below retires them: hipcc drains EVERY in-flight LDS-DMA (vmcnt(0)) before the use
+      // of a compiler-visible load result, which would expose the next tile's row staging at each epilogue.
+      if constexpr ((EF & VE_ACCUM) != 0) {
 #pragma unroll
-      for (int fp = 0; fp < 2; ++fp)
+        for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int i = min(n0 + wave * WNC + fn * 16 + l16, L - 1);
-          const size_t o = ((size_t)b * L + i) * C + fp * 32 + ch16;
-          rv[fp][fn] = *reinterpret_cast<const u32x4*>(a.x + o);
-          if constexpr ((EF & VE_ACCUM) != 0) yv[fp][fn] = *reinterpret_cast<const u32x4*>(a.y + o);
-        }
-      issued += 2 * FN * ((EF & VE_ACCUM) ? 2 : 1);
+          for (int fn = 0; fn < FN; ++fn) {
+            const int i = min(n0 + wave * WNC + fn * 16 + l16, L - 1);
+            asm volatile("global_load_dwordx4 %0, %1, off"
+                         : "=v"(yv[fp][fn])
+                         : "v"(a.y + ((size_t)b * L + i) * C + fp * 32 + ch16)
+                         : "memory");
+          }
+        issued += 2 * FN;
+        ymk = issued;
+      }
     });
     // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - HALO2 + j), zero outside [0, L)
 #pragma unroll
@@ -282,6 +298,13 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       if (ti + 1 < nmine) stage_x(ti + 1);
     });
     // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
+    if constexpr ((EF & VE_ACCUM) != 0) {
+      vp_wait_vmcnt(issued - ymk);
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fp][fn]));  // no use of yv before the wait
+    }
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll

@@ -9,7 +9,8 @@
 //      global_load_lds_dwordx4 (issued during the previous tile's second conv); one in-place VALU pass turns
 //      them into lrelu(rows);
 //   2. conv1: 32 rows x 768 frames over k taps; epilogue lrelu(round(acc + b1)), zero outside [0, L) -> T;
-//   3. conv2: 32 rows x 752 frames over k taps of T; epilogue + b2 + x [+ xs, / nk] -> y.
+//   3. conv2: 32 rows x 752 frames over k taps of T; epilogue + b2 + x (the residual rows, read from the
+//      staged raw rows before step 1's in-place pass) [+ xs, / nk] -> y.
 // A tap is one K = 32 MFMA slice, so a step carries FOUR taps (8 KiB of weights, read straight from the generic
 // [32 rows][k][32] packing) and a wave covers 96 frames (6 fragments) x both 16-row fragments: 48 MFMAs per
 // wave between barriers, as in the 64-channel kernel.
@@ -99,15 +100,14 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   int issued = 0, xmk = 0;
   int wmk[NWS] = {};
   const int ns = (k + TAPS - 1) / TAPS;  // steps per conv
-  const int S = nmine * 2 * ns;          // weight steps of this workgroup
-  auto tile_of = [&](int ti, int& b, int& n0) {
+  auto tile_of = [&](int ti, int& b, int& n0) __attribute__((always_inline)) {
     const int tile = gl + ti * G;
     b = tile / ntn;
     n0 = (tile - b * ntn) * BN;
   };
   // taps 4m .. 4m+3 (clamped to k-1) of conv1 or conv2 from the generic packing [32 rows][k][32]: wave w moves
   // tap w / 2, rows (w & 1) * 16 .. + 15
-  auto stage_w = [&](int s) {
+  auto stage_w = [&](int s) __attribute__((always_inline)) {
     const int r2 = s % (2 * ns);
     const int m = r2 < ns ? r2 : r2 - ns;
     const bf16* w = r2 < ns ? a.w1 : a.w2;
@@ -118,11 +118,13 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     issued += 1;
     wmk[s % NWS] = issued;
   };
-  auto stage_x = [&](int ti) {  // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r
+  // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r (zero rows past this workgroup's last tile)
+  auto stage_x = [&](int ti) __attribute__((always_inline)) {
     int b, n0;
     tile_of(ti, b, n0);
-    const bf16* xb = a.x + (size_t)b * L * C;
-    const int f0 = n0 - HALO2 - h1, R1 = NF1 + 2 * h1;
+    const bool live = ti < nmine;
+    const bf16* xb = a.x + (size_t)(live ? b : 0) * L * C;
+    const int f0 = n0 - HALO2 - h1, R1 = live ? NF1 + 2 * h1 : 0;
 #pragma unroll
     for (int i = 0; i < XROWS / 128; ++i) {
       const int j = wave + 8 * i;
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   };
 
   f32x4 acc[2][FN];
-  auto zero_acc = [&]() {
+  auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     bf16x8 A[2], B[FN];
   };
   // tap u of a step: A = the slot's 2 row fragments of that tap, B = FN frame fragments at rows rb0 + 16 fn
-  auto read_frag = [&](Frag& F, int slot, int u, const char* src, int rb0) {
+  auto read_frag = [&](Frag& F, int slot, int u, const char* src, int rb0) __attribute__((always_inline)) {
     const char* pa = smem + W_OFF + slot * WSLOT + u * TAPW + l16 * RB + ((g4 ^ swz(l16)) * 16);
 #pragma unroll
     for (int f = 0; f < 2; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 16 * RB);
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     }
   };
   // 2 x FN MFMAs of one tap with the reads of another tap interleaved, one per MFMA issue slot
-  auto mma_tap = [&](const Frag& F) {
+  auto mma_tap = [&](const Frag& F) __attribute__((always_inline)) {
 #pragma unroll
     for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
@@ -183,35 +185,43 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   };
   // one conv over `src`: ns steps of up to four taps (row of tap t for this lane's first fragment:
   // rb0 + t * tstride); each tap's fragments are read under the previous tap's MFMAs, the next step's first
-  // tap under this step's last (a full step has an even tap count, so it always lands in F[0])
+  // tap under this step's last (a full step has an even tap count, so it always lands in F[0]).
+  // Every step stages a weight step unconditionally (past the last one: a harmless reload into the free
+  // slot) and the first step is peeled, so its global loads (conv1: the residual rows; conv2: the next tile's
+  // raw rows) are on every path: the compiler's own wait before the epilogue consumes the residual registers
+  // then counts past the >= 8 loads issued after them instead of draining the next tile's rows (vmcnt(0)).
   Frag F[2];
   int s = 0;
-  auto conv = [&](const char* src, int rb0, int tstride, auto&& at_first_step) {
-    for (int m = 0; m < ns; ++m, ++s) {
-      const bool more = m + 1 < ns;
-      const int t0 = TAPS * m, nt = min(TAPS, k - t0);
-      wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);  // this step's weights and the next step's
-      barrier();
-      if (s + NWS - 1 < S) stage_w(s + NWS - 1);
-      const int sl = s % NWS;
-      if (m == 0) {
-        at_first_step();
-        read_frag(F[0], sl, 0, src, rb0);
-      }
+  auto conv_step = [&](const char* src, int rb0, int tstride, int m) __attribute__((always_inline)) {
+    const bool more = m + 1 < ns;
+    const int t0 = TAPS * m, nt = min(TAPS, k - t0), sl = s % NWS;
 #pragma unroll
-      for (int u = 0; u < TAPS; ++u) {
-        if (u + 1 < nt) read_frag(F[(u + 1) & 1], sl, u + 1, src, rb0 + (t0 + u + 1) * tstride);
-        else if (u + 1 == TAPS && more) read_frag(F[0], (s + 1) % NWS, 0, src, rb0 + (t0 + TAPS) * tstride);
-        if (u < nt) mma_tap(F[u & 1]);
-      }
+    for (int u = 0; u < TAPS; ++u) {
+      if (u + 1 < nt) read_frag(F[(u + 1) & 1], sl, u + 1, src, rb0 + (t0 + u + 1) * tstride);
+      else if (u + 1 == TAPS && more) read_frag(F[0], (s + 1) % NWS, 0, src, rb0 + (t0 + TAPS) * tstride);
+      if (u < nt) mma_tap(F[u & 1]);
+    }
+  };
+  auto conv = [&](const char* src, int rb0, int tstride, auto&& at_first_step) __attribute__((always_inline)) {
+    wait_vmcnt(issued - wmk[(ns > 1 ? s + 1 : s) % NWS]);  // this step's weights and the next step's
+    barrier();
+    stage_w(s + NWS - 1);
+    at_first_step();
+    read_frag(F[0], s % NWS, 0, src, rb0);
+    conv_step(src, rb0, tstride, 0);
+    ++s;
+    for (int m = 1; m < ns; ++m, ++s) {
+      wait_vmcnt(issued - wmk[(m + 1 < ns ? s + 1 : s) % NWS]);
+      barrier();
+      stage_w(s + NWS - 1);
+      conv_step(src, rb0, tstride, m);
     }
   };
 
   // ---- prologue ----
   stage_x(0);
 #pragma unroll
-  for (int p = 0; p < NWS - 1; ++p)
-    if (p < S) stage_w(p);
+  for (int p = 0; p < NWS - 1; ++p) stage_w(p);
 
   const float* par = reinterpret_cast<const float*>(smem + PAR_OFF);
   const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;  // this lane's 8 channels after the fragment swap
@@ -219,8 +229,16 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   for (int ti = 0; ti < nmine; ++ti) {
     int b, n0;
     tile_of(ti, b, n0);
-    // ---- 1. in-place lrelu of the landed raw rows ----
+    // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + HALO2 + h1), then
+    // the in-place lrelu of the landed raw rows ----
     wait_vmcnt(issued - xmk);
+    barrier();
+    u32x4 rv[FN], yv[FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int r = wave * WNC + fn * 16 + l16 + HALO2 + h1;
+      rv[fn] = *reinterpret_cast<const u32x4*>(smem + r * RB + ((qc ^ swz(r)) * 16));
+    }
     barrier();
 #pragma unroll
     for (int i = 0; i < XBUF / 16 / NT; ++i) {
@@ -233,17 +251,23 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     }
     // ---- 2. conv1 (published by its first step's barrier) ----
     zero_acc();
-    u32x4 rv[FN], yv[FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
+    int ymk = 0;
     conv(smem, wave * WNC + l16, d, [&] {
-      // the residual / old-xs rows of this tile's outputs: loaded now, consumed after conv2
+      // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2. Issued as asm so
+      // that the counted wait below retires them: hipcc drains EVERY in-flight LDS-DMA (vmcnt(0)) before the use
+      // of a compiler-visible load result, which would expose the next tile's row staging at each epilogue.
+      if constexpr ((EF & VE_ACCUM) != 0) {
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        const int i = min(n0 + wave * WNC + fn * 16 + l16, L - 1);
-        const size_t o = ((size_t)b * L + i) * C + ch16;
-        rv[fn] = *reinterpret_cast<const u32x4*>(a.x + o);
-        if constexpr ((EF & VE_ACCUM) != 0) yv[fn] = *reinterpret_cast<const u32x4*>(a.y + o);
+        for (int fn = 0; fn < FN; ++fn) {
+          const int i = min(n0 + wave * WNC + fn * 16 + l16, L - 1);
+          asm volatile("global_load_dwordx4 %0, %1, off"
+                       : "=v"(yv[fn])
+                       : "v"(a.y + ((size_t)b * L + i) * C + ch16)
+                       : "memory");
+        }
+        issued += FN;
+        ymk = issued;
       }
-      issued += FN * ((EF & VE_ACCUM) ? 2 : 1);
     });
     // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - HALO2 + j), zero outside [0, L)
 #pragma unroll
@@ -272,9 +296,14 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     zero_acc();
     conv(smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, [&] {
       // every wave is past conv1's reads of the row buffer: stage the next tile's raw rows into it
-      if (ti + 1 < nmine) stage_x(ti + 1);
+      stage_x(ti + 1);
     });
     // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
+    if constexpr ((EF & VE_ACCUM) != 0) {
+      wait_vmcnt(issued - ymk);
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fn]));  // no use of yv before the wait
+    }
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       const int i = wave * WNC + fn * 16 + l16;  // output frame n0 + i
@@ -321,6 +350,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     }
     issued += FN * ((EF & VE_DUAL) ? 2 : 1);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing row / weight DMAs land before LDS is freed
 }
 
 bool vpair32_supported(int k, int d) { return k >= 2 && (k - 1) / 2 <= HALO2 && NF1 + d * (k - 1) <= XROWS; }

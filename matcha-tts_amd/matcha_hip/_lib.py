@@ -83,6 +83,7 @@ SIGNATURES = {
                             c_int, P, c_size_t, P]),
     "mt_op_attention": (c_int, [c_int, P, P, P, c_int, c_int, c_int, P]),
     "mt_probe_start": (c_int, [c_int, c_int]),
+    "mt_probe_pause": (c_int, [c_int]),
     "mt_probe_stop": (c_int, [P, P, P, P, c_double, c_double, P]),
     "mtt_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_float, P, c_int, c_int64, P, c_int, c_int64, c_float,
                          P, c_int, c_int64, c_int, P, P, P, c_size_t, P]),

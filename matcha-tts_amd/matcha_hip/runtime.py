@@ -536,6 +536,11 @@ def probe_start(site: int, max_launches: int) -> None:
     check(lib().mt_probe_start(int(site), int(max_launches)), "probe_start")
 
 
+def probe_pause(paused: bool) -> None:
+    """Stop (True) / resume (False) recording without disarming (see mt_probe_pause)."""
+    check(lib().mt_probe_pause(int(bool(paused))), "probe_pause")
+
+
 def probe_stop(peak_flops: float = 2.5e15, peak_bw: float = 8.0e12) -> Dict[str, float]:
     """Synchronize the probe's events: launches, summed kernel ms, algorithmic FLOPs and layer-boundary
     bytes, and the summed per-launch roofline time max(F / peak_flops, B / peak_bw) in ms (defaults: the
