@@ -114,6 +114,11 @@ int mt_cfm_solve_bounded(const mt_decoder* d, const void* packed, const float* z
 /* 1 (default): mt_cfm_solve_bounded takes the query-independent attention path where max_valid allows it;
  * 0: always the general Q.K^T path (A/B, tests) */
 int mt_decoder_set_uniform_attention(mt_decoder* d, int enable);
+/* 1 (default): mt_cfm_solve / mt_cfm_solve_bounded replay the evaluation chain (time embedding + every estimator
+ * evaluation) as a captured hipGraph, cached per (packed, workspace, B, T, steps, solver, path flags); the caller's
+ * mask is staged into the workspace first, so replays read no caller pointer. 0: direct launches. Bypassed while a
+ * launch probe or the launch log is armed. Same results either way. */
+int mt_decoder_set_graphs(mt_decoder* d, int enable);
 
 size_t mt_decoder_step_workspace_bytes(const mt_decoder* d, int B, int T);
 /* one estimator evaluation: out = Decoder.forward(x, mask, mu_y, t, spks) [B,80,T] */

@@ -146,6 +146,11 @@ int mt_decoder_set_uniform_attention(mt_decoder* d, int enable) {
   d->d.uniform_attn = enable ? 1 : 0;
   return 0;
 }
+int mt_decoder_set_graphs(mt_decoder* d, int enable) {
+  MT_REQUIRE(d, "null decoder");
+  d->d.graphs = enable ? 1 : 0;
+  return 0;
+}
 size_t mt_decoder_step_workspace_bytes(const mt_decoder* d, int B, int T) {
   return d ? d->d.workspace_bytes(B, T, 1) : 0;
 }

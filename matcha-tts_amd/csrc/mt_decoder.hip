@@ -404,6 +404,7 @@ size_t Decoder::workspace_bytes(int B, int T, int S) const {
   n += align256(attention_part_bytes(B, T, heads));   // attention key-split slots
   n += align256(BT * (C / 64) * 2 * 4);               // lnp
   n += align256((size_t)B * 8 * 260 * 4);             // upart
+  n += align256(BT * 4);                              // mst
   return n;
 }
 
@@ -444,6 +445,7 @@ Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
   w.apart = (float*)take(attention_part_bytes(B, T, heads));
   w.lnp = (float*)take(BT * (C / 64) * 2 * 4);
   w.upart = (float*)take((size_t)B * 8 * 260 * 4);
+  w.mst = (float*)take(BT * 4);
   w.m0 = nullptr;
   return w;
 }
@@ -830,6 +832,69 @@ static int check_geom(int B, int T) {
   return 0;
 }
 
+// ---- captured evaluation chains (hipGraph) ----
+struct Decoder::GraphCache {
+  struct Entry {
+    const void* P;
+    const void* ws;
+    int B, T, S, n_steps, solver, uni0, uni1, vconv, gnres, uniform_attn;
+    hipGraphExec_t ex;
+  };
+  std::vector<Entry> entries;  // most recently used last
+  hipStream_t cap = nullptr;   // private capture stream (the legacy null stream cannot be captured)
+  ~GraphCache() {
+    for (Entry& e : entries) (void)hipGraphExecDestroy(e.ex);
+    if (cap) (void)hipStreamDestroy(cap);
+  }
+};
+
+namespace {
+constexpr size_t kMaxGraphs = 8;
+}
+
+int Decoder::chain_graph(const char* P, const Work& w, const TimeSched& ts, int S, int B, int T, int n_steps,
+                         int solver, const void* ws, hipGraphExec_t* out) const {
+  if (!gcache) gcache = std::make_shared<GraphCache>();
+  GraphCache& gc = *gcache;
+  const GraphCache::Entry key{P, ws, B, T, S, n_steps, solver, w.uni0, w.uni1, vconv, gnres, uniform_attn, nullptr};
+  for (size_t i = 0; i < gc.entries.size(); ++i) {
+    const GraphCache::Entry& e = gc.entries[i];
+    if (e.P == key.P && e.ws == key.ws && e.B == key.B && e.T == key.T && e.S == key.S && e.n_steps == key.n_steps &&
+        e.solver == key.solver && e.uni0 == key.uni0 && e.uni1 == key.uni1 && e.vconv == key.vconv &&
+        e.gnres == key.gnres && e.uniform_attn == key.uniform_attn) {
+      GraphCache::Entry hit = e;
+      gc.entries.erase(gc.entries.begin() + (long)i);
+      gc.entries.push_back(hit);
+      *out = hit.ex;
+      return 0;
+    }
+  }
+  if (!gc.cap) MT_CHECK_HIP(hipStreamCreateWithFlags(&gc.cap, hipStreamNonBlocking));
+  MT_CHECK_HIP(hipStreamBeginCapture(gc.cap, hipStreamCaptureModeThreadLocal));
+  const int rc = solve_chain(P, w, ts, S, B, T, n_steps, solver, gc.cap);
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(gc.cap, &g);
+  if (rc || e != hipSuccess || !g) {
+    if (g) (void)hipGraphDestroy(g);
+    if (rc) return rc;
+    set_error("decoder: graph capture failed (%s)", hipGetErrorString(e));
+    return -1;
+  }
+  hipGraphExec_t ex = nullptr;
+  const hipError_t ie = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  MT_CHECK_HIP(ie);
+  if (gc.entries.size() >= kMaxGraphs) {
+    (void)hipGraphExecDestroy(gc.entries.front().ex);
+    gc.entries.erase(gc.entries.begin());
+  }
+  GraphCache::Entry ent = key;
+  ent.ex = ex;
+  gc.entries.push_back(ent);
+  *out = ex;
+  return 0;
+}
+
 int Decoder::solve(const void* packed, const float* z_noise, float temperature, const float* mu_y,
                    const float* mask, const float* spks, int B, int T, int n_steps, int solver, float* z_out,
                    void* ws, size_t ws_bytes, hipStream_t st, int max_valid) const {
@@ -861,8 +926,26 @@ int Decoder::solve(const void* packed, const float* z_noise, float temperature, 
       ts.t[2 * i + 1] = t + dt * 0.5f;
     }
   }
-  if ((rc = time_embed(P, w, ts, S, st))) return rc;
+  if (!(graphs && !probe_any_armed() && !vclog_armed())) {
+    if ((rc = init_inputs(w, z_noise, temperature, mu_y, spks, B, T, st))) return rc;
+    if ((rc = solve_chain(P, w, ts, S, B, T, n_steps, solver, st))) return rc;
+    return btc_to_bct(F32, w.zm, NF, 0, B, NF, T, z_out, st);
+  }
+  // graph path: the chain reads only the packed weights and the workspace (inputs and mask staged into it)
+  MT_CHECK_HIP(hipMemcpyAsync(w.mst, mask, (size_t)B * T * 4, hipMemcpyDeviceToDevice, st));
+  w.m0 = w.mst;
   if ((rc = init_inputs(w, z_noise, temperature, mu_y, spks, B, T, st))) return rc;
+  hipGraphExec_t ex = nullptr;
+  if ((rc = chain_graph(P, w, ts, S, B, T, n_steps, solver, ws, &ex))) return rc;
+  MT_CHECK_HIP(hipGraphLaunch(ex, st));
+  return btc_to_bct(F32, w.zm, NF, 0, B, NF, T, z_out, st);
+}
+
+int Decoder::solve_chain(const char* P, const Work& w, const TimeSched& ts, int S, int B, int T, int n_steps,
+                         int solver, hipStream_t st) const {
+  int rc;
+  const float dt = (float)(1.0 / (double)n_steps);
+  if ((rc = time_embed(P, w, ts, S, st))) return rc;
   for (int i = 0; i < n_steps; ++i) {
     if (solver == 0) {
       Euler eu{dt, 0, 1};
@@ -877,7 +960,7 @@ int Decoder::solve(const void* packed, const float* z_noise, float temperature, 
       if (rc) return rc;
     }
   }
-  return btc_to_bct(F32, w.zm, NF, 0, B, NF, T, z_out, st);
+  return 0;
 }
 
 int Decoder::step(const void* packed, const float* x, const float* mu_y, const float* mask, const float* spks,

@@ -3,6 +3,7 @@
 // (names and shapes, canonical order) and the byte layout of its packed weight buffer.
 // The caller (PyTorch) owns every device buffer; these objects hold host metadata only.
 #pragma once
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -103,6 +104,7 @@ struct Decoder {
     float* apart;  // attention key-split slots
     float* lnp;    // per frame, per 64-channel slab (sum, sum of squares): LayerNorm partials (vconv VE_ROWSTATS)
     float* upart;  // query-independent attention: per (utterance, slice) masked sums of the normalised rows
+    float* mst;    // the solve's staged copy of the caller's mask (graph replays read only the workspace)
     int tb_ld;     // 0: one time bias per evaluation; n_res * C: one per utterance (step_times)
     const float* m0;
     // every utterance has padded frames at the full- / half-resolution level (the caller's max_valid < T /
@@ -142,6 +144,18 @@ struct Decoder {
   // 1 (default): the query-independent attention path when the caller's max_valid allows it; 0: always the
   // general Q.K^T path (A/B, tests)
   int uniform_attn = 1;
+  // 1 (default): solve() replays its evaluation chain (time embedding + every estimator evaluation, ~550
+  // launches for 10 Euler steps) as a captured hipGraph, keyed by (packed, workspace, geometry, path flags);
+  // 0: launches it directly. Bypassed while a launch probe or the launch log is armed.
+  int graphs = 1;
+  struct GraphCache;
+  mutable std::shared_ptr<GraphCache> gcache;
+  // the solve's evaluation chain: time embedding + n_steps Euler / midpoint steps on stream st
+  int solve_chain(const char* P, const Work& w, const TimeSched& ts, int S, int B, int T, int n_steps, int solver,
+                  hipStream_t st) const;
+  // the cached executable graph of solve_chain for this key, captured on first use
+  int chain_graph(const char* P, const Work& w, const TimeSched& ts, int S, int B, int T, int n_steps, int solver,
+                  const void* ws, hipGraphExec_t* out) const;
   int step(const void* packed, const float* x, const float* mu_y, const float* mask, const float* spks,
            float t, int B, int T, float* out, void* ws, size_t ws_bytes, hipStream_t st) const;
   int step_times(const void* packed, const float* x, const float* mu_y, const float* mask, const float* spks,

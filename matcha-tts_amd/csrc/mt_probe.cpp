@@ -29,6 +29,7 @@ void release() {
 }  // namespace
 
 bool probe_armed(int site) { return g_site != PROBE_NONE && g_site == site; }
+bool probe_any_armed() { return g_site != PROBE_NONE; }
 
 void probe_begin(int site, hipStream_t st) {
   if (!probe_armed(site)) return;
@@ -116,6 +117,8 @@ int vclog_start(int cap) {
   g_log_on = true;
   return 0;
 }
+
+bool vclog_armed() { return g_log_on; }
 
 int vclog_stop(int* out, int cap) {
   std::lock_guard<std::mutex> lk(g_mu);

@@ -15,6 +15,7 @@ enum ProbeSite {
 };
 
 bool probe_armed(int site);
+bool probe_any_armed();  // some site armed (its launches need per-launch host bookkeeping)
 void probe_begin(int site, hipStream_t st);
 void probe_end(int site, hipStream_t st, double flops, double bytes);
 int probe_start(int site, int max_launches);
@@ -30,5 +31,6 @@ constexpr int VCLOG_FIELDS = 11;  // ef, BM, BN, K1, ntiles, grid, taps, M, cin,
 void vclog_record(const int (&rec)[VCLOG_FIELDS]);
 int vclog_start(int cap);
 int vclog_stop(int* out, int cap);  // -> records written (cap records of VCLOG_FIELDS ints)
+bool vclog_armed();
 
 }  // namespace mt

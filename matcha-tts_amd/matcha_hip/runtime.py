@@ -260,6 +260,10 @@ class DecoderEngine:
         """1 (default): query-independent attention where the caller's max_valid proves every utterance padded."""
         check(lib().mt_decoder_set_uniform_attention(self.h, int(bool(enable))), "decoder_set_uniform_attention")
 
+    def set_graphs(self, enable) -> None:
+        """1 (default): solve() replays its evaluation chain as a cached hipGraph; 0: direct launches."""
+        check(lib().mt_decoder_set_graphs(self.h, int(bool(enable))), "decoder_set_graphs")
+
     def solve(self, packed, z_noise, temperature, mu_y, mask, spks, n_timesteps, solver="euler",
               out=None, max_valid: int = 0):
         """max_valid: the most valid frames of any utterance (synthesize's y_max), 0 when unknown."""

@@ -443,3 +443,47 @@ def test_cfm_query_independent_attention_path(lens, T):
         assert not torch.equal(uni, gen)  # the path was actually taken
     else:
         assert torch.equal(uni, gen)
+
+
+@pytest.mark.parametrize("solver", ["euler", "midpoint"])
+def test_cfm_graph_replay_bit_identical(solver):
+    """mt_cfm_solve replays its evaluation chain as a cached hipGraph (mt_decoder_set_graphs, default on). The
+    replay equals the direct launches bit for bit, on fresh input tensors at new addresses (the mask and inputs are
+    staged into the workspace, so a replay reads no stale caller pointer), after an in-place weight update (a
+    repacked buffer, a new cache key) and on the query-independent attention path (max_valid < T)."""
+    from matcha_hip import synthetic
+    dec = make_decoder(160, "bf16")
+    sd = {k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(
+        [(k, tuple(v.shape)) for k, v in dec.state_dict().items()], 23).items()}
+    dec = _load(dec, sd)
+    lens, T = [300, 251, 120], 304
+    B = len(lens)
+    eng = dec.engine()
+
+    def inputs(seed):
+        g = torch.Generator().manual_seed(seed)
+        mask = (torch.arange(T)[None] < torch.tensor(lens)[:, None]).float()[:, None]
+        mu = torch.randn(B, 80, T, generator=g) * mask
+        z = torch.randn(B, 80, T, generator=g) * 0.667
+        return mu.cuda(), z.cuda(), mask.cuda()
+
+    def run(graphs, seed, mv):
+        eng.set_graphs(graphs)
+        mu, z, mask = inputs(seed)
+        return eng.solve(dec.packed(torch.device("cuda")), z, 1.0, mu, mask, None, 3, solver=solver,
+                         max_valid=mv).cpu()
+
+    try:
+        for mv in (0, max(lens)):
+            direct = [run(0, s, mv) for s in (1, 2)]
+            graph = [run(1, s, mv) for s in (1, 2, 1)]  # capture, replay on new inputs, replay again
+            assert torch.isfinite(graph[0]).all()
+            assert torch.equal(graph[0], direct[0]) and torch.equal(graph[1], direct[1])
+            assert torch.equal(graph[2], direct[0])
+            assert not torch.equal(direct[0], direct[1])
+        with torch.no_grad():
+            dec.final_proj.weight.mul_(0.5)
+        d2, g2 = run(0, 1, 0), run(1, 1, 0)
+        assert torch.equal(d2, g2) and not torch.equal(d2, direct[0])
+    finally:
+        eng.set_graphs(1)
