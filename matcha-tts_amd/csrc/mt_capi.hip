@@ -81,6 +81,11 @@ int mt_encoder_pack(const mt_encoder* e, const float* const* params, void* packe
   return e->e.pack(params, packed, (hipStream_t)stream);
 }
 size_t mt_encoder_workspace_bytes(const mt_encoder* e, int B, int Tx) { return e ? e->e.workspace_bytes(B, Tx) : 0; }
+int mt_encoder_set_mfma_attention(mt_encoder* e, int enable) {
+  MT_REQUIRE(e, "null encoder");
+  e->e.mfma_attn = enable ? 1 : 0;
+  return 0;
+}
 int mt_encoder_forward(const mt_encoder* e, const void* packed, const int64_t* x, const int64_t* x_lengths,
                        const float* spks, int B, int Tx, float* mu, float* logw, float* x_mask, void* ws,
                        size_t ws_bytes, void* stream) {

@@ -102,6 +102,144 @@ __global__ void rope_kernel(E* __restrict__ qkv, int rows, int Tx, int W, int he
 }
 
 // ---------------------------------------------------------------------------------------
+// The same attention core for bf16 and dk = 96 on MFMA (v_mfma_f32_16x16x32_bf16). Workgroup = 64 queries
+// (4 waves x 16) of one (utterance, head); key tiles of 64 stream through LDS.
+//   S^T = K . Q^T per wave: A = K rows (LDS, 224-byte rows), B = this wave's Q rows (registers, loaded once);
+//   two 16-key blocks X / Y per 32-key slice take the keys {0-7, 16-23} / {8-15, 24-31}, so that one
+//   v_permlane16_swap of their bf16 probabilities leaves lane row g4 holding keys 8 g4 .. 8 g4 + 7 of one
+//   query: exactly the B operand of O^T = V^T . P^T, with A = V^T rows (LDS, transposed at staging,
+//   160-byte rows). Both LDS strides make every ds_read_b128 lane group conflict-free (exhaustive check).
+// Per query the softmax runs online over the key tiles in fp32 (max / sum over the 4 lanes holding its keys);
+// P enters the second product as bf16. Masked (query, key) pairs := -1e4 as the reference; key tiles that
+// are all padding and query tiles that are all padding are skipped exactly as in enc_attn_kernel.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void enc_attn_mfma96_kernel(const bf16* __restrict__ qkv,
+                                                              const float* __restrict__ xmask, float sdiv, int Tx,
+                                                              int heads, bf16* __restrict__ out) {
+  constexpr int DK = 96, KRS = 224, VRS = 160;
+  __shared__ __attribute__((aligned(16))) char Ks[64 * KRS];
+  __shared__ __attribute__((aligned(16))) char Vt[DK * VRS];
+  __shared__ float km[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g4 = lane >> 4, l16 = lane & 15;
+  const int h = blockIdx.y, b = blockIdx.z, t0 = blockIdx.x * 64;
+  const int W = heads * DK, ld = 3 * W;
+  const bf16* base = qkv + (size_t)b * Tx * ld + h * DK;
+  const int tq = t0 + 16 * wave + l16;  // this lane's query (column of S^T / O^T)
+  bf16x8 qf[3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks)
+    qf[ks] = *reinterpret_cast<const bf16x8*>(base + (size_t)min(tq, Tx - 1) * ld + ks * 32 + 8 * g4);
+  const float mq = tq < Tx ? xmask[(size_t)b * Tx + tq] : 0.f;
+  f32x4 o[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrun = -INFINITY, lrun = 0.f;
+  auto keyX = [](int i) { return i < 8 ? i : i + 8; };
+  auto keyY = [](int i) { return i < 8 ? i + 8 : i + 16; };
+  const bool any_q = __syncthreads_or(mq != 0.f);
+  for (int k0 = 0; any_q && k0 < Tx; k0 += 64) {
+    const bool kval = tid < 64 && k0 + tid < Tx && xmask[(size_t)b * Tx + k0 + tid] != 0.f;
+    if (!__syncthreads_or(kval)) continue;
+    // K rows as they are; V transposed (dim-major) for the A operand of O^T
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int e = tid + 256 * i, r = e / 12, c = e - r * 12;
+      const int t = k0 + r;
+      u32x4 kv = {0u, 0u, 0u, 0u}, vv = {0u, 0u, 0u, 0u};
+      if (t < Tx) {
+        const bf16* src = base + (size_t)t * ld + c * 8;
+        kv = *reinterpret_cast<const u32x4*>(src + W);
+        vv = *reinterpret_cast<const u32x4*>(src + 2 * W);
+      }
+      *reinterpret_cast<u32x4*>(Ks + r * KRS + c * 16) = kv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        *reinterpret_cast<uint16_t*>(Vt + (c * 8 + 2 * j) * VRS + r * 2) = (uint16_t)(vv[j] & 0xffffu);
+        *reinterpret_cast<uint16_t*>(Vt + (c * 8 + 2 * j + 1) * VRS + r * 2) = (uint16_t)(vv[j] >> 16);
+      }
+    }
+    if (tid < 64) km[tid] = k0 + tid < Tx ? xmask[(size_t)b * Tx + k0 + tid] : 0.f;
+    __syncthreads();
+    // S^T for the tile: blocks (X, Y) of slices 0 and 1
+    f32x4 s[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      s[s2][0] = s[s2][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char* ax = Ks + (32 * s2 + keyX(l16)) * KRS + g4 * 16;
+      const char* ay = Ks + (32 * s2 + keyY(l16)) * KRS + g4 * 16;
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        s[s2][0] = mfma16(*reinterpret_cast<const bf16x8*>(ax + ks * 64), qf[ks], s[s2][0]);
+        s[s2][1] = mfma16(*reinterpret_cast<const bf16x8*>(ay + ks * 64), qf[ks], s[s2][1]);
+      }
+    }
+    // scale, mask, online softmax (this lane: 16 keys of query tq; the other 48 keys on lanes l16 + 16 j)
+    float cmax = -INFINITY;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int xy = 0; xy < 2; ++xy)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int kk = 32 * s2 + (xy ? keyY(4 * g4 + r) : keyX(4 * g4 + r));
+          float sc = s[s2][xy][r] / sdiv;
+          if (mq * km[kk] == 0.f) sc = -1e4f;
+          if (k0 + kk >= Tx) sc = -INFINITY;
+          s[s2][xy][r] = sc;
+          cmax = fmaxf(cmax, sc);
+        }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    const float mnew = fmaxf(mrun, cmax);
+    const float corr = expf(mrun - mnew);
+    lrun *= corr;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) o[i] *= corr;
+    mrun = mnew;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      uint32_t pk[2][2];
+#pragma unroll
+      for (int xy = 0; xy < 2; ++xy) {
+        float p[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p[r] = expf(s[s2][xy][r] - mnew);
+          lrun += p[r];
+        }
+        pk[xy][0] = (uint32_t)__builtin_bit_cast(uint16_t, (bf16)p[0]) |
+                    ((uint32_t)__builtin_bit_cast(uint16_t, (bf16)p[1]) << 16);
+        pk[xy][1] = (uint32_t)__builtin_bit_cast(uint16_t, (bf16)p[2]) |
+                    ((uint32_t)__builtin_bit_cast(uint16_t, (bf16)p[3]) << 16);
+      }
+      const auto r0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+      const auto r1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+      const u32x4 pb = {r0[0], r1[0], r0[1], r1[1]};  // keys 32 s2 + 8 g4 .. + 7 of query tq
+      const bf16x8 bp = __builtin_bit_cast(bf16x8, pb);
+#pragma unroll
+      for (int db = 0; db < 6; ++db)
+        o[db] = mfma16(*reinterpret_cast<const bf16x8*>(Vt + (16 * db + l16) * VRS + (4 * s2 + g4) * 16), bp, o[db]);
+    }
+    __syncthreads();
+  }
+  lrun += __shfl_xor(lrun, 16, 64);
+  lrun += __shfl_xor(lrun, 32, 64);
+  if (tq < Tx) {
+    const float inv = lrun > 0.f ? 1.f / lrun : 0.f;
+    bf16* dst = out + ((size_t)b * Tx + tq) * W + h * DK + 4 * g4;
+#pragma unroll
+    for (int db = 0; db < 6; ++db) {
+      const uint32_t w0 = (uint32_t)__builtin_bit_cast(uint16_t, (bf16)(o[db][0] * inv)) |
+                          ((uint32_t)__builtin_bit_cast(uint16_t, (bf16)(o[db][1] * inv)) << 16);
+      const uint32_t w1 = (uint32_t)__builtin_bit_cast(uint16_t, (bf16)(o[db][2] * inv)) |
+                          ((uint32_t)__builtin_bit_cast(uint16_t, (bf16)(o[db][3] * inv)) << 16);
+      *reinterpret_cast<uint2*>(dst + 16 * db) = make_uint2(w0, w1);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Multi-head self-attention core (MultiHeadAttention.attention, model.py:343-364) on RoPE'd qkv.
 // Workgroup = 64 queries x 4 lanes of one (utterance, head); lane p of a query owns dk/4 dims of q and
 // of its output. Keys stream through LDS 64 at a time; scores = q.k / sqrt(dk), masked (query, key)
@@ -458,7 +596,10 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
       MT_CHECK_HIP(hipGetLastError());
     }
     const dim3 ga((Tx + 63) / 64, heads, B);
-    if (dk == 96)
+    if (std::is_same<E, bf16>::value && dk == 96 && mfma_attn)
+      hipLaunchKernelGGL(enc_attn_mfma96_kernel, ga, dim3(256), 0, st, (const bf16*)Q, xmask, sdiv, Tx, heads,
+                         (bf16*)A);
+    else if (dk == 96)
       hipLaunchKernelGGL((enc_attn_kernel<E, 96>), ga, dim3(256), 0, st, (const E*)Q, xmask, sdiv, Tx, heads, (E*)A);
     else if (dk == 128)
       hipLaunchKernelGGL((enc_attn_kernel<E, 128>), ga, dim3(256), 0, st, (const E*)Q, xmask, sdiv, Tx, heads, (E*)A);

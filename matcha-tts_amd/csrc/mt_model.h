@@ -168,6 +168,7 @@ struct Decoder {
 struct Encoder {
   int n_vocab = 0, C = 192, F = 768, heads = 2, layers = 6, k = 3, n_spks = 1, spk_dim = 0, W = 192;
   int DF = 256, dpk = 3, prenet = 1, dtype = F32, esize = 4, dk = 96;
+  int mfma_attn = 1;  // bf16, dk = 96: the attention core on MFMA (enc_attn_mfma96_kernel); 0: the fp32-VALU kernel
   ParamList params;
   size_t packed_bytes = 0;
   int emb = -1;

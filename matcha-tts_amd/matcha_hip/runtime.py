@@ -167,6 +167,10 @@ class EncoderEngine:
         except Exception:
             pass
 
+    def set_mfma_attention(self, enable) -> None:
+        """bf16, 96-dim heads: attention core on MFMA (1, default) or on the fp32-VALU kernel (0)."""
+        check(lib().mt_encoder_set_mfma_attention(self.h, int(bool(enable))), "encoder_set_mfma_attention")
+
     def pack(self, params: Dict[str, torch.Tensor], device: torch.device) -> torch.Tensor:
         """params: TextEncoder-relative reference keys -> tensors."""
         tensors = []

@@ -70,6 +70,36 @@ def test_text_encoder_bf16_close():
     assert rel_rms(logw.cpu(), logw_o) < 2e-2
 
 
+@pytest.mark.parametrize("lengths", [[80, 41, 7], [250, 193, 64, 1], [130, 129, 65]])
+def test_text_encoder_bf16_mfma_attention(lengths):
+    """bf16, 96-dim heads: the attention core on MFMA (enc_attn_mfma96_kernel: S^T = K.Q^T, online softmax,
+    O^T = V^T.P^T with bf16 probabilities) against the fp32-VALU kernel (rel-RMS 1e-2) and the fp32 oracle
+    (2e-2), over key tiles that are partly / wholly padding and query tiles past Tx."""
+    m, sd = _model(1, "bf16", 29)
+    x, xl = _inputs(lengths, 5)
+    eng = m.encoder.engine()
+    sub = {k[len("encoder."):]: v for k, v in sd.items() if k.startswith("encoder.")}
+    mu_o, logw_o, _ = O.text_encoder(sub, x, xl, dict(HP, n_spks=1))
+    try:
+        eng.set_mfma_attention(0)
+        mu_v, logw_v, _ = m.encoder(x.to(DEV), xl.to(DEV))
+        eng.set_mfma_attention(1)
+        mu_m, logw_m, xm = m.encoder(x.to(DEV), xl.to(DEV))
+    finally:
+        eng.set_mfma_attention(1)
+    mu_m, mu_v, logw_m, logw_v = mu_m.cpu(), mu_v.cpu(), logw_m.cpu(), logw_v.cpu()
+    assert torch.isfinite(mu_m).all() and torch.isfinite(logw_m).all()
+    assert not torch.equal(mu_m, mu_v)  # the MFMA kernel ran
+    e_m = (rel_rms(mu_m, mu_o), rel_rms(logw_m, logw_o))
+    e_v = (rel_rms(mu_v, mu_o), rel_rms(logw_v, logw_o))
+    print(f"mfma vs valu {rel_rms(mu_m, mu_v):.3e} / {rel_rms(logw_m, logw_v):.3e}; vs oracle: mfma "
+          f"{e_m[0]:.3e} / {e_m[1]:.3e}, valu {e_v[0]:.3e} / {e_v[1]:.3e}")
+    assert e_m[0] < 2e-2 and e_m[1] < 2e-2  # the bf16 encoder bar (test_text_encoder_bf16_close)
+    # no worse than the VALU kernel beyond bf16 noise (the duration head amplifies rounding in logw)
+    assert e_m[0] < 1.5 * e_v[0] + 2e-3 and e_m[1] < 1.5 * e_v[1] + 2e-3
+    assert torch.equal(mu_m * xm.cpu(), mu_m)  # padded frames stay zero
+
+
 def test_text_encoder_forced_duration_head_exact():
     """With the bench's forced duration head (proj weight 0, bias ln 2.5) logw is exactly
     ln(2.5) * x_mask in every precision, so the index path downstream is exact."""
