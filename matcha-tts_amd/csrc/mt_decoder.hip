@@ -461,10 +461,16 @@ int Decoder::time_embed(const char* P, const Work& w, const TimeSched& ts, int S
   if ((rc = rowdot(w.h1, TE, (const float*)(P + t2w_off), (const float*)(P + t2b_off), w.h2, TE, 0, S, TE, TE,
                    0, 2, st)))
     return rc;
-  for (int r = 0; r < n_res; ++r) {
-    if ((rc = rowdot(w.h2, TE, (const float*)(P + res[r].mlp_w_off), (const float*)(P + res[r].mlp_b_off),
-                     w.tb, n_res * C, r * C, S, C, TE, 0, 0, st)))
-      return rc;
+  // every ResnetBlock's time projection (model.py mlp: Linear(TE, C) on mish(h2)) in one launch per 8 blocks
+  for (int r0 = 0; r0 < n_res; r0 += ROWDOT_MAXSEG) {
+    RowdotSegs sg{};
+    sg.n = std::min(ROWDOT_MAXSEG, n_res - r0);
+    for (int j = 0; j < sg.n; ++j) {
+      sg.W[j] = (const float*)(P + res[r0 + j].mlp_w_off);
+      sg.b[j] = (const float*)(P + res[r0 + j].mlp_b_off);
+      sg.yoff[j] = (r0 + j) * C;
+    }
+    if ((rc = rowdot_segs(w.h2, TE, sg, w.tb, n_res * C, S, C, TE, 0, 0, st))) return rc;
   }
   return 0;
 }

@@ -38,6 +38,16 @@ int sinus_embed(const TimeSched& ts, int S, const float* freq, int half, float* 
                 const float* t_dev = nullptr);
 int rowdot(const float* x, int ldx, const float* W, const float* bias, float* y, int ldy, int yoff, int S,
            int O, int I, int pre, int post, hipStream_t st);
+// n segments of O outputs each, segment j: y[s][yoff[j] + o] = post(b[j][o] + W[j][o] . pre(x[s])), one launch
+constexpr int ROWDOT_MAXSEG = 8;
+struct RowdotSegs {
+  const float* W[ROWDOT_MAXSEG];
+  const float* b[ROWDOT_MAXSEG];
+  int yoff[ROWDOT_MAXSEG];
+  int n;
+};
+int rowdot_segs(const float* x, int ldx, const RowdotSegs& sg, float* y, int ldy, int S, int O, int I, int pre,
+                int post, hipStream_t st);
 
 int durations(const float* logw, const float* xmask, float ls, int B, int Tx, float* w_ceil, float* cum,
               long long* ylen, hipStream_t st);

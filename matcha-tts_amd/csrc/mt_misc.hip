@@ -316,9 +316,78 @@ __global__ __launch_bounds__(256) void rowdot_kernel(const float* __restrict__ x
   }
 }
 
+// The same product with one output per wave and 16-byte weight / row loads (I % 4 == 0): O / 4 workgroups per
+// segment, several weight matrices of one shape in one launch. Per (s, o) the sum order is fixed: lane-strided
+// float4 partial dot products, then the wave reduction.
+__global__ __launch_bounds__(256) void rowdot4_kernel(const float* __restrict__ x, int ldx, RowdotSegs sg,
+                                                      float* __restrict__ y, int ldy, int S, int O, int I, int pre,
+                                                      int post) {
+  __shared__ f32x4 xs[RD_S][RD_IMAX / 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bps = (O + 3) / 4, seg = blockIdx.x / bps;
+  const int o = (blockIdx.x - seg * bps) * 4 + wave, I4 = I / 4;
+  const f32x4* W4 = reinterpret_cast<const f32x4*>(sg.W[seg]);
+  constexpr int KW = RD_IMAX / 256;
+  f32x4 wv[KW];
+#pragma unroll
+  for (int k = 0; k < KW; ++k) {
+    const int i4 = lane + 64 * k;
+    wv[k] = (o < O && i4 < I4) ? W4[(size_t)o * I4 + i4] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int s0 = 0; s0 < S; s0 += RD_S) {
+    const int ns = min(RD_S, S - s0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < ns * I4; e += 256) {
+      const int r = e / I4, i4 = e - r * I4;
+      f32x4 xv = *reinterpret_cast<const f32x4*>(x + (size_t)(s0 + r) * ldx + 4 * i4);
+      if (pre == 1)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) xv[c] = xv[c] * tanhf(log1pf(expf(xv[c])));
+      xs[r][i4] = xv;
+    }
+    __syncthreads();
+    for (int r = 0; r < ns; ++r) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < KW; ++k)
+        if (lane + 64 * k < I4) {
+          const f32x4 xv = xs[r][lane + 64 * k];
+          acc += wv[k][0] * xv[0] + wv[k][1] * xv[1] + wv[k][2] * xv[2] + wv[k][3] * xv[3];
+        }
+      acc = wave_sum(acc);
+      if (lane == 0 && o < O) {
+        float v = acc + (sg.b[seg] ? sg.b[seg][o] : 0.f);
+        if (post == 1) v = v / (1.f + expf(-v));
+        if (post == 2) v = v * tanhf(log1pf(expf(v)));
+        y[(size_t)(s0 + r) * ldy + sg.yoff[seg] + o] = v;
+      }
+    }
+  }
+}
+
+int rowdot_segs(const float* x, int ldx, const RowdotSegs& sg, float* y, int ldy, int S, int O, int I, int pre,
+                int post, hipStream_t st) {
+  MT_REQUIRE(I > 0 && I <= RD_IMAX && I % 4 == 0 && ldx % 4 == 0 && S > 0 && O > 0 && sg.n >= 1 &&
+                 sg.n <= ROWDOT_MAXSEG,
+             "rowdot_segs: I %d (max %d, multiple of 4), ldx %d, S %d, O %d, %d segments", I, RD_IMAX, ldx, S, O,
+             sg.n);
+  hipLaunchKernelGGL(rowdot4_kernel, dim3(sg.n * ((O + 3) / 4)), dim3(256), 0, st, x, ldx, sg, y, ldy, S, O, I, pre,
+                     post);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 int rowdot(const float* x, int ldx, const float* W, const float* bias, float* y, int ldy, int yoff,
            int S, int O, int I, int pre, int post, hipStream_t st) {
   MT_REQUIRE(I > 0 && I <= RD_IMAX && S > 0 && O > 0, "rowdot: I %d (max %d), S %d, O %d", I, RD_IMAX, S, O);
+  if (I % 4 == 0 && ldx % 4 == 0) {
+    RowdotSegs sg{};
+    sg.W[0] = W;
+    sg.b[0] = bias;
+    sg.yoff[0] = yoff;
+    sg.n = 1;
+    return rowdot_segs(x, ldx, sg, y, ldy, S, O, I, pre, post, st);
+  }
   const int per = 4 * RD_NO;
   hipLaunchKernelGGL(rowdot_kernel, dim3((O + per - 1) / per), dim3(256), 0, st, x, ldx, W, bias, y, ldy, yoff,
                      S, O, I, pre, post);
