@@ -160,6 +160,27 @@ def _latest_profile(name):
     return files[-1] if files else None
 
 
+def roofline_by_kernel(detail):
+    """The family's launches split by kernel (mt_vconv: stages 1-2 per layer; mt_vpair / mt_vpair32: stage 3 / 4
+    pairs, priced as their two convs): mean launch ms, algorithmic rate on both sides and the fraction of the
+    side the kernel's own intensity bounds it by."""
+    out = {}
+    for kind in ("vconv", "vpair", "vpair32", "rbfuse"):
+        ls = [d for d in detail if d["kind"] == kind]
+        if not ls:
+            continue
+        ms = sum(d["ms"] for d in ls)
+        fl = sum(d["flops"] for d in ls)
+        by = sum(d["bytes"] for d in ls)
+        tf, gbs = fl / (ms * 1e-3) / 1e12, by / (ms * 1e-3) / 1e9
+        mfma = fl / by >= PEAK_FLOPS / PEAK_BW
+        out[kind] = {"launches": len(ls), "launch_ms": round(ms / len(ls), 4), "tflops": round(tf, 1),
+                     "gbs": round(gbs, 1), "intensity_flop_per_byte": round(fl / by, 1),
+                     "bound": "mfma" if mfma else "hbm",
+                     "frac": round(tf / (PEAK_FLOPS / 1e12) if mfma else gbs / (PEAK_BW / 1e9), 4)}
+    return out
+
+
 def roofline(probe, default_workload=True):
     """Dominant kernel family of the step: the LDS-DMA persistent implicit-GEMM convs that run every ResBlock
     conv of HiFi-GAN (54 launches per step): stages 1-2 per layer on mt_vconv (2 stages x 3 resblocks x 3 pairs
@@ -344,6 +365,7 @@ def main():
         step(m, g, den, x, xl, a.n_timesteps, denoise, spk)
     barrier()
     el = time.perf_counter() - t0
+    detail = rt.probe_detail()
     probe = rt.probe_stop()
 
     el, tot_frames = reduce_over_ranks(el, frames, dist, device)
@@ -370,6 +392,7 @@ def main():
             default = (a.batch, a.n_timesteps, a.seed, a.no_denoise, a.precision, a.model) == \
                 (32, 10, 1234, False, "bf16", "lj")
             out["roofline"] = roofline(probe, default_workload=default)
+            out["roofline"]["by_kernel"] = roofline_by_kernel(detail)
             out["path_roofline"] = path_roofline(el / a.steps, yls, t_pad, a.n_timesteps)
             if not a.no_north_star and a.batch != 256 and a.precision == "bf16" and not vctk:
                 out["north_star"] = north_star(m, g, den, 256, a.seed, a.n_timesteps, denoise)

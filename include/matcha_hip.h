@@ -339,6 +339,9 @@ int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, in
 #define MT_PROBE_VCONV_DEC 4
 int mt_probe_start(int site, int max_launches);
 int mt_probe_pause(int paused);
+/* per recorded launch: duration (ms), algorithmic FLOPs and bytes, kernel tag (0 mt_vconv, 1 mt_vpair,
+ * 2 mt_vpair32, 3 mt_rbfuse); synchronizes the events; call before mt_probe_stop. Returns the count written. */
+int mt_probe_detail(int cap, double* ms, double* flops, double* bytes, int* tags);
 int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes, double peak_flops, double peak_bw,
                   double* roof_ms);
 

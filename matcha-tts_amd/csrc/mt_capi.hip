@@ -378,6 +378,9 @@ int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, in
 
 int mt_probe_start(int site, int max_launches) { return mt::probe_start(site, max_launches); }
 int mt_probe_pause(int paused) { return mt::probe_pause(paused != 0); }
+int mt_probe_detail(int cap, double* ms, double* flops, double* bytes, int* tags) {
+  return mt::probe_detail(cap, ms, flops, bytes, tags);
+}
 
 int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes, double peak_flops, double peak_bw,
                   double* roof_ms) {

@@ -12,6 +12,7 @@ std::vector<hipEvent_t> g_ev;  // 2 per launch: begin, end
 int g_n = 0, g_cap = 0;
 double g_flops = 0, g_bytes = 0;
 std::vector<double> g_lf, g_lb;  // per launch: algorithmic FLOPs, bytes
+std::vector<int> g_lt;           // per launch: kernel tag
 bool g_open = false;
 bool g_paused = false;
 
@@ -22,6 +23,7 @@ void release() {
   g_flops = g_bytes = 0;
   g_lf.clear();
   g_lb.clear();
+  g_lt.clear();
   g_site = PROBE_NONE;
   g_open = false;
   g_paused = false;
@@ -39,7 +41,7 @@ void probe_begin(int site, hipStream_t st) {
   g_open = true;
 }
 
-void probe_end(int site, hipStream_t st, double flops, double bytes) {
+void probe_end(int site, hipStream_t st, double flops, double bytes, int tag) {
   if (!probe_armed(site)) return;
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_open) return;
@@ -50,6 +52,25 @@ void probe_end(int site, hipStream_t st, double flops, double bytes) {
   g_bytes += bytes;
   g_lf.push_back(flops);
   g_lb.push_back(bytes);
+  g_lt.push_back(tag);
+}
+
+int probe_detail(int cap, double* ms, double* flops, double* bytes, int* tags) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int n = std::min(cap, g_n);
+  for (int i = 0; i < n; ++i) {
+    float t = 0.f;
+    if (hipEventSynchronize(g_ev[2 * i + 1]) != hipSuccess ||
+        hipEventElapsedTime(&t, g_ev[2 * i], g_ev[2 * i + 1]) != hipSuccess) {
+      set_error("probe: event timing failed");
+      return -1;
+    }
+    if (ms) ms[i] = t;
+    if (flops) flops[i] = g_lf[i];
+    if (bytes) bytes[i] = g_lb[i];
+    if (tags) tags[i] = g_lt[i];
+  }
+  return n;
 }
 
 int probe_start(int site, int max_launches) {

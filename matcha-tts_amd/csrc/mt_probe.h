@@ -17,7 +17,12 @@ enum ProbeSite {
 bool probe_armed(int site);
 bool probe_any_armed();  // some site armed (its launches need per-launch host bookkeeping)
 void probe_begin(int site, hipStream_t st);
-void probe_end(int site, hipStream_t st, double flops, double bytes);
+// tag: the launching kernel's kind (PROBE_TAG_*), reported per launch by probe_detail
+enum ProbeTag { PROBE_TAG_VCONV = 0, PROBE_TAG_VPAIR = 1, PROBE_TAG_VPAIR32 = 2, PROBE_TAG_RBFUSE = 3 };
+void probe_end(int site, hipStream_t st, double flops, double bytes, int tag = PROBE_TAG_VCONV);
+// per-launch duration (ms), algorithmic FLOPs / bytes and tag of the recorded launches (synchronizes their
+// events; call before probe_stop) -> launches written (<= cap)
+int probe_detail(int cap, double* ms, double* flops, double* bytes, int* tags);
 int probe_start(int site, int max_launches);
 int probe_pause(bool paused);
 // roof_ms: sum over launches of max(flops / peak_flops, bytes / peak_bw) in ms (the roofline time)

@@ -405,7 +405,7 @@ int launch_rbfuse(int dtype, int C, const RBArgs& a, hipStream_t st) {
     return -1;
   }
   MT_CHECK_HIP(hipGetLastError());
-  probe_end(site, st, flops, bytes);
+  probe_end(site, st, flops, bytes, PROBE_TAG_RBFUSE);
   return 0;
 }
 

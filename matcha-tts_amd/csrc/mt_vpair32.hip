@@ -389,7 +389,7 @@ int launch_vpair32(int ef, const VPairArgs& a, hipStream_t st) {
     default: set_error("vpair32: epilogue %d not compiled in", ef); return -1;
   }
   MT_CHECK_HIP(hipGetLastError());
-  probe_end(PROBE_VCONV, st, flops, bytes);
+  probe_end(PROBE_VCONV, st, flops, bytes, PROBE_TAG_VPAIR32);
   const int rec[VCLOG_FIELDS] = {ef | 0x10000, C, BN, 0, (int)ntiles, G, a.taps, C, C, a.B, a.L};
   vclog_record(rec);
   return 0;

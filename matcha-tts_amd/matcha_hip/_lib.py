@@ -86,6 +86,7 @@ SIGNATURES = {
     "mt_op_attention": (c_int, [c_int, P, P, P, c_int, c_int, c_int, P]),
     "mt_probe_start": (c_int, [c_int, c_int]),
     "mt_probe_pause": (c_int, [c_int]),
+    "mt_probe_detail": (c_int, [c_int, P, P, P, P]),
     "mt_probe_stop": (c_int, [P, P, P, P, c_double, c_double, P]),
     "mtt_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_float, P, c_int, c_int64, P, c_int, c_int64, c_float,
                          P, c_int, c_int64, c_int, P, P, P, c_size_t, P]),

@@ -549,6 +549,19 @@ def probe_pause(paused: bool) -> None:
     check(lib().mt_probe_pause(int(bool(paused))), "probe_pause")
 
 
+PROBE_TAGS = ("vconv", "vpair", "vpair32", "rbfuse")
+
+
+def probe_detail(cap: int = 4096) -> List[Dict[str, float]]:
+    """Per recorded launch (before probe_stop): ms, algorithmic flops / bytes and the kernel kind."""
+    from ctypes import c_double
+    ms, fl, by, tg = (c_double * cap)(), (c_double * cap)(), (c_double * cap)(), (c_int * cap)()
+    n = lib().mt_probe_detail(int(cap), ms, fl, by, tg)
+    if n < 0:
+        check(n, "probe_detail")
+    return [{"ms": ms[i], "flops": fl[i], "bytes": by[i], "kind": PROBE_TAGS[tg[i]]} for i in range(n)]
+
+
 def probe_stop(peak_flops: float = 2.5e15, peak_bw: float = 8.0e12) -> Dict[str, float]:
     """Synchronize the probe's events: launches, summed kernel ms, algorithmic FLOPs and layer-boundary
     bytes, and the summed per-launch roofline time max(F / peak_flops, B / peak_bw) in ms (defaults: the

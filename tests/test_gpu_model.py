@@ -401,9 +401,14 @@ def test_launch_probe_times_vconv_launches():
     gen(mel)
     rt.probe_start(rt.PROBE_VCONV, 64)
     gen(mel)
+    detail = rt.probe_detail()
     p = rt.probe_stop()
     B, T = mel.shape[0], mel.shape[2]
     assert p["launches"] == 36 + 18 and p["ms"] > 0
+    kinds = [d["kind"] for d in detail]
+    assert (kinds.count("vconv"), kinds.count("vpair"), kinds.count("vpair32")) == (36, 9, 9), kinds
+    assert abs(sum(d["flops"] for d in detail) - p["flops"]) <= 1e-9 * p["flops"]
+    assert abs(sum(d["ms"] for d in detail) - p["ms"]) <= 1e-3 * p["ms"]
     want = sum(2.0 * 6 * C * C * 21 * B * T * r for C, r in ((256, 8), (128, 64), (64, 128), (32, 256)))
     assert abs(p["flops"] - want) <= 1e-9 * want
 
