@@ -17,6 +17,7 @@
 //     out = sum_{j masked} (1/n_masked) * v_j          (independent of q and k)
 // and for an utterance without padding the ordinary softmax over all keys applies.
 #include "mt_common.h"
+#include "mt_misc.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -319,7 +320,7 @@ size_t attention_part_bytes(int B, int T, int heads) {
 //   then x_j = bf16(x_j + o) for the slice's frames + the (mean, M2) per 64-channel slab of the stored row
 //   (the LayerNorm partials LN3 reads, VE_ROWSTATS format). Rounding as the GEMM path: V averaged in fp32,
 //   o rounded to bf16 (the attention output was stored bf16), x + (W_o o + b_o) in fp32, stored bf16.
-constexpr int UNI_C = 256, UNI_PART = UNI_C + 4;
+constexpr int UNI_C = 256, UNI_PART = UNI_C + 4;  // UNI_PSMAX (mt_misc.h): part slices per utterance
 
 __global__ __launch_bounds__(256) void attn_uni_part_kernel(const bf16* __restrict__ x, const float* __restrict__ mask,
                                                             int T, float* __restrict__ part) {
@@ -374,17 +375,28 @@ __global__ __launch_bounds__(256) void attn_uni_part_kernel(const bf16* __restri
   }
 }
 
-__global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ x, int T, const float* __restrict__ part,
+__global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ x, int T, int SP, const float* __restrict__ part,
                                                              const bf16* __restrict__ wqkv, int mq, const float* __restrict__ bqkv,
                                                              const bf16* __restrict__ wout, const float* __restrict__ bout,
                                                              float* __restrict__ row_out) {
   __shared__ float zb[UNI_C], vb[128], ob[UNI_C];
   const int S = gridDim.x, s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  {  // merge the utterance's slices in order
+  {  // merge the utterance's SP part slices in order (loads issued 8 slices at a time)
     float z = 0.f, n = 0.f;
-    for (int k = 0; k < S; ++k) {
-      z += part[((size_t)b * S + k) * UNI_PART + tid];
-      n += part[((size_t)b * S + k) * UNI_PART + UNI_C];
+    for (int k0 = 0; k0 < SP; k0 += 8) {
+      float zz[8], nn[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const size_t o = ((size_t)b * SP + min(k0 + i, SP - 1)) * UNI_PART;
+        zz[i] = part[o + tid];
+        nn[i] = part[o + UNI_C];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (k0 + i < SP) {
+          z += zz[i];
+          n += nn[i];
+        }
     }
     zb[tid] = z / n;
   }
@@ -475,14 +487,16 @@ __global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ 
 }
 
 int uniform_attention_slices(int T) { return std::max(1, std::min(8, T / 64)); }
+// the masked-sum pass streams x once: finer slices (up to 32 per utterance) for more workgroups in flight
+int uniform_part_slices(int T) { return std::max(1, std::min(UNI_PSMAX, T / 24)); }
 
 int launch_uniform_attention(void* x, const float* mask, int B, int T, const void* wqkv, int mq, const float* bqkv,
                              const void* wout, const float* bout, float* part, float* row_out, hipStream_t st) {
   MT_REQUIRE(x && mask && wqkv && bqkv && wout && bout && part && row_out && B > 0 && T > 0 && mq == 384,
              "uniform attention: arguments (C = 256, 2 heads x 64)");
-  const int S = uniform_attention_slices(T);
-  hipLaunchKernelGGL(attn_uni_part_kernel, dim3(S, B), dim3(256), 0, st, (const bf16*)x, mask, T, part);
-  hipLaunchKernelGGL(attn_uni_apply_kernel, dim3(S, B), dim3(256), 0, st, (bf16*)x, T, (const float*)part,
+  const int S = uniform_attention_slices(T), SP = uniform_part_slices(T);
+  hipLaunchKernelGGL(attn_uni_part_kernel, dim3(SP, B), dim3(256), 0, st, (const bf16*)x, mask, T, part);
+  hipLaunchKernelGGL(attn_uni_apply_kernel, dim3(S, B), dim3(256), 0, st, (bf16*)x, T, SP, (const float*)part,
                      (const bf16*)wqkv, mq, bqkv, (const bf16*)wout, bout, row_out);
   MT_CHECK_HIP(hipGetLastError());
   return 0;

@@ -71,6 +71,8 @@ size_t attention_part_bytes(int B, int T, int heads);
 // row_out [B*T][4][2] the per-slab (mean, M2) of the result; wqkv / bqkv the LN-folded QKV vconv image (mq = 384
 // rows) and bias, wout / bout the out-projection image and bias; part: B * uniform_attention_slices(T) * 260 floats
 int uniform_attention_slices(int T);
+constexpr int UNI_PSMAX = 32;  // most masked-sum slices per utterance (the workspace holds B x 32 x 260 floats)
+int uniform_part_slices(int T);
 int launch_uniform_attention(void* x, const float* mask, int B, int T, const void* wqkv, int mq, const float* bqkv,
                              const void* wout, const float* bout, float* part, float* row_out, hipStream_t st);
 

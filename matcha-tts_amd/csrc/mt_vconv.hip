@@ -661,16 +661,17 @@ int vconv_wsum(const void* img, int cin, int taps, int cout, float* wsum, hipStr
   return 0;
 }
 
-// Frames per tile of a k >= 2 conv with 128-row tiles: 256, or 128 when the 256-frame grid leaves CUs idle
-// and the finer grid finishes sooner (the decoder's half-resolution blocks: B = 32, L = 364 gives 128 tiles
-// of 256 frames (40 % of them padding) but 192 tiles of 128). A 128-frame tile carries the same per-step
-// barrier and staging overhead for half the MFMAs, priced as 1.25x its frames.
+// Frames per tile of the decoder's k >= 2 GroupNorm-stat / masked convs (128-row tiles): 256, or 192 / 128 when
+// the 256-frame grid leaves CUs idle and a finer grid finishes sooner (B = 32: L = 728 gives 192 tiles of 256
+// frames but exactly 256 of 192; L = 364 gives 128 tiles of 256 but 192 of 128). A smaller tile carries the same
+// per-step barrier and staging overhead for fewer MFMAs: priced as 1.125x (192) / 1.25x (128) its frames.
 static int vconv_tile_frames(int B, int L, int Mpad, int ef) {
-  if (Mpad % 128 != 0 || (ef & ~(VE_GNSTATS | VE_MASK)) != 0) return BN;
+  if (Mpad % 128 != 0 || (ef != VE_GNSTATS && ef != VE_MASK)) return BN;
   const long cu = cu_count(), ntm = Mpad / 128;
-  const long t256 = (long)B * ((L + 255) / 256) * ntm, t128 = (long)B * ((L + 127) / 128) * ntm;
-  const long c256 = (t256 + cu - 1) / cu * 256 * 4, c128 = (t128 + cu - 1) / cu * 128 * 5;
-  return c128 < c256 ? 128 : BN;
+  auto cost = [&](long f, long w) { return ((long)B * ((L + f - 1) / f) * ntm + cu - 1) / cu * f * w; };
+  const long c256 = cost(256, 8), c192 = cost(192, 9), c128 = cost(128, 10);
+  if (c128 < c256 && c128 <= c192) return 128;
+  return c192 < c256 ? 192 : BN;
 }
 
 int vconv_gn_parts(int B, int L, int M) {
@@ -739,14 +740,13 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   constexpr int BN64 = 384;
   if (!k1 && BM == 64) ntiles = (long)a.B * ((a.Lout + BN64 - 1) / BN64) * (a.Mpad / BM);
   MT_REQUIRE(!(ef & VE_GNSTATS) || BM == 128, "vconv: GroupNorm partials need 128-row tiles");
-  const bool half = !k1 && !placed && vconv_tile_frames(a.B, a.L, a.Mpad, ef) == 128;
-  if (half) ntiles = (long)a.B * ((a.L + 127) / 128) * (a.Mpad / BM);
+  const int tf = (!k1 && !placed) ? vconv_tile_frames(a.B, a.L, a.Mpad, ef) : BN;  // 256, 192 or 128
+  if (tf != BN) ntiles = (long)a.B * ((a.L + tf - 1) / tf) * (a.Mpad / BM);
   const int G = (int)std::min<long>(ntiles, cu_count());
-  MT_REQUIRE(!(ef & VE_GNSTATS) || a0.gn_parts == 0 ||
-                 a0.gn_parts == ((a.L + (half ? 128 : BN) - 1) / (half ? 128 : BN)) * (8 / (BM / 64)),
+  MT_REQUIRE(!(ef & VE_GNSTATS) || a0.gn_parts == 0 || a0.gn_parts == ((a.L + tf - 1) / tf) * (8 / (BM / 64)),
              "vconv: caller expects %d GroupNorm partial slots, the launch writes a different count", a0.gn_parts);
   {
-    const int bn = k1 ? (small ? 128 : BN) : (BM == 64 ? 384 : half ? 128 : BN);
+    const int bn = k1 ? (small ? 128 : BN) : (BM == 64 ? 384 : tf);
     const int rec[VCLOG_FIELDS] = {ef, BM, bn, (int)k1, (int)ntiles, G, a.taps, a.M, a.cin, a.B, a.L};
     vclog_record(rec);
   }
@@ -766,7 +766,8 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
     break;
 #define MT_VCASE_H(E)                                                                                  \
   case E:                                                                                              \
-    if (half) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 128>), dim3(G), dim3(NT), 0, st, a);     \
+    if (tf == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 128>), dim3(G), dim3(NT), 0, st, a); \
+    else if (tf == 192) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 192>), dim3(G), dim3(NT), 0, st, a); \
     else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false>), dim3(G), dim3(NT), 0, st, a); \
     else hipLaunchKernelGGL((vconv_kernel<E, 64, false, BN64>), dim3(G), dim3(NT), 0, st, a);          \
     break;
