@@ -91,19 +91,32 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
   if constexpr (NEED_GN) {
     const int C = (PF & PF_GN) ? a.cin : a.cout;
     const int G = C >> 5;
-    if (tid < G) {
-      const double* p = a.gn_in + (size_t)(b * G + tid) * a.gn_ntiles * 2;
+    if (tid < 64) {
+      // first wave: a power-of-two segment of lanes per group, each summing a strided subset of the group's
+      // partials (all loads in flight together), then a butterfly inside the segment (fixed order)
+      int lpg = 64;
+      while (lpg * G > 64) lpg >>= 1;
+      const int g = tid / lpg, sub = tid % lpg;
       double s1 = 0.0, s2 = 0.0;
-      for (int i = 0; i < a.gn_ntiles; ++i) {
-        s1 += p[2 * i];
-        s2 += p[2 * i + 1];
+      if (g < G) {
+        const double* p = a.gn_in + (size_t)(b * G + g) * a.gn_ntiles * 2;
+        for (int i = sub; i < a.gn_ntiles; i += lpg) {
+          s1 += p[2 * i];
+          s2 += p[2 * i + 1];
+        }
       }
-      const double n = 32.0 * (double)a.gn_T;
-      const double mean = s1 / n;
-      double var = s2 / n - mean * mean;
-      var = var < 0.0 ? 0.0 : var;
-      lnm[tid] = (float)mean;
-      lnr[tid] = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+      for (int o = lpg >> 1; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      if (sub == 0 && g < G) {
+        const double n = 32.0 * (double)a.gn_T;
+        const double mean = s1 / n;
+        double var = s2 / n - mean * mean;
+        var = var < 0.0 ? 0.0 : var;
+        lnm[g] = (float)mean;
+        lnr[g] = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+      }
     }
     __syncthreads();
     for (int c = tid; c < C; c += NT) {
