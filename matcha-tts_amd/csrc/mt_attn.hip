@@ -375,29 +375,28 @@ __global__ __launch_bounds__(256) void attn_uni_part_kernel(const bf16* __restri
   }
 }
 
-__global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ x, int T, int SP, const float* __restrict__ part,
-                                                             const bf16* __restrict__ wqkv, int mq, const float* __restrict__ bqkv,
-                                                             const bf16* __restrict__ wout, const float* __restrict__ bout,
-                                                             float* __restrict__ row_out) {
-  __shared__ float zb[UNI_C], vb[128], ob[UNI_C];
-  const int S = gridDim.x, s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  {  // merge the utterance's SP part slices in order (loads issued 8 slices at a time)
-    float z = 0.f, n = 0.f;
-    for (int k0 = 0; k0 < SP; k0 += 8) {
-      float zz[8], nn[8];
+// the utterance's attention output vector o_b (grid B): merge of the SP masked-sum slices, then the two GEMVs
+__global__ __launch_bounds__(256) void attn_uni_vec_kernel(int SP, const float* __restrict__ part,
+                                                           const bf16* __restrict__ wqkv, int mq, const float* __restrict__ bqkv,
+                                                           const bf16* __restrict__ wout, const float* __restrict__ bout,
+                                                           float* __restrict__ ovec) {
+  __shared__ float zb[UNI_C], vb[128];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  {  // merge the utterance's SP part slices in order (all loads in flight at once)
+    float zz[UNI_PSMAX], nn[UNI_PSMAX];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const size_t o = ((size_t)b * SP + min(k0 + i, SP - 1)) * UNI_PART;
-        zz[i] = part[o + tid];
-        nn[i] = part[o + UNI_C];
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (k0 + i < SP) {
-          z += zz[i];
-          n += nn[i];
-        }
+    for (int k = 0; k < UNI_PSMAX; ++k) {
+      const size_t o = ((size_t)b * SP + min(k, SP - 1)) * UNI_PART;
+      zz[k] = part[o + tid];
+      nn[k] = part[o + UNI_C];
     }
+    float z = 0.f, n = 0.f;
+#pragma unroll
+    for (int k = 0; k < UNI_PSMAX; ++k)
+      if (k < SP) {
+        z += zz[k];
+        n += nn[k];
+      }
     zb[tid] = z / n;
   }
   __syncthreads();
@@ -442,9 +441,17 @@ __global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ 
       for (int i = 0; i < 4; ++i) o += dot8(w[i], vb + ck * 64 + k0 + 8 * i);
       o += __shfl_xor(o, 1, 64);
       o += __shfl_xor(o, 2, 64);
-      if (q4 == 0) ob[r] = o + bout[r];
+      if (q4 == 0) ovec[(size_t)b * UNI_C + r] = o + bout[r];
     }
   }
+}
+
+// x += o_b on every frame of the slice, + the next LayerNorm's per-slab (mean, M2) (grid slices x B)
+__global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ x, int T, const float* __restrict__ ovec,
+                                                             float* __restrict__ row_out) {
+  __shared__ float ob[UNI_C];
+  const int S = gridDim.x, s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  ob[tid] = ovec[(size_t)b * UNI_C + tid];
   __syncthreads();
   const int fr = tid >> 5, cl = tid & 31, c = cl * 8;
   const int f0 = (int)((long)s * T / S), f1 = (int)((long)(s + 1) * T / S);
@@ -486,18 +493,20 @@ __global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ 
   }
 }
 
-int uniform_attention_slices(int T) { return std::max(1, std::min(8, T / 64)); }
 // the masked-sum pass streams x once: finer slices (up to 32 per utterance) for more workgroups in flight
 int uniform_part_slices(int T) { return std::max(1, std::min(UNI_PSMAX, T / 24)); }
+size_t uniform_attention_floats(int B) { return (size_t)B * (UNI_PSMAX * UNI_PART + UNI_C); }
 
 int launch_uniform_attention(void* x, const float* mask, int B, int T, const void* wqkv, int mq, const float* bqkv,
                              const void* wout, const float* bout, float* part, float* row_out, hipStream_t st) {
   MT_REQUIRE(x && mask && wqkv && bqkv && wout && bout && part && row_out && B > 0 && T > 0 && mq == 384,
              "uniform attention: arguments (C = 256, 2 heads x 64)");
-  const int S = uniform_attention_slices(T), SP = uniform_part_slices(T);
+  const int SP = uniform_part_slices(T);
+  float* ovec = part + (size_t)B * UNI_PSMAX * UNI_PART;  // [B][256] after the slice sums (uniform_attention_floats)
   hipLaunchKernelGGL(attn_uni_part_kernel, dim3(SP, B), dim3(256), 0, st, (const bf16*)x, mask, T, part);
-  hipLaunchKernelGGL(attn_uni_apply_kernel, dim3(S, B), dim3(256), 0, st, (bf16*)x, T, SP, (const float*)part,
-                     (const bf16*)wqkv, mq, bqkv, (const bf16*)wout, bout, row_out);
+  hipLaunchKernelGGL(attn_uni_vec_kernel, dim3(B), dim3(256), 0, st, SP, (const float*)part, (const bf16*)wqkv, mq,
+                     bqkv, (const bf16*)wout, bout, ovec);
+  hipLaunchKernelGGL(attn_uni_apply_kernel, dim3(SP, B), dim3(256), 0, st, (bf16*)x, T, (const float*)ovec, row_out);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -403,7 +403,7 @@ size_t Decoder::workspace_bytes(int B, int T, int S) const {
   n += 4096;                                          // trash (vconv stores past the last frame)
   n += align256(attention_part_bytes(B, T, heads));   // attention key-split slots
   n += align256(BT * (C / 64) * 2 * 4);               // lnp
-  n += align256((size_t)B * UNI_PSMAX * 260 * 4);     // upart
+  n += align256(uniform_attention_floats(B) * 4);     // upart
   n += align256(BT * 4);                              // mst
   return n;
 }
@@ -444,7 +444,7 @@ Decoder::Work Decoder::carve(void* ws, int B, int T, int S) const {
   w.tb_ld = 0;
   w.apart = (float*)take(attention_part_bytes(B, T, heads));
   w.lnp = (float*)take(BT * (C / 64) * 2 * 4);
-  w.upart = (float*)take((size_t)B * UNI_PSMAX * 260 * 4);
+  w.upart = (float*)take(uniform_attention_floats(B) * 4);
   w.mst = (float*)take(BT * 4);
   w.m0 = nullptr;
   return w;

@@ -69,10 +69,12 @@ size_t attention_part_bytes(int B, int T, int heads);
 // query-independent attention + out-projection + residual of utterances that ALL have padded frames at this
 // level (the reference's mask fill, model.py:697; mt_attn.hip): x [B][T][256] bf16 updated in place to x + attn1(x),
 // row_out [B*T][4][2] the per-slab (mean, M2) of the result; wqkv / bqkv the LN-folded QKV vconv image (mq = 384
-// rows) and bias, wout / bout the out-projection image and bias; part: B * uniform_attention_slices(T) * 260 floats
-int uniform_attention_slices(int T);
+// rows) and bias, wout / bout the out-projection image and bias; part: uniform_attention_floats(B) floats.
+// Three launches: masked sums of the normalised rows over uniform_part_slices(T) frame slices per utterance; per
+// utterance the merge and the two GEMVs (o_b); x += o_b with the row statistics over the same slices.
 constexpr int UNI_PSMAX = 32;  // most masked-sum slices per utterance (the workspace holds B x 32 x 260 floats)
 int uniform_part_slices(int T);
+size_t uniform_attention_floats(int B);  // workspace of launch_uniform_attention's `part`: slice sums + o_b
 int launch_uniform_attention(void* x, const float* mask, int B, int T, const void* wqkv, int mq, const float* bqkv,
                              const void* wout, const float* bout, float* part, float* row_out, hipStream_t st);
 
