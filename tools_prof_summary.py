@@ -41,7 +41,7 @@ for r in step:
         cur = 'denorm'
     elif cur == 'denorm' and 'bct_to_btc' in k:
         cur = 'vocoder'
-    elif 'stft_denoise_kernel' in k:
+    elif 'stft_denoise' in k:
         cur = 'denoiser'
     c = comp[cur]
     c[0] += dur(r)
