@@ -159,9 +159,10 @@ int mt_vocoder_set_fusion(mt_vocoder* v, int enable);
  * faster): also the 64-channel stage instead of the fused kernel; 0: the generic per-layer kernel. Replaces the same
  * convs as mt_vocoder_forward (hifigan/models.py:90-97, 187-192). */
 int mt_vocoder_set_vconv(mt_vocoder* v, int mode);
-/* bf16, vconv mode 2: the 64-channel stage's ResBlock pairs (conv_{k,d} -> lrelu -> conv_{k,1} -> + x,
- * hifigan/models.py:90-97) each as ONE launch with the intermediate on chip and the input activation applied
- * on chip (1, default) or as two per-layer launches (0). Same bits either way. */
+/* bf16, vconv mode 2: ResBlock pairs (conv_{k,d} -> lrelu -> conv_{k,1} -> + x, hifigan/models.py:90-97) each as
+ * ONE launch with the intermediate on chip and the input activation applied on chip. 1 (default): the 64- and
+ * 32-channel stages' pairs and the 128-channel stage's k = 3 resblock; 4: every 128-channel pair too; 2: none of
+ * the 128-channel stage; 0: every pair as two per-layer launches. Same bits in every mode. */
 int mt_vocoder_set_pair(mt_vocoder* v, int enable);
 int mt_vocoder_pack(const mt_vocoder* v, const float* const* params, void* packed, void* stream);
 size_t mt_vocoder_workspace_bytes(const mt_vocoder* v, int B, int T);

@@ -219,7 +219,7 @@ int mt_vocoder_set_vconv(mt_vocoder* v, int enable) {
 }
 int mt_vocoder_set_pair(mt_vocoder* v, int enable) {
   MT_REQUIRE(v, "null vocoder");
-  v->v.pair = enable ? 1 : 0;
+  v->v.pair = enable < 0 ? 0 : enable;
   return 0;
 }
 size_t mt_vocoder_packed_bytes(const mt_vocoder* v) { return v ? v->v.packed_bytes : 0; }

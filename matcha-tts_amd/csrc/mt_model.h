@@ -209,7 +209,8 @@ struct Vocoder {
   int resblock = 1, dtype = BF16, esize = 2;
   int fuse = 1;  // fused ResBlock stages (mt_rbfuse) where supported
   int vconv = 2; // LDS-DMA persistent convs (mt_vconv): 1 = C >= 128 stages, 2 = also C = 64 (per layer)
-  // the 64- and 32-channel stages' ResBlock pairs as one launch each (mt_vpair / mt_vpair32; needs vconv >= 2)
+  // the 128-, 64- and 32-channel stages' ResBlock pairs as one launch each (mt_vpair128 / mt_vpair / mt_vpair32;
+  // needs vconv >= 2). The 128-channel stage: 1 = its k = 3 resblock fused, 4 = all fused, 2 = none (per layer)
   int pair = 1;
   size_t zero_off = 0;  // 256 zero bytes in the packed buffer (vconv padding rows)
   bool any_vc = false;
@@ -227,9 +228,12 @@ struct Vocoder {
            const std::vector<int>& rb_kernels, const std::vector<std::vector<int>>& rb_dils, int dtype);
   int pack(const float* const* p, void* packed, hipStream_t st) const;
   bool stage_vc(int i) const;  // stage i runs its ResBlock convs through mt_vconv
-  bool stage_vp(int i) const;  // ... as fused pairs (mt_vpair): its input needs no activated copy
+  bool rb_vp(int i, int j) const;  // resblock j of stage i as fused pairs (mt_vpair128 / mt_vpair)
+  bool stage_vp(int i) const;  // ... every resblock as fused pairs: the stage input needs no activated copy
   bool stage_vp32(int i) const;  // a 32-channel stage as fused pairs (mt_vpair32, generic weight packing)
   // stage i's ResBlocks as one fused-pair launch per pair: X -> XS (+ lrelu(XS) in RA when act_out)
+  int pair_resblock(const char* P, int i, int j, int B, int L, const char* X, char* XS, char* Tb, char* R,
+                    char* RA, char* trash, bool act_out, hipStream_t st) const;
   int pair_chain(const char* P, int i, int B, int L, const char* X, char* XS, char* Tb, char* R, char* RA,
                  char* trash, bool act_out, hipStream_t st) const;
   size_t frame_elems() const;  // max over stages of (samples per mel frame) x channels

@@ -221,16 +221,28 @@ bool Vocoder::stage_vc(int i) const {
   return vconv >= 2 || !(fuse && rbfuse_supported(dtype, C));
 }
 
-bool Vocoder::stage_vp(int i) const {
+// resblock j of wide stage i as one fused-pair launch per pair. C = 128 (mt_vpair128) pays only where the pair is
+// HBM-bound: pair mode 1 (default) fuses its k = 3 resblock, 4 every resblock, 2 none (measured per pair at B = 256:
+// k = 3 3.9 ms fused vs 4.3 per layer, k = 7 / 11 7.0 / 10.3 fused vs 6.9 / 9.4 per layer)
+bool Vocoder::rb_vp(int i, int j) const {
   if (!pair || vconv < 2 || !stage_vc(i)) return false;
   const int nk = (int)rb_kernels.size();
-  for (int j = 0; j < nk; ++j)
-    for (size_t q = 0; q < rb1[(size_t)i * nk + j].size(); ++q) {
-      const GemmW& a = rb1[(size_t)i * nk + j][q];
-      const GemmW& b = rb2[(size_t)i * nk + j][q];
-      if (!vpair_supported(a.cout, a.k, a.dil) || b.k != a.k || b.dil != 1) return false;
-    }
+  for (size_t q = 0; q < rb1[(size_t)i * nk + j].size(); ++q) {
+    const GemmW& a = rb1[(size_t)i * nk + j][q];
+    const GemmW& b = rb2[(size_t)i * nk + j][q];
+    const bool ok = a.cout == 128 ? (pair == 4 || (pair == 1 && a.k == 3)) && a.cin == 128 &&
+                                        vpair128_supported(a.k, a.dil)
+                                  : vpair_supported(a.cout, a.k, a.dil);
+    if (!ok || b.k != a.k || b.dil != 1) return false;
+  }
   return true;
+}
+
+bool Vocoder::stage_vp(int i) const {
+  const int nk = (int)rb_kernels.size();
+  for (int j = 0; j < nk; ++j)
+    if (!rb_vp(i, j)) return false;
+  return nk > 0;
 }
 
 bool Vocoder::stage_vp32(int i) const {
@@ -248,50 +260,59 @@ bool Vocoder::stage_vp32(int i) const {
   return true;
 }
 
-// One launch per pair (mt_vpair / mt_vpair32); the chain state ping-pongs between R and Tb (a pair reads its
-// input's halo, so it cannot write in place); the inputs' activations are applied in LDS.
+// One launch per pair (mt_vpair128 / mt_vpair / mt_vpair32); the chain state ping-pongs between R and Tb (a pair
+// reads its input's halo, so it cannot write in place); the inputs' activations are applied in LDS.
+int Vocoder::pair_resblock(const char* P, int i, int j, int B, int L, const char* X, char* XS, char* Tb, char* R,
+                           char* RA, char* trash, bool act_out, hipStream_t st) const {
+  const int nk = (int)rb_kernels.size();
+  const int C = rb1[(size_t)i * nk][0].cout;
+  const bool c32 = C == 32;
+  int rc;
+  const std::vector<GemmW>& c1 = rb1[(size_t)i * nk + j];
+  const std::vector<GemmW>& c2 = rb2[(size_t)i * nk + j];
+  const int np = (int)c1.size();
+  const char* state = X;
+  for (int q = 0; q < np; ++q) {
+    const bool last = q == np - 1;
+    VPairArgs a{};
+    a.x = (const bf16*)state;
+    a.B = B;
+    a.L = L;
+    a.w1 = (const bf16*)(P + (c32 ? c1[q].w_off : c1[q].v_off));
+    a.b1 = (const float*)(P + c1[q].b_off);
+    a.w2 = (const bf16*)(P + (c32 ? c2[q].w_off : c2[q].v_off));
+    a.b2 = (const float*)(P + c2[q].b_off);
+    a.taps = c1[q].k;
+    a.dil = c1[q].dil;
+    a.div = (float)nk;
+    a.slope = 0.1f;
+    a.zero = (const bf16*)(P + zero_off);
+    a.trash = (bf16*)trash;
+    int ef = 0;
+    if (!last) {
+      a.y = (bf16*)((q & 1) ? Tb : R);
+    } else {
+      a.y = (bf16*)XS;
+      if (j > 0) ef |= VE_ACCUM;
+      if (j == nk - 1) ef |= VE_DIV;
+      if (j == nk - 1 && act_out) {  // lrelu(xs) for the next upsampler
+        a.y2 = (bf16*)RA;
+        ef |= VE_DUAL;
+      }
+    }
+    if ((rc = c32 ? launch_vpair32(ef, a, st) : C == 128 ? launch_vpair128(ef, a, st) : launch_vpair(ef, a, st)))
+      return rc;
+    state = (const char*)a.y;
+  }
+  return 0;
+}
+
 int Vocoder::pair_chain(const char* P, int i, int B, int L, const char* X, char* XS, char* Tb, char* R, char* RA,
                         char* trash, bool act_out, hipStream_t st) const {
   const int nk = (int)rb_kernels.size();
-  const bool c32 = rb1[(size_t)i * nk][0].cout == 32;
   int rc;
-  for (int j = 0; j < nk; ++j) {
-    const std::vector<GemmW>& c1 = rb1[(size_t)i * nk + j];
-    const std::vector<GemmW>& c2 = rb2[(size_t)i * nk + j];
-    const int np = (int)c1.size();
-    const char* state = X;
-    for (int q = 0; q < np; ++q) {
-      const bool last = q == np - 1;
-      VPairArgs a{};
-      a.x = (const bf16*)state;
-      a.B = B;
-      a.L = L;
-      a.w1 = (const bf16*)(P + (c32 ? c1[q].w_off : c1[q].v_off));
-      a.b1 = (const float*)(P + c1[q].b_off);
-      a.w2 = (const bf16*)(P + (c32 ? c2[q].w_off : c2[q].v_off));
-      a.b2 = (const float*)(P + c2[q].b_off);
-      a.taps = c1[q].k;
-      a.dil = c1[q].dil;
-      a.div = (float)nk;
-      a.slope = 0.1f;
-      a.zero = (const bf16*)(P + zero_off);
-      a.trash = (bf16*)trash;
-      int ef = 0;
-      if (!last) {
-        a.y = (bf16*)((q & 1) ? Tb : R);
-      } else {
-        a.y = (bf16*)XS;
-        if (j > 0) ef |= VE_ACCUM;
-        if (j == nk - 1) ef |= VE_DIV;
-        if (j == nk - 1 && act_out) {  // lrelu(xs) for the next upsampler
-          a.y2 = (bf16*)RA;
-          ef |= VE_DUAL;
-        }
-      }
-      if ((rc = c32 ? launch_vpair32(ef, a, st) : launch_vpair(ef, a, st))) return rc;
-      state = (const char*)a.y;
-    }
-  }
+  for (int j = 0; j < nk; ++j)
+    if ((rc = pair_resblock(P, i, j, B, L, X, XS, Tb, R, RA, trash, act_out, st))) return rc;
   return 0;
 }
 
@@ -358,6 +379,10 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
   int rc;
   if (stage_vp(i)) return pair_chain(P, i, B, L, X, XS, Tb, R, RA, trash, act_out, st);
   for (int j = 0; j < nk; ++j) {
+    if (rb_vp(i, j)) {  // this resblock as fused pairs (from the raw X), the others per layer (from XA)
+      if ((rc = pair_resblock(P, i, j, B, L, X, XS, Tb, R, RA, trash, act_out, st))) return rc;
+      continue;
+    }
     const std::vector<GemmW>& c1 = rb1[(size_t)i * nk + j];
     const std::vector<GemmW>& c2 = rb2[(size_t)i * nk + j];
     const int np = (int)c1.size();

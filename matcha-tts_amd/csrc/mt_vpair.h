@@ -1,5 +1,6 @@
-// Fused HiFi-GAN ResBlock1 pair (conv_{k,d} -> lrelu -> conv_{k,1} -> + x) for the 64- and 32-channel stages,
-// bf16: the intermediate stays in LDS and the input's activation is applied on chip (mt_vpair.hip, mt_vpair32.hip).
+// Fused HiFi-GAN ResBlock1 pair (conv_{k,d} -> lrelu -> conv_{k,1} -> + x) for the 128-, 64- and 32-channel
+// stages, bf16: the intermediate stays in LDS and the input's activation is applied on chip (mt_vpair128.hip,
+// mt_vpair.hip, mt_vpair32.hip).
 #pragma once
 #include "mt_vconv.h"
 
@@ -8,7 +9,7 @@ namespace mt {
 struct VPairArgs {
   const bf16* x;        // [B][L][C] pair input (raw chain state; also the residual)
   int B, L;
-  const bf16* w1;       // C = 64: mt_vconv image [1][taps][64][64]; C = 32: generic packing [32][taps][32]
+  const bf16* w1;       // C = 128 / 64: mt_vconv image [C/64][taps][C][64]; C = 32: generic packing [32][taps][32]
   const float* b1;      // [C]
   const bf16* w2;       // image of convs2[q] (dilation 1)
   const float* b2;      // [C]
@@ -26,5 +27,8 @@ int launch_vpair(int ef, const VPairArgs& a, hipStream_t st);
 // the 32-channel kernel (weights in the generic conv packing)
 bool vpair32_supported(int k, int d);
 int launch_vpair32(int ef, const VPairArgs& a, hipStream_t st);
+// the 128-channel kernel (mt_vconv image [2][taps][128][64])
+bool vpair128_supported(int k, int d);
+int launch_vpair128(int ef, const VPairArgs& a, hipStream_t st);
 
 }  // namespace mt

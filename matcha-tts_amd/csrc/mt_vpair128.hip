@@ -1,0 +1,407 @@
+// Fused HiFi-GAN ResBlock1 PAIR for the 128-channel stage (stage 2 of v1), bf16, gfx950 — the 128-channel
+// sibling of mt_vpair.hip:
+//
+//   t = conv_{k, d}(lrelu(x)) ;  y = conv_{k, 1}(lrelu(t)) + x          (hifigan/models.py:90-97)
+//   (the last pair of resblock j: xs = [xs +] y [/ nk], + lrelu(xs) for the next upsampler, models.py:187-192)
+//
+// Per layer (mt_vconv) this pair moves x_act in, t out, t back in, x in, y and y_act out: six 128-channel
+// tensors. Fused it moves x in and y out. The price is LDS: a 128-channel row is 256 bytes, so a tile is only
+// 192 conv1 frames (the intermediate t is 192 x 128 channels), and conv2 keeps BN = 192 - 2 h2 of them
+// (h2 = (k - 1) / 2: 190 / 186 / 182 output frames for k = 3 / 7 / 11).
+//
+// One persistent 512-thread workgroup per CU walks the tiles. Waves: 2 along rows (64 output channels each)
+// x 4 along frames (48 frames = 3 fragments each). Per tile:
+//   1. the RAW input rows (192 conv1 frames + the conv1 halo 2 h1 <= 56 rows) of both 64-channel planes land
+//      in LDS by global_load_lds_dwordx4 (issued during the previous tile's second conv); each lane reads its
+//      residual rows out of them, then one in-place VALU pass turns them into lrelu(rows);
+//   2. conv1: 128 rows x 192 frames over (chunk, tap) steps; epilogue lrelu(round(acc + b1)), zero outside
+//      [0, L) -> T (two 64-channel planes in LDS);
+//   3. conv2: 128 rows x 192 frames over T (frames past BN discarded); epilogue + b2 + x [+ xs, / nk] -> y
+//      (+ lrelu(y)).
+// A step is one (64-channel chunk, tap) pair: a 16 KiB weight slot of the mt_vconv image [2][k][128][64]
+// (3-slot LDS ring, two steps in flight) and 24 MFMAs per wave. Steps run chunk-major, taps ascending, two
+// K = 32 slices each: the per-output MFMA accumulation order of mt_vconv's K loop, and the rounding points of
+// the per-layer path (every stored tensor rounded to bf16, lrelu of the rounded value), so the results are
+// the same bits as the per-layer mt_vconv path.
+// LDS (162,816 B): T planes (2 x 192 rows) | X planes (2 x 248 rows) | weight ring | biases. Rows are 128 B
+// with the 16-byte unit XOR-swizzled by (row & 6) (mt_vconv's conflict-free layout). conv2's discarded last
+// fragments read up to 2 h2 rows past a T plane: into the next plane / the X planes, never outside LDS.
+#include <algorithm>
+
+#include "mt_probe.h"
+#include "mt_vpair.h"
+
+namespace mt {
+
+namespace {
+constexpr int NT = 512, C = 128;
+constexpr int FN = 3;                // 16-frame fragments per wave
+constexpr int WNC = 16 * FN;         // frames per wave (4 waves along frames)
+constexpr int NF1 = 4 * WNC;         // conv1 frames per tile (192)
+constexpr int XROWS = NF1 + 56;      // staged input rows >= NF1 + 2 h1
+constexpr int XPL = XROWS * 128;     // one 64-channel plane of X
+constexpr int TPL = NF1 * 128;       // one 64-channel plane of T
+constexpr int WSLOT = C * 128;       // one step: 128 output rows x 64 input channels (16 KiB)
+constexpr int NWS = 3;
+constexpr int T_OFF = 0, X_OFF = 2 * TPL, W_OFF = X_OFF + 2 * XPL, PAR_OFF = W_OFF + NWS * WSLOT;
+constexpr int LDS_BYTES = PAR_OFF + 2 * C * 4;
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+static_assert(XROWS % 8 == 0, "X staged 8 rows per DMA instruction");
+
+__device__ __forceinline__ void glds16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  if (n < 7) {
+    if (n < 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (n < 4) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else if (n < 15) {
+    if (n < 10) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  } else {
+    if (n < 23) asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+    else if (n < 31) asm volatile("s_waitcnt vmcnt(23)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(31)" ::: "memory");
+  }
+}
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+}  // namespace
+
+template <int EF>
+__global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;  // 64-row half, 48-frame quarter
+  const int g4 = lane >> 4, l16 = lane & 15, lrow = lane >> 3, lp = lane & 7;
+  const int k = a.taps, d = a.dil, L = a.L;
+  const int h1 = d * (k - 1) / 2, h2 = (k - 1) / 2;
+  const int BN = NF1 - 2 * h2;  // output frames per tile
+  const int R1 = NF1 + 2 * h1;  // staged rows per plane
+  const int nxi = (R1 + 7) / 8; // DMA instructions per plane
+  const int ntn = (L + BN - 1) / BN, ntiles = a.B * ntn;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
+  const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
+  if (nmine == 0) return;
+  for (int i = tid; i < C; i += NT) {
+    reinterpret_cast<float*>(smem + PAR_OFF)[i] = a.b1[i];
+    reinterpret_cast<float*>(smem + PAR_OFF)[C + i] = a.b2[i];
+  }
+  __syncthreads();
+
+  int issued = 0, xmk = 0;
+  int wmk[NWS] = {};
+  const int ns = 2 * k;          // steps per conv: (chunk, tap), chunk-major
+  const int S = nmine * 2 * ns;  // weight steps of this workgroup
+  auto tile_of = [&](int ti, int& b, int& n0) {
+    const int tile = gl + ti * G;
+    b = tile / ntn;
+    n0 = (tile - b * ntn) * BN;
+  };
+  auto stage_w = [&](int s) {  // step m of conv1 or conv2: image block (chunk m / k, tap m % k)
+    const int r2 = s % (2 * ns);
+    const int m = r2 < ns ? r2 : r2 - ns;
+    const bf16* w = (r2 < ns ? a.w1 : a.w2) + (size_t)m * C * 64;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = 16 * wave + 8 * u + lrow;
+      glds16(w + r * 64 + (lp ^ (r & 6)) * 8, smem + W_OFF + (s % NWS) * WSLOT + (16 * wave + 8 * u) * 128);
+    }
+    issued += 2;
+    wmk[s % NWS] = issued;
+  };
+  auto stage_x = [&](int ti) {  // raw rows of tile ti, both planes: row r = frame n0 - h2 - h1 + r
+    int b, n0;
+    tile_of(ti, b, n0);
+    const bf16* xb = a.x + (size_t)b * L * C;
+    const int f0 = n0 - h2 - h1;
+    for (int j = wave; j < 2 * nxi; j += 8) {
+      const int p = j & 1, blk = j >> 1;
+      const int r = 8 * blk + lrow;
+      const int q = lp ^ (r & 6);
+      const int f = f0 + r;
+      const bool ok = r < R1 && f >= 0 && f < L;
+      glds16(ok ? xb + (size_t)f * C + p * 64 + q * 8 : a.zero + q * 8, smem + X_OFF + p * XPL + blk * 1024);
+      ++issued;
+    }
+    xmk = issued;
+  };
+
+  auto swap16 = [](uint32_t& x, uint32_t& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+  };
+  auto bf2 = [](uint32_t w, int i) -> float { return __uint_as_float(i ? (w & 0xffff0000u) : (w << 16)); };
+  auto pack2 = [](bf16 lo, bf16 hi) -> uint32_t {
+    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+  };
+  const int ha = l16 & 6;
+
+  f32x4 acc[4][FN];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  struct Frag {
+    bf16x8 A[4], B[FN];
+  };
+  // K-slice ks of a step: A = this wave's 4 row fragments of the slot, B = FN frame fragments at rows
+  // rb + 16 fn of plane `pl`
+  auto read_frag = [&](Frag& F, int ks, int slot, const char* pl, int rb0) {
+    const char* pa = smem + W_OFF + slot * WSLOT + (wm * 64 + l16) * 128 + (((ks * 4 + g4) ^ ha) * 16);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048);
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int rb = rb0 + fn * 16;
+      F.B[fn] = *reinterpret_cast<const bf16x8*>(pl + rb * 128 + (((ks * 4 + g4) ^ (rb & 6)) * 16));
+    }
+  };
+  auto mma_slice = [&](const Frag& F) {
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+    constexpr int NR = 4 + FN, NMF = 4 * FN;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, NMF - NR, 0);
+  };
+  // one conv over the two planes of `src` (plane stride `pst`): steps (chunk c, tap t), the lane's first B row
+  // of tap t at rb0 + t * tstride; each step's second K-slice is read under its first, the next step's first
+  // under its second
+  Frag F0, F1;
+  int s = 0;
+  auto conv = [&](const char* src, int pst, int rb0, int tstride, auto&& at_first_step) {
+    for (int m = 0; m < ns; ++m, ++s) {
+      const bool more = m + 1 < ns;
+      wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);  // this step's weights and the next step's
+      barrier();
+      if (s + NWS - 1 < S) stage_w(s + NWS - 1);
+      const int sl = s % NWS;
+      const int c = m >= k ? 1 : 0, t = m - c * k;
+      if (m == 0) {
+        at_first_step();
+        read_frag(F0, 0, sl, src, rb0);
+      }
+      read_frag(F1, 1, sl, src + c * pst, rb0 + t * tstride);
+      mma_slice(F0);
+      if (more) {
+        const int c2 = m + 1 >= k ? 1 : 0, t2 = m + 1 - c2 * k;
+        read_frag(F0, 0, (s + 1) % NWS, src + c2 * pst, rb0 + t2 * tstride);
+      }
+      mma_slice(F1);
+    }
+  };
+
+  // ---- prologue ----
+  stage_x(0);
+#pragma unroll
+  for (int p = 0; p < NWS - 1; ++p)
+    if (p < S) stage_w(p);
+
+  const float* par = reinterpret_cast<const float*>(smem + PAR_OFF);
+  const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;  // + fp * 32: this lane's 8 channels after the pair swap
+  const char* xpl = smem + X_OFF + wm * XPL;        // this wave's rows' plane of X
+  for (int ti = 0; ti < nmine; ++ti) {
+    int b, n0;
+    tile_of(ti, b, n0);
+    // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + h2 + h1), then the
+    // in-place lrelu of the landed raw rows ----
+    wait_vmcnt(issued - xmk);
+    barrier();
+    u32x4 rv[2][FN], yv[2][FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int r = wn * WNC + fn * 16 + l16 + h2 + h1;
+        const int q = fp * 4 + (g4 & 1) * 2 + (g4 >> 1);
+        rv[fp][fn] = *reinterpret_cast<const u32x4*>(xpl + r * 128 + ((q ^ (r & 6)) * 16));
+      }
+    barrier();
+    for (int e = tid; e < 2 * XROWS * 8; e += NT) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(smem + X_OFF + e * 16);
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        v[w] = pack2((bf16)lrelu_f(bf2(v[w], 0), a.slope), (bf16)lrelu_f(bf2(v[w], 1), a.slope));
+      *reinterpret_cast<u32x4*>(smem + X_OFF + e * 16) = v;
+    }
+    // ---- 2. conv1 (published by its first step's barrier) ----
+    zero_acc();
+    int ymk = 0;
+    conv(smem + X_OFF, XPL, wn * WNC + l16, d, [&] {
+      // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2 (asm, so the
+      // counted wait below retires them instead of a compiler vmcnt(0) that would drain the row staging)
+      if constexpr ((EF & VE_ACCUM) != 0) {
+#pragma unroll
+        for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) {
+            const int i = min(n0 + wn * WNC + fn * 16 + l16, L - 1);
+            asm volatile("global_load_dwordx4 %0, %1, off"
+                         : "=v"(yv[fp][fn])
+                         : "v"(a.y + ((size_t)b * L + i) * C + wm * 64 + fp * 32 + ch16)
+                         : "memory");
+          }
+        issued += 2 * FN;
+        ymk = issued;
+      }
+    });
+    // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - h2 + j), zero outside [0, L)
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int j = wn * WNC + fn * 16 + l16;
+        const int f = n0 - h2 + j;
+        const bool ok = f >= 0 && f < L;
+        uint32_t o[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int fm = 2 * fp + h;
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + wm * 64 + fm * 16 + 4 * g4);
+          bf16 ob[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const bf16 rb = (bf16)(acc[fm][fn][r] + b4[r]);
+            ob[r] = ok ? (bf16)lrelu_f((float)rb, a.slope) : (bf16)0.f;
+          }
+          o[h][0] = pack2(ob[0], ob[1]);
+          o[h][1] = pack2(ob[2], ob[3]);
+        }
+        swap16(o[0][0], o[1][0]);
+        swap16(o[0][1], o[1][1]);
+        const int q = fp * 4 + (g4 & 1) * 2 + (g4 >> 1);
+        *reinterpret_cast<u32x4*>(smem + T_OFF + wm * TPL + j * 128 + ((q ^ (j & 6)) * 16)) =
+            u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
+      }
+    // ---- 3. conv2 ----
+    zero_acc();
+    conv(smem + T_OFF, TPL, wn * WNC + l16, 1, [&] {
+      // every wave is past conv1's reads of the row planes: stage the next tile's raw rows into them
+      if (ti + 1 < nmine) stage_x(ti + 1);
+    });
+    // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
+    if constexpr ((EF & VE_ACCUM) != 0) {
+      wait_vmcnt(issued - ymk);
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fp][fn]));  // no use of yv before the wait
+    }
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int i = wn * WNC + fn * 16 + l16;  // output frame n0 + i
+        uint32_t rx0 = rv[fp][fn][0], rx1 = rv[fp][fn][1], ry0 = rv[fp][fn][2], ry1 = rv[fp][fn][3];
+        swap16(rx0, ry0);  // back to the accumulator layout
+        swap16(rx1, ry1);
+        uint32_t yx0 = 0, yx1 = 0, yy0 = 0, yy1 = 0;
+        if constexpr ((EF & VE_ACCUM) != 0) {
+          yx0 = yv[fp][fn][0], yx1 = yv[fp][fn][1], yy0 = yv[fp][fn][2], yy1 = yv[fp][fn][3];
+          swap16(yx0, yy0);
+          swap16(yx1, yy1);
+        }
+        uint32_t o1[2][2], o2[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int fm = 2 * fp + h;
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + C + wm * 64 + fm * 16 + 4 * g4);
+          const uint32_t rr[2] = {h ? ry0 : rx0, h ? ry1 : rx1};
+          const uint32_t yy[2] = {h ? yy0 : yx0, h ? yy1 : yx1};
+          bf16 ob[4], ab[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[fm][fn][r] + b4[r];
+            v = v + bf2(rr[r >> 1], r & 1);
+            if constexpr ((EF & VE_ACCUM) != 0) v = bf2(yy[r >> 1], r & 1) + v;
+            if constexpr ((EF & VE_DIV) != 0) v = v / a.div;
+            ob[r] = (bf16)v;
+            ab[r] = (bf16)lrelu_f((float)ob[r], a.slope);
+          }
+          o1[h][0] = pack2(ob[0], ob[1]);
+          o1[h][1] = pack2(ob[2], ob[3]);
+          o2[h][0] = pack2(ab[0], ab[1]);
+          o2[h][1] = pack2(ab[2], ab[3]);
+        }
+        swap16(o1[0][0], o1[1][0]);
+        swap16(o1[0][1], o1[1][1]);
+        const bool ok = i < BN && n0 + i < L;
+        const size_t o = ((size_t)b * L + n0 + i) * C + wm * 64 + fp * 32 + ch16;
+        *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
+        if constexpr ((EF & VE_DUAL) != 0) {
+          swap16(o2[0][0], o2[1][0]);
+          swap16(o2[0][1], o2[1][1]);
+          *reinterpret_cast<u32x4*>(ok ? a.y2 + o : a.trash + 8 * lane) = u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]};
+        }
+      }
+    issued += 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+  }
+}
+
+bool vpair128_supported(int k, int d) {
+  return k >= 3 && k % 2 == 1 && NF1 - (k - 1) > 0 && NF1 + d * (k - 1) <= XROWS;
+}
+
+static int vp128_cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+int launch_vpair128(int ef, const VPairArgs& a, hipStream_t st) {
+  MT_REQUIRE(a.x && a.w1 && a.w2 && a.b1 && a.b2 && a.y && a.zero && a.trash && a.B > 0 && a.L > 0,
+             "vpair128: null argument / empty");
+  MT_REQUIRE(vpair128_supported(a.taps, a.dil), "vpair128: k %d d %d", a.taps, a.dil);
+  MT_REQUIRE(!(ef & VE_DUAL) || a.y2, "vpair128: y2");
+  MT_REQUIRE(a.y != a.x, "vpair128: y must not alias x (neighbour tiles read x's halo)");
+  const int BN = NF1 - (a.taps - 1);
+  const long ntiles = (long)a.B * ((a.L + BN - 1) / BN);
+  MT_REQUIRE(ntiles < (1L << 31), "vpair128: too many tiles");
+  const int G = (int)std::min<long>(ntiles, vp128_cu_count());
+  // probe: the pair is two of the family's convs (SURVEY §8d algorithmic FLOPs and layer-boundary bytes)
+  const double flops = 2.0 * 2.0 * C * C * a.taps * (double)a.B * a.L;
+  const double bytes = 2.0 * (2.0 * 2.0 * C * (double)a.B * a.L) + 2.0 * 2.0 * C * C * a.taps;
+  probe_begin(PROBE_VCONV, st);
+  switch (ef) {
+    case 0: hipLaunchKernelGGL((vpair128_kernel<0>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_ACCUM: hipLaunchKernelGGL((vpair128_kernel<VE_ACCUM>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_ACCUM | VE_DIV: hipLaunchKernelGGL((vpair128_kernel<VE_ACCUM | VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_ACCUM | VE_DIV | VE_DUAL:
+      hipLaunchKernelGGL((vpair128_kernel<VE_ACCUM | VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a);
+      break;
+    case VE_DIV: hipLaunchKernelGGL((vpair128_kernel<VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_DIV | VE_DUAL: hipLaunchKernelGGL((vpair128_kernel<VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a); break;
+    default: set_error("vpair128: epilogue %d not compiled in", ef); return -1;
+  }
+  MT_CHECK_HIP(hipGetLastError());
+  probe_end(PROBE_VCONV, st, flops, bytes, PROBE_TAG_VPAIR128);
+  const int rec[VCLOG_FIELDS] = {ef | 0x10000, C, BN, 0, (int)ntiles, G, a.taps, C, C, a.B, a.L};
+  vclog_record(rec);
+  return 0;
+}
+
+}  // namespace mt

@@ -11,9 +11,11 @@
 //   2. conv1: 32 rows x 768 frames over k taps; epilogue lrelu(round(acc + b1)), zero outside [0, L) -> T;
 //   3. conv2: 32 rows x 752 frames over k taps of T; epilogue + b2 + x (the residual rows, read from the
 //      staged raw rows before step 1's in-place pass) [+ xs, / nk] -> y.
-// A tap is one K = 32 MFMA slice, so a step carries FOUR taps (8 KiB of weights, read straight from the generic
-// [32 rows][k][32] packing) and a wave covers 96 frames (6 fragments) x both 16-row fragments: 48 MFMAs per
-// wave between barriers, as in the 64-channel kernel.
+// A tap is one K = 32 MFMA slice and a wave covers 96 frames (6 fragments) x both 16-row fragments. ALL of the
+// pair's weights (2 convs x k taps x 2 KiB <= 52 KiB, read straight from the generic [32 rows][k][32] packing)
+// land in LDS once per launch, so the conv loops run with no weight DMA and no barrier: a tile has four
+// barriers (rows landed, residuals read, rows activated, T written) where a 3-slot weight ring of 4-tap steps
+// had 2 + 2 ceil(k / 4).
 // LDS rows are 64 bytes (four 16-byte chunks); chunk c of row r lives in slot c ^ ((r >> 1) & 2). With the
 // ds_read_b128 lane groups ({0-3,12-15,20-27}, ...; MI355X_MICROARCH.md §LDS) every B-fragment read (16
 // consecutive rows from any start row, chunk g4) and every A-fragment read is conflict-free, and so are the
@@ -39,14 +41,12 @@ constexpr int XROWS = NF1 + 128;     // staged input rows >= NF1 + 2 * h1, h1 = 
 constexpr int XBUF = XROWS * RB;
 constexpr int TROWS = NF1 + 16;      // conv2's last (discarded) fragment reads up to row NF1 - 1 + 16
 constexpr int TBUF = TROWS * RB;
-constexpr int TAPS = 4;              // taps per step
+constexpr int KMAX = 13;             // largest kernel size whose weights stay resident
 constexpr int TAPW = C * RB;         // one tap: 32 output rows x 32 input channels (2 KiB)
-constexpr int WSLOT = TAPS * TAPW;
-constexpr int NWS = 3;
-constexpr int T_OFF = XBUF, W_OFF = T_OFF + TBUF, PAR_OFF = W_OFF + NWS * WSLOT;
+constexpr int T_OFF = XBUF, W_OFF = T_OFF + TBUF, PAR_OFF = W_OFF + 2 * KMAX * TAPW;  // W: [conv][tap]
 constexpr int LDS_BYTES = PAR_OFF + 2 * C * 4;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-static_assert(XROWS % 128 == 0 && WSLOT == 8 * 1024, "one 1 KiB DMA per wave per weight step");
+static_assert(XROWS % 128 == 0 && TAPW == 2 * 1024, "two 1 KiB DMAs per tap");
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 2; }
 
@@ -98,25 +98,20 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   __syncthreads();
 
   int issued = 0, xmk = 0;
-  int wmk[NWS] = {};
-  const int ns = (k + TAPS - 1) / TAPS;  // steps per conv
   auto tile_of = [&](int ti, int& b, int& n0) __attribute__((always_inline)) {
     const int tile = gl + ti * G;
     b = tile / ntn;
     n0 = (tile - b * ntn) * BN;
   };
-  // taps 4m .. 4m+3 (clamped to k-1) of conv1 or conv2 from the generic packing [32 rows][k][32]: wave w moves
-  // tap w / 2, rows (w & 1) * 16 .. + 15
-  auto stage_w = [&](int s) __attribute__((always_inline)) {
-    const int r2 = s % (2 * ns);
-    const int m = r2 < ns ? r2 : r2 - ns;
-    const bf16* w = r2 < ns ? a.w1 : a.w2;
-    const int u = wave >> 1, r = (wave & 1) * 16 + lrow;
-    const int t = min(TAPS * m + u, k - 1);
-    glds16(w + ((size_t)r * k + t) * C + (lp ^ swz(r)) * 8,
-           smem + W_OFF + (s % NWS) * WSLOT + u * TAPW + (wave & 1) * 1024);
-    issued += 1;
-    wmk[s % NWS] = issued;
+  // every tap of both convs from the generic packing [32 rows][k][32]: DMA j moves tap (j / 2) % k of conv
+  // j / 2k, rows (j & 1) * 16 .. + 15
+  auto stage_weights = [&]() {
+    for (int j = wave; j < 4 * k; j += 8) {
+      const int cv = j / (2 * k), t = (j >> 1) - cv * k, r = (j & 1) * 16 + lrow;
+      const bf16* w = cv ? a.w2 : a.w1;
+      glds16(w + ((size_t)r * k + t) * C + (lp ^ swz(r)) * 8, smem + W_OFF + (cv * k + t) * TAPW + (j & 1) * 1024);
+      ++issued;
+    }
   };
   // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r (zero rows past this workgroup's last tile)
   auto stage_x = [&](int ti) __attribute__((always_inline)) {
@@ -158,9 +153,9 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   struct Frag {
     bf16x8 A[2], B[FN];
   };
-  // tap u of a step: A = the slot's 2 row fragments of that tap, B = FN frame fragments at rows rb0 + 16 fn
-  auto read_frag = [&](Frag& F, int slot, int u, const char* src, int rb0) __attribute__((always_inline)) {
-    const char* pa = smem + W_OFF + slot * WSLOT + u * TAPW + l16 * RB + ((g4 ^ swz(l16)) * 16);
+  // tap t of conv cv: A = the tap's 2 row fragments, B = FN frame fragments at rows rb0 + 16 fn
+  auto read_frag = [&](Frag& F, int cv, int t, const char* src, int rb0) __attribute__((always_inline)) {
+    const char* pa = smem + W_OFF + (cv * k + t) * TAPW + l16 * RB + ((g4 ^ swz(l16)) * 16);
 #pragma unroll
     for (int f = 0; f < 2; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 16 * RB);
 #pragma unroll
@@ -183,45 +178,25 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     }
     __builtin_amdgcn_sched_group_barrier(0x008, NMF - NR, 0);
   };
-  // one conv over `src`: ns steps of up to four taps (row of tap t for this lane's first fragment:
-  // rb0 + t * tstride); each tap's fragments are read under the previous tap's MFMAs, the next step's first
-  // tap under this step's last (a full step has an even tap count, so it always lands in F[0]).
-  // Every step stages a weight step unconditionally (past the last one: a harmless reload into the free
-  // slot) and the first step is peeled, so its global loads (conv1: the residual rows; conv2: the next tile's
-  // raw rows) are on every path: the compiler's own wait before the epilogue consumes the residual registers
-  // then counts past the >= 8 loads issued after them instead of draining the next tile's rows (vmcnt(0)).
-  Frag F[2];
-  int s = 0;
-  auto conv_step = [&](const char* src, int rb0, int tstride, int m) __attribute__((always_inline)) {
-    const bool more = m + 1 < ns;
-    const int t0 = TAPS * m, nt = min(TAPS, k - t0), sl = s % NWS;
-#pragma unroll
-    for (int u = 0; u < TAPS; ++u) {
-      if (u + 1 < nt) read_frag(F[(u + 1) & 1], sl, u + 1, src, rb0 + (t0 + u + 1) * tstride);
-      else if (u + 1 == TAPS && more) read_frag(F[0], (s + 1) % NWS, 0, src, rb0 + (t0 + TAPS) * tstride);
-      if (u < nt) mma_tap(F[u & 1]);
-    }
-  };
-  auto conv = [&](const char* src, int rb0, int tstride, auto&& at_first_step) __attribute__((always_inline)) {
-    wait_vmcnt(issued - wmk[(ns > 1 ? s + 1 : s) % NWS]);  // this step's weights and the next step's
-    barrier();
-    stage_w(s + NWS - 1);
-    at_first_step();
-    read_frag(F[0], s % NWS, 0, src, rb0);
-    conv_step(src, rb0, tstride, 0);
-    ++s;
-    for (int m = 1; m < ns; ++m, ++s) {
-      wait_vmcnt(issued - wmk[(m + 1 < ns ? s + 1 : s) % NWS]);
-      barrier();
-      stage_w(s + NWS - 1);
-      conv_step(src, rb0, tstride, m);
+  // one conv over `src` (row of tap t for this lane's first fragment: rb0 + t * tstride), taps ascending, each
+  // tap's fragments read under the previous tap's MFMAs; no barrier inside (weights resident, `src` published)
+  Frag F0, F1;
+  auto conv = [&](int cv, const char* src, int rb0, int tstride) __attribute__((always_inline)) {
+    read_frag(F0, cv, 0, src, rb0);
+    for (int t = 0; t < k; t += 2) {
+      const bool one = t + 1 < k, two = t + 2 < k;
+      if (one) read_frag(F1, cv, t + 1, src, rb0 + (t + 1) * tstride);
+      mma_tap(F0);
+      if (one) {
+        if (two) read_frag(F0, cv, t + 2, src, rb0 + (t + 2) * tstride);
+        mma_tap(F1);
+      }
     }
   };
 
-  // ---- prologue ----
+  // ---- prologue: the weights, then the first tile's rows (the first row wait covers both) ----
+  stage_weights();
   stage_x(0);
-#pragma unroll
-  for (int p = 0; p < NWS - 1; ++p) stage_w(p);
 
   const float* par = reinterpret_cast<const float*>(smem + PAR_OFF);
   const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;  // this lane's 8 channels after the fragment swap
@@ -249,26 +224,26 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
         v[w] = pack2((bf16)lrelu_f(bf2(v[w], 0), a.slope), (bf16)lrelu_f(bf2(v[w], 1), a.slope));
       *reinterpret_cast<u32x4*>(smem + e * 16) = v;
     }
-    // ---- 2. conv1 (published by its first step's barrier) ----
+    barrier();  // activated rows published
+    // ---- 2. conv1 ----
     zero_acc();
     int ymk = 0;
-    conv(smem, wave * WNC + l16, d, [&] {
-      // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2. Issued as asm so
-      // that the counted wait below retires them: hipcc drains EVERY in-flight LDS-DMA (vmcnt(0)) before the use
-      // of a compiler-visible load result, which would expose the next tile's row staging at each epilogue.
-      if constexpr ((EF & VE_ACCUM) != 0) {
+    // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2. Issued as asm so that
+    // the counted wait below retires them: hipcc drains EVERY in-flight LDS-DMA (vmcnt(0)) before the use of a
+    // compiler-visible load result, which would expose the next tile's row staging at each epilogue.
+    if constexpr ((EF & VE_ACCUM) != 0) {
 #pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const int i = min(n0 + wave * WNC + fn * 16 + l16, L - 1);
-          asm volatile("global_load_dwordx4 %0, %1, off"
-                       : "=v"(yv[fn])
-                       : "v"(a.y + ((size_t)b * L + i) * C + ch16)
-                       : "memory");
-        }
-        issued += FN;
-        ymk = issued;
+      for (int fn = 0; fn < FN; ++fn) {
+        const int i = min(n0 + wave * WNC + fn * 16 + l16, L - 1);
+        asm volatile("global_load_dwordx4 %0, %1, off"
+                     : "=v"(yv[fn])
+                     : "v"(a.y + ((size_t)b * L + i) * C + ch16)
+                     : "memory");
       }
-    });
+      issued += FN;
+      ymk = issued;
+    }
+    conv(0, smem, wave * WNC + l16, d);
     // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - HALO2 + j), zero outside [0, L)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
@@ -293,11 +268,10 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       *reinterpret_cast<u32x4*>(smem + T_OFF + j * RB + ((qc ^ swz(j)) * 16)) = u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
     }
     // ---- 3. conv2 ----
+    barrier();  // T published; every wave is past conv1's reads of the row buffer: stage the next tile's rows
+    stage_x(ti + 1);
     zero_acc();
-    conv(smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, [&] {
-      // every wave is past conv1's reads of the row buffer: stage the next tile's raw rows into it
-      stage_x(ti + 1);
-    });
+    conv(1, smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1);
     // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
     if constexpr ((EF & VE_ACCUM) != 0) {
       wait_vmcnt(issued - ymk);
@@ -353,7 +327,9 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing row / weight DMAs land before LDS is freed
 }
 
-bool vpair32_supported(int k, int d) { return k >= 2 && (k - 1) / 2 <= HALO2 && NF1 + d * (k - 1) <= XROWS; }
+bool vpair32_supported(int k, int d) {
+  return k >= 2 && k <= KMAX && (k - 1) / 2 <= HALO2 && NF1 + d * (k - 1) <= XROWS;
+}
 
 static int cu_count() {
   static int n = 0;

@@ -339,9 +339,10 @@ class VocoderEngine:
     def set_fusion(self, enable: bool) -> None:
         check(lib().mt_vocoder_set_fusion(self.h, int(bool(enable))), "vocoder_set_fusion")
 
-    def set_pair(self, enable) -> None:
-        """bf16: the 64-channel stage's ResBlock pairs fused into one launch each (default) or per layer."""
-        check(lib().mt_vocoder_set_pair(self.h, int(bool(enable))), "vocoder_set_pair")
+    def set_pair(self, mode) -> None:
+        """bf16 ResBlock pairs as one launch each: 1 (default) the 64- / 32-channel stages and the 128-channel
+        stage's k = 3 resblock; 4 every 128-channel pair too; 2 none of the 128-channel stage; 0 all per layer."""
+        check(lib().mt_vocoder_set_pair(self.h, int(mode)), "vocoder_set_pair")
 
     def set_vconv(self, mode) -> None:
         """0 generic per-layer kernel, 1 vconv for the 128/256-channel stages, 2 (default) also for 64."""
@@ -549,7 +550,7 @@ def probe_pause(paused: bool) -> None:
     check(lib().mt_probe_pause(int(bool(paused))), "probe_pause")
 
 
-PROBE_TAGS = ("vconv", "vpair", "vpair32", "rbfuse")
+PROBE_TAGS = ("vconv", "vpair", "vpair32", "rbfuse", "vpair128")
 
 
 def probe_detail(cap: int = 4096) -> List[Dict[str, float]]:

@@ -172,17 +172,23 @@ def test_vconv_stages_match_generic_per_layer(T):
 
 @pytest.mark.parametrize("B,T", [(2, 37), (3, 200)])
 def test_fused_pair_stage_bit_identical_to_per_layer(B, T):
-    """bf16: the 64- and 32-channel stages as fused ResBlock pairs (mt_vpair / mt_vpair32: intermediate in LDS,
-    input activation applied on chip, ping-pong chain state) reproduce the per-layer paths bit for bit (same
-    rounding points, same MFMA accumulation order), including tile edges and utterance ends. References: pair 0
-    (64-channel stage per layer on mt_vconv, 32-channel stage on the fused-stage kernel mt_rbfuse) and fusion 0
-    (32-channel stage on the generic per-layer conv kernel)."""
+    """bf16: the 128-, 64- and 32-channel stages as fused ResBlock pairs (mt_vpair128 / mt_vpair / mt_vpair32:
+    intermediate in LDS, input activation applied on chip, ping-pong chain state) reproduce the per-layer paths
+    bit for bit (same rounding points, same MFMA accumulation order), including tile edges and utterance ends.
+    References: pair 0 (128- and 64-channel stages per layer on mt_vconv, 32-channel stage on the fused-stage
+    kernel mt_rbfuse), pair 2 / 4 (128-channel stage per layer / every pair fused; default 1 fuses its k = 3
+    resblock) and fusion 0 (32-channel stage on the generic
+    per-layer conv kernel)."""
     g, gen = _gen("bf16", True)
     mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(7 + T)) * 2 - 5
     mel = mel.to(DEV)
     eng = gen.engine()
     eng.set_pair(0)
     a = gen(mel)
+    eng.set_pair(2)  # pairs except the 128-channel stage (per layer on mt_vconv)
+    d = gen(mel)
+    eng.set_pair(4)  # every 128-channel pair fused too
+    e = gen(mel)
     eng.set_pair(1)
     eng.set_fusion(0)
     c = gen(mel)
@@ -190,6 +196,8 @@ def test_fused_pair_stage_bit_identical_to_per_layer(B, T):
     b = gen(mel)
     assert torch.isfinite(b).all()
     assert torch.equal(a, b), (a - b).abs().max().item()
+    assert torch.equal(d, b), (d - b).abs().max().item()
+    assert torch.equal(e, b), (e - b).abs().max().item()
     assert torch.equal(c, b), (c - b).abs().max().item()
 
 
@@ -393,8 +401,9 @@ def test_launch_probe_times_fused_stage():
 
 
 def test_launch_probe_times_vconv_launches():
-    """PROBE_VCONV: events around every ResBlock-conv launch of the default vocoder (stages 1-2: 3
-    resblocks x 3 pairs x 2 per-layer convs; stages 3-4: 3 x 3 fused pairs each), their algorithmic FLOPs summed."""
+    """PROBE_VCONV: events around every ResBlock-conv launch of the default vocoder (stage 1 and the k = 7 / 11
+    resblocks of stage 2: 5 resblocks x 3 pairs x 2 per-layer convs; the k = 3 resblock of stage 2: 3 fused
+    pairs; stages 3-4: 3 x 3 fused pairs each), their algorithmic FLOPs summed."""
     from matcha_hip import runtime as rt
     g, gen = _gen("bf16", True)
     mel = t(g["mel"], DEV)
@@ -404,9 +413,9 @@ def test_launch_probe_times_vconv_launches():
     detail = rt.probe_detail()
     p = rt.probe_stop()
     B, T = mel.shape[0], mel.shape[2]
-    assert p["launches"] == 36 + 18 and p["ms"] > 0
+    assert p["launches"] == 30 + 21 and p["ms"] > 0
     kinds = [d["kind"] for d in detail]
-    assert (kinds.count("vconv"), kinds.count("vpair"), kinds.count("vpair32")) == (36, 9, 9), kinds
+    assert [kinds.count(k) for k in ("vconv", "vpair128", "vpair", "vpair32")] == [30, 3, 9, 9], kinds
     assert abs(sum(d["flops"] for d in detail) - p["flops"]) <= 1e-9 * p["flops"]
     assert abs(sum(d["ms"] for d in detail) - p["ms"]) <= 1e-3 * p["ms"]
     want = sum(2.0 * 6 * C * C * 21 * B * T * r for C, r in ((256, 8), (128, 64), (64, 128), (32, 256)))
