@@ -94,6 +94,24 @@ __device__ __forceinline__ float mish_f(float x) {
   return x * __fdividef(n, n + 2.f);
 }
 __device__ __forceinline__ float lrelu_f(float x, float slope) { return x > 0.f ? x : x * slope; }
+
+// bf16 epilogue helpers: two channels of one packed word as packed fp32 math (v_pk_add_f32 / v_pk_mul_f32), one
+// v_cvt_pk_bf16_f32 (RNE) per word, lrelu as max(x, slope * x) — equal to x > 0 ? x : slope * x for every non-NaN
+// x when 0 <= slope <= 1 (files using it build with -mno-amdgpu-ieee so the max needs no NaN canonicalize)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+__device__ __forceinline__ f32x2 unpk_bf16(uint32_t w) {
+  return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+__device__ __forceinline__ f32x2 lrelu2(f32x2 t, float slope) {
+  const f32x2 m = t * slope;
+  return f32x2{__builtin_fmaxf(t.x, m.x), __builtin_fmaxf(t.y, m.y)};
+}
+// lrelu of the two bf16 of a packed word, rounded back (the producer-side activated copy's rounding)
+__device__ __forceinline__ uint32_t lrelu_pk(uint32_t w, float slope) { return pk_bf16(lrelu2(unpk_bf16(w), slope)); }
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + expf(-x)); }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -107,20 +107,10 @@ __device__ __forceinline__ void rb_chunk_dispatch(int nj, int ng, const char* bs
   }
 }
 
-// bf16 epilogue helpers: pairs of frames' channels as packed fp32 math (v_pk_add / v_pk_mul), one
-// v_cvt_pk_bf16_f32 per pair, lrelu as max(x, slope * x) (equal to x > 0 ? x : slope * x for 0 < slope < 1)
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t rb_pack(f32x2 v) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
-}
-__device__ __forceinline__ f32x2 rb_unpack(uint32_t w) {
-  return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
-}
-__device__ __forceinline__ f32x2 rb_lrelu(f32x2 t, float slope) {
-  const f32x2 m = t * slope;
-  return f32x2{__builtin_fmaxf(t.x, m.x), __builtin_fmaxf(t.y, m.y)};
-}
+// bf16 epilogue helpers (mt_common.h): packed fp32 pairs, one v_cvt_pk_bf16_f32 per pair, max-form lrelu
+__device__ __forceinline__ uint32_t rb_pack(f32x2 v) { return pk_bf16(v); }
+__device__ __forceinline__ f32x2 rb_unpack(uint32_t w) { return unpk_bf16(w); }
+__device__ __forceinline__ f32x2 rb_lrelu(f32x2 t, float slope) { return lrelu2(t, slope); }
 
 template <class E, int C, int N>
 __global__ __launch_bounds__(512) void rbfuse_kernel(RBArgs a) {

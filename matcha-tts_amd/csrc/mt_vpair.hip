@@ -20,6 +20,8 @@
 // and the MFMA accumulation order per output is the same (taps ascending, one 64-channel chunk, two K-slices),
 // so the results are the same bits.
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "mt_probe.h"
 #include "mt_vpair.h"
@@ -136,10 +138,6 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     x = r[0];
     y = r[1];
   };
-  auto bf2 = [](uint32_t w, int i) -> float { return __uint_as_float(i ? (w & 0xffff0000u) : (w << 16)); };
-  auto pack2 = [](bf16 lo, bf16 hi) -> uint32_t {
-    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
-  };
   const int ha = l16 & 6;
 
   f32x4 acc[4][FN];
@@ -237,8 +235,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       const int e = tid + i * NT;
       u32x4 v = *reinterpret_cast<const u32x4*>(smem + e * 16);
 #pragma unroll
-      for (int w = 0; w < 4; ++w)
-        v[w] = pack2((bf16)lrelu_f(bf2(v[w], 0), a.slope), (bf16)lrelu_f(bf2(v[w], 1), a.slope));
+      for (int w = 0; w < 4; ++w) v[w] = lrelu_pk(v[w], a.slope);
       *reinterpret_cast<u32x4*>(smem + e * 16) = v;
     }
     // ---- 2. conv1 (published by its first step's barrier) ----
@@ -276,14 +273,11 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         for (int h = 0; h < 2; ++h) {
           const int fm = 2 * fp + h;
           const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + fm * 16 + 4 * g4);
-          bf16 ob[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const bf16 rb = (bf16)(acc[fm][fn][r] + b4[r]);
-            ob[r] = ok ? (bf16)lrelu_f((float)rb, a.slope) : (bf16)0.f;
-          }
-          o[h][0] = pack2(ob[0], ob[1]);
-          o[h][1] = pack2(ob[2], ob[3]);
+          // lrelu(round(acc + b1)), rounded again; zero outside [0, L)
+          const uint32_t t0 = pk_bf16(f32x2{acc[fm][fn][0], acc[fm][fn][1]} + f32x2{b4[0], b4[1]});
+          const uint32_t t1 = pk_bf16(f32x2{acc[fm][fn][2], acc[fm][fn][3]} + f32x2{b4[2], b4[3]});
+          o[h][0] = ok ? lrelu_pk(t0, a.slope) : 0u;
+          o[h][1] = ok ? lrelu_pk(t1, a.slope) : 0u;
         }
         swap16(o[0][0], o[1][0]);
         swap16(o[0][1], o[1][1]);
@@ -326,20 +320,16 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
           const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + C + fm * 16 + 4 * g4);
           const uint32_t rr[2] = {h ? ry0 : rx0, h ? ry1 : rx1};
           const uint32_t yy[2] = {h ? yy0 : yx0, h ? yy1 : yx1};
-          bf16 ob[4], ab[4];
+          // round(acc + b2 + x [+ xs] [/ nk]) and its lrelu, two channels per packed op
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = acc[fm][fn][r] + b4[r];
-            v = v + bf2(rr[r >> 1], r & 1);
-            if constexpr ((EF & VE_ACCUM) != 0) v = bf2(yy[r >> 1], r & 1) + v;
-            if constexpr ((EF & VE_DIV) != 0) v = v / a.div;
-            ob[r] = (bf16)v;
-            ab[r] = (bf16)lrelu_f((float)ob[r], a.slope);
+          for (int u = 0; u < 2; ++u) {
+            f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]} + f32x2{b4[2 * u], b4[2 * u + 1]};
+            v = v + unpk_bf16(rr[u]);
+            if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
+            if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
+            o1[h][u] = pk_bf16(v);
+            o2[h][u] = lrelu_pk(o1[h][u], a.slope);
           }
-          o1[h][0] = pack2(ob[0], ob[1]);
-          o1[h][1] = pack2(ob[2], ob[3]);
-          o2[h][0] = pack2(ab[0], ab[1]);
-          o2[h][1] = pack2(ab[2], ab[3]);
         }
         swap16(o1[0][0], o1[1][0]);
         swap16(o1[0][1], o1[1][1]);
@@ -354,6 +344,262 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       }
     issued += 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
   }
+}
+
+// ---- k = 3 pairs: HBM-bound (stage 3 at B = 256: 2.5 ms per pair for 6.3 GB of x in / y out), so this variant
+// keeps the pair's 48 KiB of weights resident (no ring, four barriers per tile) and double-buffers the row
+// staging: tiles of 256 conv1 frames (2 fragments per wave, HALO2 = h2 = 1, 254 output frames) and the NEXT
+// tile's rows issued at the start of this one. Same fragments, accumulation order and rounding points as
+// vpair_kernel (taps ascending, two K-slices each), so the same bits.
+namespace {
+// FNT 16-frame fragments per wave; DB: two row buffers (the next tile's rows issued at the start of this one)
+template <int FNT, bool DB>
+struct K3G {
+  static constexpr int FN = FNT, WNC = 16 * FN, NF1 = 8 * WNC, HALO2 = 1, BN = NF1 - 2 * HALO2;
+  static constexpr int XROWS = NF1 + 16;  // >= NF1 + 2 d for d <= 8
+  static constexpr int XBUF = XROWS * 128, NXB = DB ? 2 : 1;
+  static constexpr int TROWS = NF1 + 8;   // conv2 reads rows <= NF1 - 1 + 2
+  static constexpr int T_OFF = NXB * XBUF, W_OFF = T_OFF + TROWS * 128, PAR_OFF = W_OFF + 6 * TAPW;
+  static constexpr int LDS = PAR_OFF + 2 * C * 4;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(XROWS % 8 == 0, "rows staged 8 per DMA");
+};
+}  // namespace
+
+template <int EF, int FNT, bool DB>
+__global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
+  using G3 = K3G<FNT, DB>;
+  __shared__ __attribute__((aligned(1024))) char smem[G3::LDS];
+  constexpr int FN = G3::FN, WNC = G3::WNC, NF1 = G3::NF1, HALO2 = G3::HALO2, BN = G3::BN;
+  constexpr int K3_XROWS = G3::XROWS, K3_XBUF = G3::XBUF, K3_T_OFF = G3::T_OFF, K3_W_OFF = G3::W_OFF;
+  constexpr int K3_PAR_OFF = G3::PAR_OFF;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g4 = lane >> 4, l16 = lane & 15, lrow = lane >> 3, lp = lane & 7;
+  const int d = a.dil, L = a.L;
+  const int h1 = d;  // k = 3: h1 = d, h2 = 1 = HALO2
+  const int ntn = (L + BN - 1) / BN, ntiles = a.B * ntn;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
+  const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
+  if (nmine == 0) return;
+  for (int i = tid; i < C; i += NT) {
+    reinterpret_cast<float*>(smem + K3_PAR_OFF)[i] = a.b1[i];
+    reinterpret_cast<float*>(smem + K3_PAR_OFF)[C + i] = a.b2[i];
+  }
+  __syncthreads();
+
+  int issued = 0;
+  int xmk[2] = {0, 0};
+  auto tile_of = [&](int ti, int& b, int& n0) {
+    const int tile = gl + ti * G;
+    b = tile / ntn;
+    n0 = (tile - b * ntn) * BN;
+  };
+  // both convs' 3 taps: DMA j moves rows (j & 7) * 8 .. + 7 of tap j / 8 (conv (j / 8) / 3)
+  for (int j = wave; j < 48; j += 8) {
+    const int tp = j >> 3, r = (j & 7) * 8 + lrow;
+    const bf16* w = (tp < 3 ? a.w1 : a.w2) + (size_t)(tp % 3) * C * 64;
+    vp_glds16(w + r * 64 + (lp ^ (r & 6)) * 8, smem + K3_W_OFF + tp * TAPW + (j & 7) * 1024);
+    ++issued;
+  }
+  auto stage_x = [&](int ti) {  // raw rows of tile ti into buffer ti & 1: row r = frame n0 - HALO2 - h1 + r
+    int b, n0;
+    tile_of(ti, b, n0);
+    const bool live = ti < nmine;
+    const bf16* xb = a.x + (size_t)(live ? b : 0) * L * C;
+    const int f0 = n0 - HALO2 - h1, R1 = live ? NF1 + 2 * h1 : 0;
+    for (int j = wave; j < K3_XROWS / 8; j += 8) {
+      const int r = 8 * j + lrow;
+      const int q = lp ^ (r & 6);
+      const int f = f0 + r;
+      const bool ok = r < R1 && f >= 0 && f < L;
+      vp_glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + (DB ? ti & 1 : 0) * K3_XBUF + j * 1024);
+      ++issued;
+    }
+    xmk[DB ? ti & 1 : 0] = issued;
+  };
+
+  auto swap16 = [](uint32_t& x, uint32_t& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = r[0];
+    y = r[1];
+  };
+  const int ha = l16 & 6;
+  f32x4 acc[4][FN];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  struct Frag {
+    bf16x8 A[4], B[FN];
+  };
+  auto read_frag = [&](Frag& F, int ks, int tp, const char* src, int rb0) {
+    const char* pa = smem + K3_W_OFF + tp * TAPW + l16 * 128 + (((ks * 4 + g4) ^ ha) * 16);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048);
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int rb = rb0 + fn * 16;
+      F.B[fn] = *reinterpret_cast<const bf16x8*>(src + rb * 128 + (((ks * 4 + g4) ^ (rb & 6)) * 16));
+    }
+  };
+  auto mma_slice = [&](const Frag& F) {
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+    constexpr int NR = 4 + FN, NMF = 4 * FN;
+#pragma unroll
+    for (int i = 0; i < NMF; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      if (i < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    }
+  };
+  // one conv (tp0 = 0: conv1, 3: conv2): taps ascending, two K-slices each, each slice read under the previous
+  Frag F0, F1;
+  auto conv = [&](int tp0, const char* src, int rb0, int tstride) {
+    read_frag(F0, 0, tp0, src, rb0);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      read_frag(F1, 1, tp0 + t, src, rb0 + t * tstride);
+      mma_slice(F0);
+      if (t < 2) read_frag(F0, 0, tp0 + t + 1, src, rb0 + (t + 1) * tstride);
+      mma_slice(F1);
+    }
+  };
+
+  stage_x(0);
+  const float* par = reinterpret_cast<const float*>(smem + K3_PAR_OFF);
+  const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;
+  for (int ti = 0; ti < nmine; ++ti) {
+    int b, n0;
+    tile_of(ti, b, n0);
+    char* xs = smem + (DB ? ti & 1 : 0) * K3_XBUF;
+    // ---- 1. rows landed (the first wait also covers the weights); old-xs loads, then the next tile's rows
+    // into the other buffer (vmcnt retires in order); residual rows; in-place lrelu ----
+    vp_wait_vmcnt(issued - xmk[DB ? ti & 1 : 0]);
+    vp_barrier();
+    u32x4 rv[2][FN], yv[2][FN];
+    int ymk = 0;
+    if constexpr ((EF & VE_ACCUM) != 0) {
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int i = min(n0 + wave * WNC + fn * 16 + l16, L - 1);
+          asm volatile("global_load_dwordx4 %0, %1, off"
+                       : "=v"(yv[fp][fn])
+                       : "v"(a.y + ((size_t)b * L + i) * C + fp * 32 + ch16)
+                       : "memory");
+        }
+      issued += 2 * FN;
+      ymk = issued;
+    }
+    if constexpr (DB) stage_x(ti + 1);
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int r = wave * WNC + fn * 16 + l16 + HALO2 + h1;
+        const int q = fp * 4 + (g4 & 1) * 2 + (g4 >> 1);
+        rv[fp][fn] = *reinterpret_cast<const u32x4*>(xs + r * 128 + ((q ^ (r & 6)) * 16));
+      }
+    vp_barrier();
+    for (int e = tid; e < K3_XBUF / 16; e += NT) {
+      u32x4 v = *reinterpret_cast<const u32x4*>(xs + e * 16);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) v[w] = lrelu_pk(v[w], a.slope);
+      *reinterpret_cast<u32x4*>(xs + e * 16) = v;
+    }
+    vp_barrier();
+    // ---- 2. conv1 -> T ----
+    zero_acc();
+    conv(0, xs, wave * WNC + l16, d);
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int j = wave * WNC + fn * 16 + l16;
+        const int f = n0 - HALO2 + j;
+        const bool ok = f >= 0 && f < L;
+        uint32_t o[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int fm = 2 * fp + h;
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + fm * 16 + 4 * g4);
+          // lrelu(round(acc + b1)), rounded again; zero outside [0, L)
+          const uint32_t t0 = pk_bf16(f32x2{acc[fm][fn][0], acc[fm][fn][1]} + f32x2{b4[0], b4[1]});
+          const uint32_t t1 = pk_bf16(f32x2{acc[fm][fn][2], acc[fm][fn][3]} + f32x2{b4[2], b4[3]});
+          o[h][0] = ok ? lrelu_pk(t0, a.slope) : 0u;
+          o[h][1] = ok ? lrelu_pk(t1, a.slope) : 0u;
+        }
+        swap16(o[0][0], o[1][0]);
+        swap16(o[0][1], o[1][1]);
+        const int q = fp * 4 + (g4 & 1) * 2 + (g4 >> 1);
+        *reinterpret_cast<u32x4*>(smem + K3_T_OFF + j * 128 + ((q ^ (j & 6)) * 16)) =
+            u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
+      }
+    vp_barrier();  // T published (single buffer: every wave is past conv1's reads of the rows)
+    if constexpr (!DB) stage_x(ti + 1);
+    // ---- 3. conv2 -> y ----
+    zero_acc();
+    conv(3, smem + K3_T_OFF, wave * WNC + l16, 1);
+    if constexpr ((EF & VE_ACCUM) != 0) {
+      vp_wait_vmcnt(issued - ymk);
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fp][fn]));
+    }
+#pragma unroll
+    for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int i = wave * WNC + fn * 16 + l16;
+        uint32_t rx0 = rv[fp][fn][0], rx1 = rv[fp][fn][1], ry0 = rv[fp][fn][2], ry1 = rv[fp][fn][3];
+        swap16(rx0, ry0);
+        swap16(rx1, ry1);
+        uint32_t yx0 = 0, yx1 = 0, yy0 = 0, yy1 = 0;
+        if constexpr ((EF & VE_ACCUM) != 0) {
+          yx0 = yv[fp][fn][0], yx1 = yv[fp][fn][1], yy0 = yv[fp][fn][2], yy1 = yv[fp][fn][3];
+          swap16(yx0, yy0);
+          swap16(yx1, yy1);
+        }
+        uint32_t o1[2][2], o2[2][2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int fm = 2 * fp + h;
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + C + fm * 16 + 4 * g4);
+          const uint32_t rr[2] = {h ? ry0 : rx0, h ? ry1 : rx1};
+          const uint32_t yy[2] = {h ? yy0 : yx0, h ? yy1 : yx1};
+          // round(acc + b2 + x [+ xs] [/ nk]) and its lrelu, two channels per packed op
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]} + f32x2{b4[2 * u], b4[2 * u + 1]};
+            v = v + unpk_bf16(rr[u]);
+            if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
+            if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
+            o1[h][u] = pk_bf16(v);
+            o2[h][u] = lrelu_pk(o1[h][u], a.slope);
+          }
+        }
+        swap16(o1[0][0], o1[1][0]);
+        swap16(o1[0][1], o1[1][1]);
+        const bool ok = i < BN && n0 + i < L;
+        const size_t o = ((size_t)b * L + n0 + i) * C + fp * 32 + ch16;
+        *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
+        if constexpr ((EF & VE_DUAL) != 0) {
+          swap16(o2[0][0], o2[1][0]);
+          swap16(o2[0][1], o2[1][1]);
+          *reinterpret_cast<u32x4*>(ok ? a.y2 + o : a.trash + 8 * lane) = u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]};
+        }
+      }
+    issued += 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing row DMAs land before LDS is freed
 }
 
 bool vpair_supported(int C_, int k, int d) {
@@ -377,13 +623,36 @@ int launch_vpair(int ef, const VPairArgs& a, hipStream_t st) {
   MT_REQUIRE(vpair_supported(C, a.taps, a.dil) && a.taps % 2 == 1, "vpair: k %d d %d", a.taps, a.dil);
   MT_REQUIRE(!(ef & VE_DUAL) || a.y2, "vpair: y2");
   MT_REQUIRE(a.y != a.x, "vpair: y must not alias x (neighbour tiles read x's halo)");
-  const long ntiles = (long)a.B * ((a.L + BN - 1) / BN);
+  // k = 3: resident weights; MT_VPAIR3 (A/B knob, read once) picks the geometry: "2d" (default) 2 fragments per
+  // wave + double-buffered rows, "2" / "3" 2 / 3 fragments single-buffered, "0" the weight-ring kernel
+  static const int k3mode = [] {
+    const char* e = getenv("MT_VPAIR3");
+    return !e ? 1 : !strcmp(e, "0") ? 0 : !strcmp(e, "2") ? 2 : !strcmp(e, "3") ? 3 : 1;
+  }();
+  const bool k3 = a.taps == 3 && a.dil <= 8 && k3mode != 0;
+  const int bn = !k3 ? BN : k3mode == 3 ? K3G<3, false>::BN : K3G<2, true>::BN;
+  const long ntiles = (long)a.B * ((a.L + bn - 1) / bn);
   const int G = (int)std::min<long>(ntiles, vp_cu_count());
   // probe: the pair is two of the family's convs (SURVEY §8d algorithmic FLOPs and layer-boundary bytes)
   const double flops = 2.0 * 2.0 * C * C * a.taps * (double)a.B * a.L;
   const double bytes = 2.0 * (2.0 * 2.0 * C * (double)a.B * a.L) + 2.0 * 2.0 * C * C * a.taps;
   probe_begin(PROBE_VCONV, st);
-  switch (ef) {
+  if (k3) {
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(G), dim3(NT), 0, st, a); };
+#define MT_VP3(E)                                                       \
+  (k3mode == 3 ? go(vpair3_kernel<E, 3, false>) : k3mode == 2 ? go(vpair3_kernel<E, 2, false>) \
+               : go(vpair3_kernel<E, 2, true>))
+    switch (ef) {
+      case 0: MT_VP3(0); break;
+      case VE_ACCUM: MT_VP3(VE_ACCUM); break;
+      case VE_ACCUM | VE_DIV: MT_VP3(VE_ACCUM | VE_DIV); break;
+      case VE_ACCUM | VE_DIV | VE_DUAL: MT_VP3(VE_ACCUM | VE_DIV | VE_DUAL); break;
+      case VE_DIV: MT_VP3(VE_DIV); break;
+      case VE_DIV | VE_DUAL: MT_VP3(VE_DIV | VE_DUAL); break;
+      default: set_error("vpair: epilogue %d not compiled in", ef); return -1;
+    }
+#undef MT_VP3
+  } else switch (ef) {
     case 0: hipLaunchKernelGGL((vpair_kernel<0>), dim3(G), dim3(NT), 0, st, a); break;
     case VE_ACCUM: hipLaunchKernelGGL((vpair_kernel<VE_ACCUM>), dim3(G), dim3(NT), 0, st, a); break;
     case VE_ACCUM | VE_DIV: hipLaunchKernelGGL((vpair_kernel<VE_ACCUM | VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
@@ -396,7 +665,7 @@ int launch_vpair(int ef, const VPairArgs& a, hipStream_t st) {
   }
   MT_CHECK_HIP(hipGetLastError());
   probe_end(PROBE_VCONV, st, flops, bytes, PROBE_TAG_VPAIR);
-  const int rec[VCLOG_FIELDS] = {ef | 0x10000, C, BN, 0, (int)ntiles, G, a.taps, C, C, a.B, a.L};
+  const int rec[VCLOG_FIELDS] = {ef | 0x10000, C, bn, 0, (int)ntiles, G, a.taps, C, C, a.B, a.L};
   vclog_record(rec);
   return 0;
 }

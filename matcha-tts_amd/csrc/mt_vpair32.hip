@@ -138,10 +138,6 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     x = r[0];
     y = r[1];
   };
-  auto bf2 = [](uint32_t w, int i) -> float { return __uint_as_float(i ? (w & 0xffff0000u) : (w << 16)); };
-  auto pack2 = [](bf16 lo, bf16 hi) -> uint32_t {
-    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
-  };
 
   f32x4 acc[2][FN];
   auto zero_acc = [&]() __attribute__((always_inline)) {
@@ -220,8 +216,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       const int e = tid + i * NT;
       u32x4 v = *reinterpret_cast<const u32x4*>(smem + e * 16);
 #pragma unroll
-      for (int w = 0; w < 4; ++w)
-        v[w] = pack2((bf16)lrelu_f(bf2(v[w], 0), a.slope), (bf16)lrelu_f(bf2(v[w], 1), a.slope));
+      for (int w = 0; w < 4; ++w) v[w] = lrelu_pk(v[w], a.slope);
       *reinterpret_cast<u32x4*>(smem + e * 16) = v;
     }
     barrier();  // activated rows published
@@ -254,14 +249,11 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + h * 16 + 4 * g4);
-        bf16 ob[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bf16 rb = (bf16)(acc[h][fn][r] + b4[r]);
-          ob[r] = ok ? (bf16)lrelu_f((float)rb, a.slope) : (bf16)0.f;
-        }
-        o[h][0] = pack2(ob[0], ob[1]);
-        o[h][1] = pack2(ob[2], ob[3]);
+        // lrelu(round(acc + b1)), rounded again; zero outside [0, L)
+        const uint32_t t0 = pk_bf16(f32x2{acc[h][fn][0], acc[h][fn][1]} + f32x2{b4[0], b4[1]});
+        const uint32_t t1 = pk_bf16(f32x2{acc[h][fn][2], acc[h][fn][3]} + f32x2{b4[2], b4[3]});
+        o[h][0] = ok ? lrelu_pk(t0, a.slope) : 0u;
+        o[h][1] = ok ? lrelu_pk(t1, a.slope) : 0u;
       }
       swap16(o[0][0], o[1][0]);
       swap16(o[0][1], o[1][1]);
@@ -296,20 +288,16 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
         const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + C + h * 16 + 4 * g4);
         const uint32_t rr[2] = {h ? ry0 : rx0, h ? ry1 : rx1};
         const uint32_t yy[2] = {h ? yy0 : yx0, h ? yy1 : yx1};
-        bf16 ob[4], ab[4];
+        // round(acc + b2 + x [+ xs] [/ nk]) and its lrelu, two channels per packed op
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[h][fn][r] + b4[r];
-          v = v + bf2(rr[r >> 1], r & 1);
-          if constexpr ((EF & VE_ACCUM) != 0) v = bf2(yy[r >> 1], r & 1) + v;
-          if constexpr ((EF & VE_DIV) != 0) v = v / a.div;
-          ob[r] = (bf16)v;
-          ab[r] = (bf16)lrelu_f((float)ob[r], a.slope);
+        for (int u = 0; u < 2; ++u) {
+          f32x2 v = f32x2{acc[h][fn][2 * u], acc[h][fn][2 * u + 1]} + f32x2{b4[2 * u], b4[2 * u + 1]};
+          v = v + unpk_bf16(rr[u]);
+          if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
+          if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
+          o1[h][u] = pk_bf16(v);
+          o2[h][u] = lrelu_pk(o1[h][u], a.slope);
         }
-        o1[h][0] = pack2(ob[0], ob[1]);
-        o1[h][1] = pack2(ob[2], ob[3]);
-        o2[h][0] = pack2(ab[0], ab[1]);
-        o2[h][1] = pack2(ab[2], ab[3]);
       }
       swap16(o1[0][0], o1[1][0]);
       swap16(o1[0][1], o1[1][1]);

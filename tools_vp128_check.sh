@@ -8,3 +8,5 @@ export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/prof_bench.log 2>&1 || { tail $OUT/prof_bench.log; exit 1; }
 timeout -k 10 300 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench.log 2>&1 || { tail $OUT/bench.log; exit 1; }
 tail -1 $OUT/bench.log | cut -c1-400
+timeout -k 10 120 python3 tools_pair_probe.py 256 756 2 > $OUT/probe256.log 2>&1 || { tail $OUT/probe256.log; exit 1; }
+grep "launches" $OUT/probe256.log
