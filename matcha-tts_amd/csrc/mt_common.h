@@ -112,6 +112,11 @@ __device__ __forceinline__ f32x2 lrelu2(f32x2 t, float slope) {
 }
 // lrelu of the two bf16 of a packed word, rounded back (the producer-side activated copy's rounding)
 __device__ __forceinline__ uint32_t lrelu_pk(uint32_t w, float slope) { return pk_bf16(lrelu2(unpk_bf16(w), slope)); }
+// the same with the compare / select lrelu (for files built with IEEE mode on, where a max needs a canonicalize)
+__device__ __forceinline__ uint32_t lrelu_pk_sel(uint32_t w, float slope) {
+  const f32x2 t = unpk_bf16(w), m = t * slope;
+  return pk_bf16(f32x2{t.x > 0.f ? t.x : m.x, t.y > 0.f ? t.y : m.y});
+}
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + expf(-x)); }
 
 __device__ __forceinline__ float wave_sum(float v) {

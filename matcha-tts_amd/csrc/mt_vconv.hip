@@ -231,6 +231,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   // Every lane stores (frames past L go to a trash line), so the store count per tile is a constant the
   // vmcnt bookkeeping can add: NST younger VMEM operations the next steps' waits may leave in flight.
   constexpr int NST = 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+  // epilogues without per-element transcendental / statistics work run as packed fp32 pairs
+  constexpr bool PK = (EF & ~(VE_RESID | VE_ACCUM | VE_DIV | VE_ACT | VE_DUAL | VE_MASK | VE_PMASK)) == 0;
   auto bf2 = [](uint32_t w, int i) -> float { return __uint_as_float(i ? (w & 0xffff0000u) : (w << 16)); };
   auto pack2 = [](bf16 lo, bf16 hi) -> uint32_t {
     return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
@@ -331,6 +333,23 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
             bet4 = *reinterpret_cast<const f32x4*>(smem + GNP_OFF + 4 * (MMAX + m));
           }
           const uint32_t yy[2] = {h ? yy0 : yx0, h ? yy1 : yx1};
+          if constexpr (PK) {
+            // the HiFi-GAN / plain epilogues as packed fp32 pairs (same operations and order as the scalar path)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]} + f32x2{bias4[2 * u], bias4[2 * u + 1]};
+              if constexpr ((EF & VE_RESID) != 0) v = v + unpk_bf16(rr[u]);
+              if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
+              if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
+              if constexpr ((EF & VE_MASK) != 0) v = v * mk[fn];
+              if constexpr ((EF & VE_PMASK) != 0) v = v * pmk;
+              const uint32_t rb = pk_bf16(v);
+              const uint32_t av = (EF & (VE_ACT | VE_DUAL)) ? lrelu_pk_sel(rb, a.slope) : 0u;
+              o1[h][u] = (EF & VE_ACT) ? av : rb;
+              o2[h][u] = av;
+            }
+            continue;
+          }
           bf16 ob[4], ab[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {

@@ -20,6 +20,7 @@
 // and the MFMA accumulation order per output is the same (taps ascending, one 64-channel chunk, two K-slices),
 // so the results are the same bits.
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 
@@ -141,12 +142,6 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   const int ha = l16 & 6;
 
   f32x4 acc[4][FN];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
   struct Frag {
     bf16x8 A[4], B[FN];
   };
@@ -163,11 +158,13 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     }
   };
   // 4 x FN MFMAs of one K-slice with the reads of another slice interleaved, one per MFMA issue slot
-  auto mma_slice = [&](const Frag& F) {
+  // first: the conv's first K-slice starts the accumulators from the MFMA's zero C operand
+  auto mma_slice = [&](const Frag& F, auto first) {
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+      for (int fn = 0; fn < FN; ++fn)
+        acc[fm][fn] = mfma16(F.A[fm], F.B[fn], decltype(first)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn]);
     constexpr int NR = 4 + FN, NMF = 4 * FN;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
@@ -182,27 +179,30 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   Frag F0, F1;
   int s = 0;
   auto conv = [&](const char* src, int rb0, int tstride, auto&& at_first_step) {
-    for (int m = 0; m < ns; ++m, ++s) {
+    auto step = [&](int m, auto first) {
       const bool more = m + 1 < ns, two = 2 * m + 1 < k;
       vp_wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);  // this step's weights and the next step's
       vp_barrier();
       if (s + NWS - 1 < S) stage_w(s + NWS - 1);
       const int sl = s % NWS, t0 = 2 * m;
-      if (m == 0) {
+      if constexpr (decltype(first)::value) {
         at_first_step();
         read_frag(F0, 0, sl, 0, src, rb0);
       }
       read_frag(F1, 1, sl, 0, src, rb0 + t0 * tstride);
-      mma_slice(F0);
+      mma_slice(F0, first);
       if (two) {
         read_frag(F0, 0, sl, 1, src, rb0 + (t0 + 1) * tstride);
-        mma_slice(F1);
+        mma_slice(F1, std::false_type{});
         read_frag(F1, 1, sl, 1, src, rb0 + (t0 + 1) * tstride);
-        mma_slice(F0);
+        mma_slice(F0, std::false_type{});
       }
       if (more) read_frag(F0, 0, (s + 1) % NWS, 0, src, rb0 + (t0 + 2) * tstride);
-      mma_slice(F1);
-    }
+      mma_slice(F1, std::false_type{});
+    };
+    step(0, std::true_type{});
+    ++s;
+    for (int m = 1; m < ns; ++m, ++s) step(m, std::false_type{});
   };
 
   // ---- prologue ----
@@ -239,7 +239,6 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       *reinterpret_cast<u32x4*>(smem + e * 16) = v;
     }
     // ---- 2. conv1 (published by its first step's barrier) ----
-    zero_acc();
     int ymk = 0;
     conv(smem, wave * WNC + l16, d, [&] {
       // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2. Issued as asm so
@@ -286,7 +285,6 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
             u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
       }
     // ---- 3. conv2 ----
-    zero_acc();
     conv(smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, [&] {
       // every wave is past conv1's reads of the row buffer: stage the next tile's raw rows into it
       if (ti + 1 < nmine) stage_x(ti + 1);
@@ -427,12 +425,6 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   };
   const int ha = l16 & 6;
   f32x4 acc[4][FN];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
   struct Frag {
     bf16x8 A[4], B[FN];
   };
@@ -446,11 +438,13 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
       F.B[fn] = *reinterpret_cast<const bf16x8*>(src + rb * 128 + (((ks * 4 + g4) ^ (rb & 6)) * 16));
     }
   };
-  auto mma_slice = [&](const Frag& F) {
+  // first: the conv's first K-slice starts the accumulators from the MFMA's zero C operand
+  auto mma_slice = [&](const Frag& F, auto first) {
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+      for (int fn = 0; fn < FN; ++fn)
+        acc[fm][fn] = mfma16(F.A[fm], F.B[fn], decltype(first)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn]);
     constexpr int NR = 4 + FN, NMF = 4 * FN;
 #pragma unroll
     for (int i = 0; i < NMF; ++i) {
@@ -462,12 +456,16 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   Frag F0, F1;
   auto conv = [&](int tp0, const char* src, int rb0, int tstride) {
     read_frag(F0, 0, tp0, src, rb0);
+    read_frag(F1, 1, tp0, src, rb0);
+    mma_slice(F0, std::true_type{});
+    read_frag(F0, 0, tp0 + 1, src, rb0 + tstride);
+    mma_slice(F1, std::false_type{});
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
+    for (int t = 1; t < 3; ++t) {
       read_frag(F1, 1, tp0 + t, src, rb0 + t * tstride);
-      mma_slice(F0);
+      mma_slice(F0, std::false_type{});
       if (t < 2) read_frag(F0, 0, tp0 + t + 1, src, rb0 + (t + 1) * tstride);
-      mma_slice(F1);
+      mma_slice(F1, std::false_type{});
     }
   };
 
@@ -516,7 +514,6 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
     }
     vp_barrier();
     // ---- 2. conv1 -> T ----
-    zero_acc();
     conv(0, xs, wave * WNC + l16, d);
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
@@ -545,7 +542,6 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
     vp_barrier();  // T published (single buffer: every wave is past conv1's reads of the rows)
     if constexpr (!DB) stage_x(ti + 1);
     // ---- 3. conv2 -> y ----
-    zero_acc();
     conv(3, smem + K3_T_OFF, wave * WNC + l16, 1);
     if constexpr ((EF & VE_ACCUM) != 0) {
       vp_wait_vmcnt(issued - ymk);

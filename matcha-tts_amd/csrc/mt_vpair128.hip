@@ -27,6 +27,7 @@
 // with the 16-byte unit XOR-swizzled by (row & 6) (mt_vconv's conflict-free layout). conv2's discarded last
 // fragments read up to 2 h2 rows past a T plane: into the next plane / the X planes, never outside LDS.
 #include <algorithm>
+#include <type_traits>
 
 #include "mt_probe.h"
 #include "mt_vpair.h"
@@ -145,12 +146,6 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   const int ha = l16 & 6;
 
   f32x4 acc[4][FN];
-  auto zero_acc = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
   struct Frag {
     bf16x8 A[4], B[FN];
   };
@@ -166,11 +161,13 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
       F.B[fn] = *reinterpret_cast<const bf16x8*>(pl + rb * 128 + (((ks * 4 + g4) ^ (rb & 6)) * 16));
     }
   };
-  auto mma_slice = [&](const Frag& F) {
+  // first: the conv's first K-slice starts the accumulators from the MFMA's zero C operand
+  auto mma_slice = [&](const Frag& F, auto first) {
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+      for (int fn = 0; fn < FN; ++fn)
+        acc[fm][fn] = mfma16(F.A[fm], F.B[fn], decltype(first)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn]);
     constexpr int NR = 4 + FN, NMF = 4 * FN;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
@@ -185,25 +182,28 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   Frag F0, F1;
   int s = 0;
   auto conv = [&](const char* src, int pst, int rb0, int tstride, auto&& at_first_step) {
-    for (int m = 0; m < ns; ++m, ++s) {
+    auto step = [&](int m, auto first) {
       const bool more = m + 1 < ns;
       wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);  // this step's weights and the next step's
       barrier();
       if (s + NWS - 1 < S) stage_w(s + NWS - 1);
       const int sl = s % NWS;
       const int c = m >= k ? 1 : 0, t = m - c * k;
-      if (m == 0) {
+      if constexpr (decltype(first)::value) {
         at_first_step();
         read_frag(F0, 0, sl, src, rb0);
       }
       read_frag(F1, 1, sl, src + c * pst, rb0 + t * tstride);
-      mma_slice(F0);
+      mma_slice(F0, first);
       if (more) {
         const int c2 = m + 1 >= k ? 1 : 0, t2 = m + 1 - c2 * k;
         read_frag(F0, 0, (s + 1) % NWS, src + c2 * pst, rb0 + t2 * tstride);
       }
-      mma_slice(F1);
-    }
+      mma_slice(F1, std::false_type{});
+    };
+    step(0, std::true_type{});
+    ++s;
+    for (int m = 1; m < ns; ++m, ++s) step(m, std::false_type{});
   };
 
   // ---- prologue ----
@@ -239,7 +239,6 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
       *reinterpret_cast<u32x4*>(smem + X_OFF + e * 16) = v;
     }
     // ---- 2. conv1 (published by its first step's barrier) ----
-    zero_acc();
     int ymk = 0;
     conv(smem + X_OFF, XPL, wn * WNC + l16, d, [&] {
       // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2 (asm, so the
@@ -285,7 +284,6 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
             u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
       }
     // ---- 3. conv2 ----
-    zero_acc();
     conv(smem + T_OFF, TPL, wn * WNC + l16, 1, [&] {
       // every wave is past conv1's reads of the row planes: stage the next tile's raw rows into them
       if (ti + 1 < nmine) stage_x(ti + 1);

@@ -23,6 +23,7 @@
 // Rounding points and the per-output accumulation order (taps ascending, one K = 32 slice per tap) equal the
 // generic per-layer conv path's (mt_conv.hip: 32-channel chunks, taps in order), so the results are the same bits.
 #include <algorithm>
+#include <type_traits>
 
 #include "mt_probe.h"
 #include "mt_vpair.h"
@@ -140,12 +141,6 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   };
 
   f32x4 acc[2][FN];
-  auto zero_acc = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
   struct Frag {
     bf16x8 A[2], B[FN];
   };
@@ -160,12 +155,14 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       F.B[fn] = *reinterpret_cast<const bf16x8*>(src + rb * RB + ((g4 ^ swz(rb)) * 16));
     }
   };
-  // 2 x FN MFMAs of one tap with the reads of another tap interleaved, one per MFMA issue slot
-  auto mma_tap = [&](const Frag& F) __attribute__((always_inline)) {
+  // 2 x FN MFMAs of one tap with the reads of another tap interleaved, one per MFMA issue slot; the first tap of
+  // a conv starts the accumulators from the MFMA's zero C operand (no accumulator-zeroing moves)
+  auto mma_tap = [&](const Frag& F, auto first) __attribute__((always_inline)) {
 #pragma unroll
     for (int fm = 0; fm < 2; ++fm)
 #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+      for (int fn = 0; fn < FN; ++fn)
+        acc[fm][fn] = mfma16(F.A[fm], F.B[fn], decltype(first)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn]);
     constexpr int NR = 2 + FN, NMF = 2 * FN;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
@@ -179,14 +176,13 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   Frag F0, F1;
   auto conv = [&](int cv, const char* src, int rb0, int tstride) __attribute__((always_inline)) {
     read_frag(F0, cv, 0, src, rb0);
-    for (int t = 0; t < k; t += 2) {
-      const bool one = t + 1 < k, two = t + 2 < k;
-      if (one) read_frag(F1, cv, t + 1, src, rb0 + (t + 1) * tstride);
-      mma_tap(F0);
-      if (one) {
-        if (two) read_frag(F0, cv, t + 2, src, rb0 + (t + 2) * tstride);
-        mma_tap(F1);
-      }
+    read_frag(F1, cv, 1, src, rb0 + tstride);  // k >= 3 (odd)
+    mma_tap(F0, std::true_type{});
+    for (int t = 1; t < k; t += 2) {  // taps t (in F1) and t + 1 (into F0)
+      read_frag(F0, cv, t + 1, src, rb0 + (t + 1) * tstride);
+      mma_tap(F1, std::false_type{});
+      if (t + 2 < k) read_frag(F1, cv, t + 2, src, rb0 + (t + 2) * tstride);
+      mma_tap(F0, std::false_type{});
     }
   };
 
@@ -221,7 +217,6 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     }
     barrier();  // activated rows published
     // ---- 2. conv1 ----
-    zero_acc();
     int ymk = 0;
     // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2. Issued as asm so that
     // the counted wait below retires them: hipcc drains EVERY in-flight LDS-DMA (vmcnt(0)) before the use of a
@@ -262,7 +257,6 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     // ---- 3. conv2 ----
     barrier();  // T published; every wave is past conv1's reads of the row buffer: stage the next tile's rows
     stage_x(ti + 1);
-    zero_acc();
     conv(1, smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1);
     // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
     if constexpr ((EF & VE_ACCUM) != 0) {
@@ -316,7 +310,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
 }
 
 bool vpair32_supported(int k, int d) {
-  return k >= 2 && k <= KMAX && (k - 1) / 2 <= HALO2 && NF1 + d * (k - 1) <= XROWS;
+  return k >= 3 && k % 2 == 1 && k <= KMAX && (k - 1) / 2 <= HALO2 && NF1 + d * (k - 1) <= XROWS;
 }
 
 static int cu_count() {
