@@ -161,11 +161,12 @@ def _latest_profile(name):
 
 
 def roofline_by_kernel(detail):
-    """The family's launches split by kernel (mt_vconv: stages 1-2 per layer; mt_vpair / mt_vpair32: stage 3 / 4
+    """The family's launches split by kernel (mt_vconv: stage 1 and stage 2's k = 7 / 11 resblocks per layer;
+    mt_vpair128: stage 2's k = 3 resblock as fused pairs; mt_vpair / mt_vpair32: stage 3 / 4
     pairs, priced as their two convs): mean launch ms, algorithmic rate on both sides and the fraction of the
     side the kernel's own intensity bounds it by."""
     out = {}
-    for kind in ("vconv", "vpair", "vpair32", "rbfuse"):
+    for kind in ("vconv", "vpair128", "vpair", "vpair32", "rbfuse"):
         ls = [d for d in detail if d["kind"] == kind]
         if not ls:
             continue
@@ -183,10 +184,10 @@ def roofline_by_kernel(detail):
 
 def roofline(probe, default_workload=True):
     """Dominant kernel family of the step: the LDS-DMA persistent implicit-GEMM convs that run every ResBlock
-    conv of HiFi-GAN (54 launches per step): stages 1-2 per layer on mt_vconv (2 stages x 3 resblocks x 3 pairs
-    x 2 convs; C = 256/128 on B x 8/64 * T_y frames) and stages 3-4 as fused conv pairs on mt_vpair /
-    mt_vpair32 (2 x 9 launches, C = 64/32 on B x 128/256 * T_y frames; a pair launch is priced as its two
-    convs); k = 3/7/11. Timed by HIP events recorded on
+    conv of HiFi-GAN (51 launches per step): per layer on mt_vconv, stage 1 and stage 2's k = 7 / 11 resblocks
+    (30 convs; C = 256/128 on B x 8/64 * T_y frames); as fused conv pairs, stage 2's k = 3 resblock on
+    mt_vpair128 (3 launches) and stages 3-4 on mt_vpair / mt_vpair32 (2 x 9 launches, C = 64/32 on
+    B x 128/256 * T_y frames; a pair launch is priced as its two convs); k = 3/7/11. Timed by HIP events recorded on
     its launch stream around each of its launches in the LAST step of the timed region (mt_probe_*, site
     PROBE_VCONV). Per launch (SURVEY.md §8d): algorithmic FLOPs = 2 * C_out * C_in * k * B * L;
     algorithmic bytes = layer-boundary bytes 2 * B * L * (C_in + C_out) (bf16 input read once, output
@@ -221,7 +222,7 @@ def roofline(probe, default_workload=True):
             "frac": round(achieved / peak, 4), "traffic": traffic,
             "traffic_ratio": round(traffic / nbytes, 3) if traffic else None,
             "traffic_source": os.path.relpath(pmc_file, HERE) if traffic else None,
-            "kernel": "vconv_kernel<bf16> LDS-DMA implicit-GEMM conv, HiFi-GAN stage 1-4 ResBlock convs (stages 3-4 as fused pairs)",
+            "kernel": "vconv_kernel<bf16> LDS-DMA implicit-GEMM conv, HiFi-GAN stage 1-4 ResBlock convs (stage 2 k=3 and stages 3-4 as fused pairs)",
             "launches": n, "launch_ms": round(ms, 4), "flops_per_launch": flops,
             "algo_bytes_per_launch": nbytes, "intensity_flop_per_byte": round(intensity, 1),
             "tflops": round(tflops, 2), "mfma_frac": round(tflops / peak_f, 4),
