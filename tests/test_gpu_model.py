@@ -170,7 +170,9 @@ def test_vconv_stages_match_generic_per_layer(T):
     eng.set_vconv(2)
 
 
-@pytest.mark.parametrize("B,T", [(2, 37), (3, 200)])
+# (5, 200): every fused-pair kernel has more tiles than CUs (mt_vpair128 340, vpair3 505, vpair32 345), so workgroups
+# walk several tiles (cross-tile row prefetch, double buffers) under the bit-exact comparison
+@pytest.mark.parametrize("B,T", [(2, 37), (3, 200), (5, 200)])
 def test_fused_pair_stage_bit_identical_to_per_layer(B, T):
     """bf16: the 128-, 64- and 32-channel stages as fused ResBlock pairs (mt_vpair128 / mt_vpair / mt_vpair32:
     intermediate in LDS, input activation applied on chip, ping-pong chain state) reproduce the per-layer paths
