@@ -22,6 +22,8 @@
 // boundaries, so the next tile's first weights and rows land while this tile's epilogue stores.
 // Zero padding (frames outside [0, L)) is read from a zero page instead of branching.
 #include <algorithm>
+#include <climits>
+#include <cstdlib>
 
 #include "mt_probe.h"
 #include "mt_vconv.h"
@@ -42,6 +44,7 @@ struct VT {
   static constexpr int WAVES_M = BM / 64, WAVES_N = 8 / WAVES_M;
   static constexpr int WNC = TBN / WAVES_N;       // frames per wave
   static constexpr int FN = WNC / 16;             // 16-frame fragments per wave
+  static_assert(WNC % 16 == 0, "a wave covers whole 16-frame fragments");
   static constexpr int WSLOT = BM * 128;          // BM rows x 64 bf16 channels
   static constexpr int NWW = BM / 64;             // W wave-instructions per wave per step
   static constexpr int NWSLOT = K1_ ? 3 : 4;      // weight ring (NWSLOT - 1 steps in flight)
@@ -753,8 +756,23 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
 #ifndef VCONV_SMALL_MULT
 #define VCONV_SMALL_MULT 1
 #endif
-  const bool small = k1 && ntiles < (long)VCONV_SMALL_MULT * cu_count();
-  if (small) ntiles = (long)((a.L + 127) / 128) * (a.Mpad / BM);
+  // tile width by the k >= 2 convs' cost model (rounds of tiles x frames x per-frame weight 8 / 9 / 10 for 256 /
+  // 192 / 128 frames: a smaller tile amortises its fixed per-tile work over fewer frames);
+  // MT_K1_TILES=0 (A/B knob, read once): the round-2 rule (128 only when 256-frame tiles leave CUs idle)
+  static const int k1_model = [] {
+    const char* e = getenv("MT_K1_TILES");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  bool small = k1 && ntiles < (long)VCONV_SMALL_MULT * cu_count();
+  int tf1 = k1 ? (small ? 128 : BN) : 0;  // 1x1 tile frames: 256, 192 or 128
+  if (k1 && k1_model) {
+    const long cu = cu_count(), ntm = a.Mpad / BM;
+    auto cost = [&](long f, long w) { return (((long)a.L + f - 1) / f * ntm + cu - 1) / cu * f * w; };
+    const long c256 = cost(256, 8), c192 = BM == 128 ? cost(192, 9) : LONG_MAX, c128 = cost(128, 10);
+    tf1 = (c128 < c256 && c128 <= c192) ? 128 : c192 < c256 ? 192 : BN;
+    small = tf1 == 128;
+  }
+  if (k1 && tf1 != BN) ntiles = (long)((a.L + tf1 - 1) / tf1) * (a.Mpad / BM);
   // k >= 2 convs with 64-row tiles take 384 frames per tile: 1.5x the MFMAs per step barrier
   constexpr int BN64 = 384;
   if (!k1 && BM == 64) ntiles = (long)a.B * ((a.Lout + BN64 - 1) / BN64) * (a.Mpad / BM);
@@ -765,7 +783,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(!(ef & VE_GNSTATS) || a0.gn_parts == 0 || a0.gn_parts == ((a.L + tf - 1) / tf) * (8 / (BM / 64)),
              "vconv: caller expects %d GroupNorm partial slots, the launch writes a different count", a0.gn_parts);
   {
-    const int bn = k1 ? (small ? 128 : BN) : (BM == 64 ? 384 : tf);
+    const int bn = k1 ? tf1 : (BM == 64 ? 384 : tf);
     const int rec[VCLOG_FIELDS] = {ef, BM, bn, (int)k1, (int)ntiles, G, a.taps, a.M, a.cin, a.B, a.L};
     vclog_record(rec);
   }
@@ -792,9 +810,11 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
     break;
 #define MT_VCASE1(E)                                                                                    \
   case E:                                                                                               \
-    if (small) {                                                                                        \
+    if (tf1 == 128) {                                                                                   \
       if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, true, 128>), dim3(G), dim3(NT), 0, st, a); \
       else hipLaunchKernelGGL((vconv_kernel<E, 64, true, 128>), dim3(G), dim3(NT), 0, st, a);           \
+    } else if (tf1 == 192) { /* BM = 128 only (64-row tiles would give 24-frame waves) */               \
+      hipLaunchKernelGGL((vconv_kernel<E, 128, true, 192>), dim3(G), dim3(NT), 0, st, a);               \
     } else {                                                                                            \
       if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, true>), dim3(G), dim3(NT), 0, st, a);     \
       else hipLaunchKernelGGL((vconv_kernel<E, 64, true>), dim3(G), dim3(NT), 0, st, a);                \
