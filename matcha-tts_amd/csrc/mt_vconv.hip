@@ -776,6 +776,16 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   // k >= 2 convs with 64-row tiles take 384 frames per tile: 1.5x the MFMAs per step barrier
   constexpr int BN64 = 384;
   if (!k1 && BM == 64) ntiles = (long)a.B * ((a.Lout + BN64 - 1) / BN64) * (a.Mpad / BM);
+  // the text encoder's FFN conv2 (k = 3, 192 rows -> 64-row tiles) on short utterances: 128-frame tiles when the
+  // 384-frame grid leaves CUs idle (same cost model, 384-frame tiles weighted 7.5 per frame); 64-row tiles of
+  // 128 frames run one fragment per wave
+  bool bm64_128 = false;
+  if (!k1 && BM == 64 && !placed && ef == (VE_RESID | VE_MASK)) {
+    const long cu = cu_count(), ntm = a.Mpad / BM;
+    const long t384 = (long)a.B * ((a.L + 383) / 384) * ntm, t128 = (long)a.B * ((a.L + 127) / 128) * ntm;
+    bm64_128 = (t128 + cu - 1) / cu * 128 * 10 < (t384 + cu - 1) / cu * 384 * 15 / 2;
+    if (bm64_128) ntiles = t128;
+  }
   MT_REQUIRE(!(ef & VE_GNSTATS) || BM == 128, "vconv: GroupNorm partials need 128-row tiles");
   const int tf = (!k1 && !placed) ? vconv_tile_frames(a.B, a.L, a.Mpad, ef) : BN;  // 256, 192 or 128
   if (tf != BN) ntiles = (long)a.B * ((a.L + tf - 1) / tf) * (a.Mpad / BM);
@@ -783,7 +793,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(!(ef & VE_GNSTATS) || a0.gn_parts == 0 || a0.gn_parts == ((a.L + tf - 1) / tf) * (8 / (BM / 64)),
              "vconv: caller expects %d GroupNorm partial slots, the launch writes a different count", a0.gn_parts);
   {
-    const int bn = k1 ? tf1 : (BM == 64 ? 384 : tf);
+    const int bn = k1 ? tf1 : (BM == 64 ? (bm64_128 ? 128 : 384) : tf);
     const int rec[VCLOG_FIELDS] = {ef, BM, bn, (int)k1, (int)ntiles, G, a.taps, a.M, a.cin, a.B, a.L};
     vclog_record(rec);
   }
@@ -833,7 +843,11 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE(VE_DUAL)
       MT_VCASE(VE_RELU | VE_MASK)
       MT_VCASE(VE_PMASK)
-      MT_VCASE(VE_RESID | VE_MASK)
+      case VE_RESID | VE_MASK:
+        if (bm64_128) hipLaunchKernelGGL((vconv_kernel<VE_RESID | VE_MASK, 64, false, 128>), dim3(G), dim3(NT), 0, st, a);
+        else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<VE_RESID | VE_MASK, 128, false>), dim3(G), dim3(NT), 0, st, a);
+        else hipLaunchKernelGGL((vconv_kernel<VE_RESID | VE_MASK, 64, false, BN64>), dim3(G), dim3(NT), 0, st, a);
+        break;
       MT_VCASE(VE_RESID | VE_DIV | VE_DUAL)
       MT_VCASE(VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL)
       MT_VCASE(0)
