@@ -18,7 +18,9 @@
 // HBM traffic per pair: x read once (+ halo) and y written once, instead of the per-layer path's x_act read, t written and read back, x read, y and y_act written.
 // Rounding points are the per-layer path's (every stored tensor rounded to bf16, lrelu of the rounded value)
 // and the MFMA accumulation order per output is the same (taps ascending, one 64-channel chunk, two K-slices),
-// so the results are the same bits.
+// so the results are the same bits. The epilogues and the in-place lrelu pass run as packed fp32 pairs (the
+// kernels are VALU-issue-bound: DESIGN.md §4), and each conv's first K-slice starts from the MFMA's zero C
+// operand. k = 3 pairs run vpair3_kernel below (weights resident, double-buffered rows).
 #include <algorithm>
 #include <type_traits>
 #include <cstdlib>
