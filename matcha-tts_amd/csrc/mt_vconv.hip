@@ -236,6 +236,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   constexpr int NST = 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
   // epilogues without per-element transcendental / statistics work run as packed fp32 pairs
   constexpr bool PK = (EF & ~(VE_RESID | VE_ACCUM | VE_DIV | VE_ACT | VE_DUAL | VE_MASK | VE_PMASK)) == 0;
+  constexpr bool PKS = (EF & VE_LN) != 0 && (EF & ~(VE_LN | VE_LNP | VE_SNAKE)) == 0;
   auto bf2 = [](uint32_t w, int i) -> float { return __uint_as_float(i ? (w & 0xffff0000u) : (w << 16)); };
   auto pack2 = [](bf16 lo, bf16 hi) -> uint32_t {
     return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
@@ -350,6 +351,24 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
               const uint32_t av = (EF & (VE_ACT | VE_DUAL)) ? lrelu_pk_sel(rb, a.slope) : 0u;
               o1[h][u] = (EF & VE_ACT) ? av : rb;
               o2[h][u] = av;
+            }
+            continue;
+          }
+          if constexpr (PKS) {
+            // LayerNorm-folded (+ SnakeBeta) epilogues (the transformer FF1 / QKV GEMMs) as packed fp32 pairs, the
+            // same operations in the same order as the scalar path below
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]};
+              v = (v - lns[fn].x * f32x2{ws4[2 * u], ws4[2 * u + 1]}) * lns[fn].y;
+              v = v + f32x2{bias4[2 * u], bias4[2 * u + 1]};
+              if constexpr ((EF & VE_SNAKE) != 0) {
+                const f32x2 arg = v * f32x2{al4[2 * u], al4[2 * u + 1]};
+                const f32x2 sn = f32x2{__sinf(arg.x), __sinf(arg.y)};
+                v = v + f32x2{ib4[2 * u], ib4[2 * u + 1]} * (sn * sn);
+              }
+              o1[h][u] = pk_bf16(v);
+              o2[h][u] = 0u;
             }
             continue;
           }

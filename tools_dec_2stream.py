@@ -11,6 +11,9 @@ import bench
 from matcha_hip import _lib as rt
 from matcha_hip._lib import lib
 
+if __import__("os").environ.get("MT_LIB"):  # timing experiments: another build of the library
+    rt.LIB_PATH = __import__("os").environ["MT_LIB"]
+
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 728
 REPS = int(sys.argv[3]) if len(sys.argv) > 3 else 10
