@@ -1,5 +1,6 @@
 #!/bin/bash
-# vpair128 first run: bit-identity tests, then vocoder timing A/B and a kernel trace
+# Fused-pair iteration: pair bit-identity + probe tests, a traced bench, a plain bench and the per-kind ResBlock
+# launch probe at B = 256. Usage: bash tools_vp128_check.sh TAG
 OUT=gpurun_out/${1:-vp128a}
 mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "pair or probe or vconv_stages or generator" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
