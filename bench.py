@@ -8,13 +8,16 @@ collective: inference is embarrassingly parallel); a barrier +
 synchronize brackets the timed region and the MAX over ranks is reported.
 
 One step = the reference's text->wav call sequence on a batch (main.py:181-198 plus the
-notebook denoiser, MOS_audiou_generator.ipynb:277): ``MatchaTTS.synthesize`` (host-PyTorch
-text encoder, HIP duration/alignment path, HIP CFM 10-step Euler U-Net solver,
-denormalize) -> ``Generator(mel).clamp(-1, 1)`` (HIP HiFi-GAN v1) -> ``Denoiser`` (HIP).
+notebook denoiser, MOS_audiou_generator.ipynb:277): ``MatchaTTS.synthesize`` (HIP text encoder +
+duration predictor in fp32, HIP duration/alignment path, HIP CFM 10-step Euler U-Net solver in bf16,
+denormalize) -> ``Generator(mel).clamp(-1, 1)`` (HIP HiFi-GAN v1, bf16) -> ``Denoiser`` (HIP).
 Workload (configs[1] of BASELINE.json): 32 utterances/GPU, 10 ODE steps, bf16 MFMA;
 synthetic LJSpeech-shaped text (x_len ~ U[150,251] with blanks) and synthetic weights
 with the duration head forced to 3 frames/token -> 450..753 frames each.
 ``value`` = useful mel frames (sum of y_lengths) of all ranks / max-rank wall time.
+Sub-records on rank 0 at N=1 (default workload): ``north_star`` (B=256 on one GPU), ``general_attention``
+(a B=32 batch whose longest utterance is unpadded: the decoder's general attention path), ``batch1``
+(batch-1 RTF as the reference's notebook times it), ``fp32_parity_mode`` and ``cpu_baseline``.
 """
 from __future__ import annotations
 
@@ -47,6 +50,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-utterances", type=int, default=3, help="CPU baseline sample size (batch 1)")
     p.add_argument("--no-north-star", action="store_true", help="skip the B=256 single-GPU record")
+    p.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode record")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--model", default="lj", choices=["lj", "vctk"],
                    help="lj: single speaker (configs[1..2]); vctk: 109 speakers with the speaker-embedding "
@@ -295,7 +299,7 @@ def cpu_baseline(m_sd, g_sd, x, xl, n_ts, n_utt=3):
     return out
 
 
-def north_star(m, g, den, batch, seed, n_ts, denoise, steps=3, warmup=1):
+def north_star(m, g, den, batch, seed, n_ts, denoise, steps=10, warmup=2):
     """BASELINE north_star target point: B=256 utterances on ONE MI355X, 10-step text->wav, timed in this
     same run (its own warm-up; barrier-free single GPU)."""
     x_cpu, xl_cpu = shard_inputs(0, 1, batch, seed)
@@ -314,6 +318,75 @@ def north_star(m, g, den, batch, seed, n_ts, denoise, steps=3, warmup=1):
     return {"batch": batch, "steps": steps, "warmup": warmup, "ms_per_step": round(el * 1e3, 3),
             "value": round(sum(yls) / el, 2), "unit": "mel-frames/s", "seq_len": t_pad,
             "rtf": round(el / (sum(yls) * HOP / SR), 6), "path_roofline": path_roofline(el, yls, t_pad, n_ts)}
+
+
+def timed_batch(m, g, den, x, xl, n_ts, denoise, steps, warmup):
+    """mean seconds per step and the step's y_lengths, for one fixed batch already on the device"""
+    for _ in range(warmup):
+        step(m, g, den, x, xl, n_ts, denoise)
+    _, yl, _ = step(m, g, den, x, xl, n_ts, denoise)
+    yls = [int(v) for v in yl.cpu()]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(m, g, den, x, xl, n_ts, denoise)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps, yls
+
+
+def general_attention_record(m, g, den, batch, seed, n_ts, denoise, steps=10):
+    """The bench batch with its longest texts clipped to a multiple of 4 tokens (3 frames per token -> the longest
+    y_len % 4 == 0 -> T_pad = y_max, no padded frame in the longest utterance): the decoder's general Q.K^T
+    attention path at both U-Net levels instead of the query-independent one (model.py:687-700, :1281). 4 of the
+    8 shards of the 8-GPU configs[2] job are such batches (y_max 744, 744, 744, 732)."""
+    x_cpu, xl_cpu = shard_inputs(0, 1, batch, seed)
+    l4 = int(xl_cpu.max()) // 4 * 4
+    xl_cpu = xl_cpu.clamp(max=l4)
+    x_cpu = x_cpu[:, :l4].contiguous()
+    dev = m.mel_mean.device
+    el, yls = timed_batch(m, g, den, x_cpu.to(dev), xl_cpu.to(dev), n_ts, denoise, steps, 2)
+    t_pad = 4 * math.ceil(max(yls) / 4)
+    assert t_pad == max(yls)
+    return {"batch": batch, "steps": steps, "ms_per_step": round(el * 1e3, 3), "value": round(sum(yls) / el, 2),
+            "unit": "mel-frames/s", "seq_len": t_pad, "attention": "general (longest utterance unpadded)"}
+
+
+def batch1_record(m, g, den, seed, n_ts, n_utt=10, reps=3):
+    """The reference's only published number is batch-1 text->wav + denoiser RTF over 10 LJSpeech sentences
+    (0.0173 on an unnamed CUDA GPU, MOS_audiou_generator.ipynb:257; upstream Matcha package and trained
+    checkpoints, so context only): the same loop here, synchronising after every utterance as the notebook does."""
+    x_all, xl_all = shard_inputs(0, 1, n_utt, seed + 99)
+    dev = m.mel_mean.device
+    rtf, lat, frames = [], [], 0
+    for i in range(n_utt):
+        x, xl = x_all[i:i + 1, : int(xl_all[i])].to(dev), xl_all[i:i + 1].to(dev)
+        step(m, g, den, x, xl, n_ts, True)
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _, yl, wav = step(m, g, den, x, xl, n_ts, True)
+            wav.cpu()  # the notebook's .cpu() inside its timer
+            ts.append(time.perf_counter() - t0)
+        dt = sorted(ts)[len(ts) // 2]
+        n = int(yl[0])
+        frames += n
+        lat.append(dt)
+        rtf.append(dt / (n * HOP / SR))
+    return {"utterances": n_utt, "n_timesteps": n_ts, "denoiser": True, "rtf_mean": round(sum(rtf) / n_utt, 6),
+            "latency_ms_mean": round(1e3 * sum(lat) / n_utt, 3), "mel_frames_per_s": round(frames / sum(lat), 1),
+            "published_rtf_context": 0.0173,
+            "note": "median of 3 per utterance; published figure: unnamed CUDA GPU, upstream Matcha, trained weights"}
+
+
+def fp32_record(device, seed, batch, n_ts, denoise, steps=3):
+    """The parity mode (the reference's own fp32 arithmetic, exact-fp32 MFMA) on the bench workload."""
+    m, g, den, _, _ = build_models(device, "fp32", seed)
+    x_cpu, xl_cpu = shard_inputs(0, 1, batch, seed)
+    el, yls = timed_batch(m, g, den, x_cpu.to(device), xl_cpu.to(device), n_ts, denoise, steps, 1)
+    return {"batch": batch, "steps": steps, "ms_per_step": round(el * 1e3, 3), "value": round(sum(yls) / el, 2),
+            "unit": "mel-frames/s", "dtype": "fp32",
+            "ceiling_note": "fp32 MFMA 157.3 TF / 735 MFLOP per frame -> 214k frames/s (SURVEY.md §8d)"}
 
 
 def main():
@@ -395,8 +468,14 @@ def main():
             out["roofline"] = roofline(probe, default_workload=default)
             out["roofline"]["by_kernel"] = roofline_by_kernel(detail)
             out["path_roofline"] = path_roofline(el / a.steps, yls, t_pad, a.n_timesteps)
+            if default:
+                out["general_attention"] = general_attention_record(m, g, den, a.batch, a.seed, a.n_timesteps,
+                                                                    denoise)
+                out["batch1"] = batch1_record(m, g, den, a.seed, a.n_timesteps)
             if not a.no_north_star and a.batch != 256 and a.precision == "bf16" and not vctk:
                 out["north_star"] = north_star(m, g, den, 256, a.seed, a.n_timesteps, denoise)
+            if default and not a.no_fp32:
+                out["fp32_parity_mode"] = fp32_record(device, a.seed, a.batch, a.n_timesteps, denoise)
             if not a.no_cpu_baseline and not vctk:
                 out["cpu_baseline"] = cpu_baseline(msd, gsd, x_cpu, xl_cpu, a.n_timesteps, a.cpu_utterances)
         print(json.dumps(out), flush=True)

@@ -122,6 +122,11 @@ int mt_decoder_set_uniform_attention(mt_decoder* d, int enable);
  * mask is staged into the workspace first, so replays read no caller pointer. 0: direct launches. Bypassed while a
  * launch probe or the launch log is armed. Same results either way. */
 int mt_decoder_set_graphs(mt_decoder* d, int enable);
+/* Debug taps honoured by mt_decoder_step only: taps[i] (device fp32 [B,256,T_l], or NULL) receives a copy of
+ * the block output the reference fixture records with forward hooks — 0 down_blocks[0][0] (ResnetBlock1D),
+ * 1 down_blocks[0][1][0] (BasicTransformerBlock, channel-major), 2 mid_blocks[-1][1][0] (T/2), 3 up_blocks[0][2]
+ * (Upsample1D, masked), 4 up_blocks[1][1][0] (model.py:984-1043). n <= 5; NULL / n = 0 clears them. */
+int mt_decoder_set_taps(mt_decoder* d, float* const* taps, int n);
 
 size_t mt_decoder_step_workspace_bytes(const mt_decoder* d, int B, int T);
 /* one estimator evaluation: out = Decoder.forward(x, mask, mu_y, t, spks) [B,80,T] */

@@ -156,6 +156,12 @@ int mt_decoder_set_graphs(mt_decoder* d, int enable) {
   d->d.graphs = enable ? 1 : 0;
   return 0;
 }
+int mt_decoder_set_taps(mt_decoder* d, float* const* taps, int n) {
+  MT_REQUIRE(d, "null decoder");
+  MT_REQUIRE(n >= 0 && n <= mt::Decoder::N_TAPS, "decoder_set_taps: %d taps (at most %d)", n, mt::Decoder::N_TAPS);
+  for (int i = 0; i < mt::Decoder::N_TAPS; ++i) d->d.taps[i] = (taps && i < n) ? taps[i] : nullptr;
+  return 0;
+}
 size_t mt_decoder_step_workspace_bytes(const mt_decoder* d, int B, int T) {
   return d ? d->d.workspace_bytes(B, T, 1) : 0;
 }

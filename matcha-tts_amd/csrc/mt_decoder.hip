@@ -682,6 +682,11 @@ int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const fl
   return mask_out ? mask_rows(dtype, x, B * Tl, C, mask, st) : 0;
 }
 
+int Decoder::tap(const Work& w, int i, const void* src, int B, int Tl, hipStream_t st) const {
+  if (!w.taps || !w.taps[i]) return 0;
+  return btc_to_bct(dtype, src, C, 0, B, C, Tl, w.taps[i], st);
+}
+
 template <class E>
 int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Euler& eu, hipStream_t st) const {
   int rc;
@@ -723,7 +728,9 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   // down 0 @T
   const int xc = mio ? xld() : c_cond;  // input channels of the first ResnetBlock as stored
   if ((rc = resnet<E>(P, w, res[0], w.xin, nullptr, xc, xc, mio, w.H0, m0, B, T, tbp(0), &rs, st))) return rc;
+  if ((rc = tap(w, 0, w.H0, B, T, st))) return rc;
   if ((rc = tblocks(0, w.H0, m0, T))) return rc;
+  if ((rc = tap(w, 1, w.H0, B, T, st))) return rc;
   if (mio && vc(down0)) {  // frame pairs: [T][C] rows read as [T/2][2C]
     VConvArgs a = vargs(down0, P, w, w.H0, B, T1, w.XA);
     a.taps = 2;
@@ -744,6 +751,7 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
     if ((rc = resnet<E>(P, w, res[2 + i], half[cur], nullptr, C, C, mio, half[nx], m1, B, T1, tbp(2 + i), &rs, st)))
       return rc;
     if ((rc = tblocks(2 + i, half[nx], m1, T1))) return rc;
+    if (i == n_mid - 1 && (rc = tap(w, 2, half[nx], B, T1, st))) return rc;
     cur = nx;
   }
   // up 0 @T/2: cat(x, skip=H1)
@@ -772,12 +780,14 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
     } else if ((rc = plain(up0, half[nx], m1, m0, T1, w.U))) {  // ConvTranspose1d k4 s2 p1 -> T
       return rc;
     }
+    if ((rc = tap(w, 3, w.U, B, T, st))) return rc;
   }
   // up 1 @T: cat(U, skip=H0)
   {
     const int r = 3 + n_mid;
     if ((rc = resnet<E>(P, w, res[r], w.U, w.H0, C, 2 * C, mio, w.XF, m0, B, T, tbp(r), &rs, st))) return rc;
     if ((rc = tblocks(r, w.XF, m0, T))) return rc;
+    if ((rc = tap(w, 4, w.XF, B, T, st))) return rc;
     if ((rc = plain(up1, w.XF, m0, m0, T, w.U))) return rc;
   }
   // final block + projection + ODE update
@@ -977,6 +987,7 @@ int Decoder::step(const void* packed, const float* x, const float* mu_y, const f
   const char* P = (const char*)packed;
   Work w = carve(ws, B, T, 1);
   w.m0 = mask;
+  w.taps = taps;
   TimeSched ts{};
   ts.t[0] = t;
   if ((rc = time_embed(P, w, ts, 1, st))) return rc;

@@ -110,6 +110,9 @@ struct Decoder {
     // every utterance has padded frames at the full- / half-resolution level (the caller's max_valid < T /
     // <= T - 2): the transformer blocks there take the query-independent attention path
     bool uni0 = false, uni1 = false;
+    // debug taps (mt_decoder_set_taps; honoured by step() only): fp32 [B][C][T_l] copies of the block outputs
+    // the reference fixture G2 records (down0_res, down0_tb, mid1_tb, up0_out, up1_tb)
+    float* const* taps = nullptr;
   };
   Work carve(void* ws, int B, int T, int S) const;
   int time_embed(const char* P, const Work& w, const TimeSched& ts, int S, hipStream_t st,
@@ -148,6 +151,9 @@ struct Decoder {
   // launches for 10 Euler steps) as a captured hipGraph, keyed by (packed, workspace, geometry, path flags);
   // 0: launches it directly. Bypassed while a launch probe or the launch log is armed.
   int graphs = 1;
+  static constexpr int N_TAPS = 5;
+  float* taps[N_TAPS] = {};
+  int tap(const Work& w, int i, const void* src, int B, int Tl, hipStream_t st) const;
   struct GraphCache;
   mutable std::shared_ptr<GraphCache> gcache;
   // the solve's evaluation chain: time embedding + n_steps Euler / midpoint steps on stream st

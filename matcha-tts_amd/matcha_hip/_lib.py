@@ -48,6 +48,7 @@ SIGNATURES = {
                                      P]),
     "mt_decoder_set_uniform_attention": (c_int, [P, c_int]),
     "mt_decoder_set_graphs": (c_int, [P, c_int]),
+    "mt_decoder_set_taps": (c_int, [P, P, c_int]),
     "mt_decoder_step_workspace_bytes": (c_size_t, [P, c_int, c_int]),
     "mt_decoder_step": (c_int, [P, P, P, P, P, P, c_float, c_int, c_int, P, P, c_size_t, P]),
     "mt_vocoder_create": (c_int, [c_int, c_int, POINTER(c_int), POINTER(c_int), c_int, c_int,

@@ -284,6 +284,22 @@ class DecoderEngine:
                                      ws.data_ptr(), ws.numel(), stream_handle(mu_y.device)), "cfm_solve")
         return out
 
+    TAPS = ("down0_res", "down0_tb", "mid1_tb", "up0_out", "up1_tb")
+
+    def step_taps(self, packed, x, mu_y, mask, spks, t: float):
+        """One evaluation plus the block outputs of DecoderEngine.TAPS as fp32 [B,256,T_l] (mt_decoder_set_taps)."""
+        B, _, T = mu_y.shape
+        taps = [torch.empty((B, 256, T // 2 if n == "mid1_tb" else T), dtype=torch.float32, device=mu_y.device)
+                for n in self.TAPS]
+        arr = (c_void_p * len(taps))(*[t_.data_ptr() for t_ in taps])
+        check(lib().mt_decoder_set_taps(self.h, arr, len(taps)), "decoder_set_taps")
+        try:
+            out = self.step(packed, x, mu_y, mask, spks, t)
+            torch.cuda.current_stream(mu_y.device).synchronize()
+        finally:
+            check(lib().mt_decoder_set_taps(self.h, None, 0), "decoder_set_taps")
+        return out, dict(zip(self.TAPS, taps))
+
     def step(self, packed, x, mu_y, mask, spks, t: float, out=None):
         B, C, T = mu_y.shape
         out = torch.empty_like(mu_y) if out is None else out

@@ -466,8 +466,13 @@ class CFM(BASECFM):
 # ======================================================================================
 
 class MatchaTTS(nn.Module):
+    """``precision`` sets the CFM estimator ("fp32" parity mode, "bf16" performance mode). The text encoder and
+    duration predictor run in ``encoder_precision``, fp32 by default in BOTH modes: ``ceil(exp(logw))``
+    (model.py:1273-1275) flips on a 1-ulp change of logw, so the index path is only bit-exact when logw is the
+    reference's fp32 arithmetic; the encoder is < 1 % of the FLOPs."""
+
     def __init__(self, n_vocab, n_spks, spk_emb_dim, encoder_params, decoder_params, cfm_params,
-                 duration_predictor_params, precision: str = "fp32"):
+                 duration_predictor_params, precision: str = "fp32", encoder_precision: str = "fp32"):
         super().__init__()
         self.n_vocab, self.n_spks, self.spk_emb_dim = n_vocab, n_spks, spk_emb_dim
         if n_spks > 1:
@@ -475,7 +480,7 @@ class MatchaTTS(nn.Module):
         self.register_buffer("mel_mean", torch.tensor(0.0))
         self.register_buffer("mel_std", torch.tensor(1.0))
         self.encoder = TextEncoder(_get(encoder_params, "encoder_type"), encoder_params, duration_predictor_params,
-                                   n_vocab, n_spks, spk_emb_dim, precision=precision)
+                                   n_vocab, n_spks, spk_emb_dim, precision=encoder_precision)
         n_feats = _get(encoder_params, "n_feats")
         dec_in = 2 * n_feats + (spk_emb_dim if n_spks > 1 else 0)
         est = Decoder(in_channels=dec_in, out_channels=n_feats, channels=_get(decoder_params, "channels"),
@@ -487,10 +492,11 @@ class MatchaTTS(nn.Module):
         self.decoder = CFM(n_feats=n_feats, cfm_params=cfm_params, n_spks=n_spks, spk_emb_dim=spk_emb_dim,
                            estimator=est)
 
-    def set_precision(self, precision: str):
-        """'fp32' (parity mode, default) or 'bf16' (bf16 MFMA, fp32 accumulate)."""
+    def set_precision(self, precision: str, encoder_precision: str = "fp32"):
+        """Estimator: 'fp32' (parity mode, default) or 'bf16' (bf16 MFMA, fp32 accumulate). The text encoder keeps
+        fp32 unless ``encoder_precision`` says otherwise (see the class docstring)."""
         self.decoder.estimator.set_precision(precision)
-        self.encoder.set_precision(precision)
+        self.encoder.set_precision(encoder_precision)
         return self
 
     def forward(self, x, x_lengths, y, y_lengths, spks=None):

@@ -273,8 +273,11 @@ def _tblocks(sd: SD, x: Tensor, mask: Tensor, heads: int) -> Tensor:
 
 
 def decoder_forward(sd: SD, x: Tensor, mask: Tensor, mu: Tensor, t: Tensor,
-                    spks: Optional[Tensor] = None, heads: int = 2) -> Tensor:
-    """model.py:964-1048 — one velocity evaluation. sd = estimator sub-dict."""
+                    spks: Optional[Tensor] = None, heads: int = 2, taps: Optional[dict] = None) -> Tensor:
+    """model.py:964-1048 — one velocity evaluation. sd = estimator sub-dict. ``taps`` (optional dict) receives the
+    block outputs the G2 fixture records with forward hooks (tests/golden/make_golden.py): down0_res, down0_tb,
+    mid1_tb, up0_out, up1_tb, all [B,C,T_l]."""
+    taps = {} if taps is None else taps
     c_in = sd["time_mlp.linear_1.weight"].shape[1]
     temb = time_mlp(sub(sd, "time_mlp"), t, c_in)
     x = torch.cat([x, mu], dim=1)
@@ -285,7 +288,11 @@ def decoder_forward(sd: SD, x: Tensor, mask: Tensor, mu: Tensor, t: Tensor,
     for i in range(n_down):
         md = masks[-1]
         x = resnet1d(sub(sd, f"down_blocks.{i}.0"), x, md, temb)
+        if i == 0:
+            taps["down0_res"] = x
         x = _tblocks(sub(sd, f"down_blocks.{i}.1"), x, md, heads)
+        if i == 0:
+            taps["down0_tb"] = x
         hiddens.append(x)
         ds = sub(sd, f"down_blocks.{i}.2")
         if i < n_down - 1:   # Downsample1D: Conv1d k3 s2 p1 (model.py:792-798)
@@ -299,6 +306,7 @@ def decoder_forward(sd: SD, x: Tensor, mask: Tensor, mu: Tensor, t: Tensor,
     while f"mid_blocks.{i}.0.res_conv.weight" in sd:
         x = resnet1d(sub(sd, f"mid_blocks.{i}.0"), x, mm, temb)
         x = _tblocks(sub(sd, f"mid_blocks.{i}.1"), x, mm, heads)
+        taps["mid1_tb"] = x
         i += 1
     n_up = sum(1 for k in sd if k.startswith("up_blocks.") and k.endswith(".0.res_conv.weight"))
     mu_ = None
@@ -310,9 +318,13 @@ def decoder_forward(sd: SD, x: Tensor, mask: Tensor, mu: Tensor, t: Tensor,
         x = torch.cat([x, skip], dim=1)
         x = resnet1d(sub(sd, f"up_blocks.{i}.0"), x, mu_, temb)
         x = _tblocks(sub(sd, f"up_blocks.{i}.1"), x, mu_, heads)
+        if i == n_up - 1:
+            taps["up1_tb"] = x
         us = sub(sd, f"up_blocks.{i}.2")
         if i < n_up - 1:     # Upsample1D: ConvTranspose1d k4 s2 p1 (model.py:800-817)
             x = F.conv_transpose1d(x * mu_, us["conv.weight"], us["conv.bias"], stride=2, padding=1)
+            if i == 0:
+                taps["up0_out"] = x
         else:
             x = F.conv1d(x * mu_, us["weight"], us["bias"], padding=1)
     x = block1d(sub(sd, "final_block"), x, mu_)

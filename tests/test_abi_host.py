@@ -121,6 +121,10 @@ def test_synthetic_recipe_is_deterministic():
 def test_precision_switch():
     m = make_matcha(1)
     m.set_precision("bf16")
-    assert m.decoder.estimator.precision == "bf16"
+    # the text encoder / duration predictor stay fp32 in the bf16 mode: the index path is exact only on fp32 logw
+    assert m.decoder.estimator.precision == "bf16" and m.encoder.precision == "fp32"
+    m.set_precision("bf16", encoder_precision="bf16")
+    assert m.encoder.precision == "bf16"
+    assert make_matcha(1, precision="bf16").encoder.precision == "fp32"
     with pytest.raises(ValueError):
         m.set_precision("int8")

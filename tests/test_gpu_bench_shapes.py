@@ -15,10 +15,11 @@ so only grids with more tiles than CUs exercise the multi-tile walk (cross-tile 
 
 and record every mt_vconv launch (variant + grid) so the last test can assert that each variant
 the bench step launches was parity-checked here with a multi-tile grid whenever the bench runs it
-multi-tile. Tolerances: bf16 vs the fp32 oracle by relative RMS 2e-2 (the SURVEY §8c bf16 bar; the
-reference itself under autocast-bf16 is ~3e-3) on the estimator, encoder mu, generator waveform and
-on the bench rows' mel and denoised waveform (measured on MI355X: 1.0e-2, 1.1e-2, 5.5e-3, 5.7e-3 and
-9.6e-3); fp32 CFM atol 2e-4 (SURVEY §8c fp32 mode; measured 3.9e-6).
+multi-tile. Tolerances: bf16 vs the fp32 oracle by relative RMS 1e-2 (the SURVEY §8c bf16 bar) on the
+estimator, generator waveform and on the bench rows' mel and denoised waveform (measured on MI355X: 9.7e-3,
+5.5e-3, 5.7e-3 and 9.6e-3; the reference's own autocast-bf16 on the same weights: 1.1e-2 for one estimator
+evaluation, 6.6e-3 on the Generator — tests/test_gpu_parity_bf16.py); the text encoder runs fp32 in the bf16
+model (mu 1e-4); fp32 CFM atol 2e-4 (SURVEY §8c fp32 mode; measured 3.9e-6).
 Reference: model.py:964-1048, 1084-1109, 1264-1300; hifigan/models.py:181-197;
 hifigan/denoiser.py:62-68.
 """
@@ -80,7 +81,7 @@ def test_decoder_bf16_step_bench_shape_vs_oracle(B):
     worst = max(rel_rms(out[i], ref[i]) for i in range(B))
     print(f"decoder B={B} T={T}: rel-RMS {err:.3e}, worst row {worst:.3e}")
     assert torch.isfinite(out).all()
-    assert err < 2e-2 and worst < 2e-2, (err, worst)
+    assert err < 1e-2 and worst < 1e-2, (err, worst)
     gn = [r for r in LOGS[f"decoder{B}"] if r["ef"] & 256]
     # tile widths by the cost model: B=32 -> 192 (full resolution, exactly 256 tiles) and 128 (half);
     # B=128 -> 256 (full) and 192 (half), both multi-tile as at the north-star batch
@@ -90,26 +91,30 @@ def test_decoder_bf16_step_bench_shape_vs_oracle(B):
         assert all(r["ntiles"] > r["grid"] for r in gn), "GroupNorm convs must walk several tiles"
 
 
+@pytest.mark.parametrize("enc_precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("B", [32, 256])
-def test_text_encoder_bf16_bench_batch_vs_oracle(B):
-    """The bench's text batch (x_len ~ U[150,251] with blanks) through the bf16 encoder; at B=256 its
-    FFN convs run multi-tile."""
+def test_text_encoder_bench_batch_vs_oracle(B, enc_precision):
+    """The bench's text batch (x_len ~ U[150,251] with blanks) through the text encoder. fp32 is what the bf16
+    model runs (model.MatchaTTS: the index path needs the reference's fp32 logw): mu within 1e-4. bf16 is the
+    opt-in ``encoder_precision="bf16"`` mode, off the product path: its FFN convs run on mt_vconv (multi-tile at
+    B=256) and its bar is the 2e-2 this mode was built to (mu measured 1.1e-2), not the §8c contract."""
     from matcha_hip import runtime as rt
     from oracle import matcha_oracle as O
     bench = _bench()
     m, _, _, msd, _ = bench.build_models(torch.device(DEV), "bf16", 1234)
+    m.set_precision("bf16", encoder_precision=enc_precision)
     x, xl = bench.shard_inputs(0, 1, B, 1234)
     rt.vconv_log_start()
     mu, logw, xm = m.encoder(x.to(DEV), xl.to(DEV))
     torch.cuda.synchronize()
-    LOGS[f"encoder{B}"] = rt.vconv_log_stop()
+    LOGS[f"encoder{B}_{enc_precision}"] = rt.vconv_log_stop()
     sd = {k[len("encoder."):]: v.cpu() for k, v in msd.items() if k.startswith("encoder.")}
     mu_o, logw_o, xm_o = O.text_encoder(sd, x, xl, dict(n_channels=192, n_layers=6, n_heads=2, kernel_size=3,
                                                         dp_kernel_size=3, n_spks=1))
     assert torch.equal(xm.cpu(), xm_o) and torch.equal(logw.cpu(), logw_o)
     err = rel_rms(mu.cpu(), mu_o)
-    print(f"encoder B={B} Tx={x.shape[1]}: mu rel-RMS {err:.3e}")
-    assert err < 2e-2, err
+    print(f"encoder {enc_precision} B={B} Tx={x.shape[1]}: mu rel-RMS {err:.3e}")
+    assert err < (1e-4 if enc_precision == "fp32" else 2e-2), err
 
 
 # ------------------------------------------------------------------------------- (b) generator
@@ -131,7 +136,7 @@ def test_generator_bf16_bench_length_vs_oracle():
     err = rel_rms(wav, ref)
     worst = max(rel_rms(wav[i], ref[i]) for i in range(B))
     print(f"generator B={B} T={T}: rel-RMS {err:.3e}, worst row {worst:.3e}")
-    assert err < 2e-2 and worst < 2e-2, (err, worst)
+    assert err < 1e-2 and worst < 1e-2, (err, worst)
     # stage 1 + stage 2's k = 7 / 11 resblocks: 30 per-layer ResBlock convs; stage 2's k = 3 resblock: 3 fused pairs
     # (mt_vpair128); stages 3-4: 9 fused pairs each (mt_vpair / mt_vpair32); fused launches log ef | 0x10000
     res = [r for r in LOGS["generator"] if not r["k1"] and r["taps"] >= 3]
@@ -196,8 +201,8 @@ def _bench_rows_vs_oracle(batch, rows, tag, rank=0, world=1, vctk=False, n_ts=10
           f"denoised wav rel-RMS {e_wav:.3e}")
     for i, r in enumerate(rows):  # every row inside its useful length, and silence-free
         n = int(yl[r]) * 256
-        assert rel_rms(wav.cpu()[r, :n], den_ref[i, :n]) < 2e-2
-    assert e_mel < 2e-2 and e_wav < 2e-2, (e_mel, e_wav)
+        assert rel_rms(wav.cpu()[r, :n], den_ref[i, :n]) < 1e-2
+    assert e_mel < 1e-2 and e_wav < 1e-2, (e_mel, e_wav)
     return t_pad
 
 
@@ -254,7 +259,7 @@ def test_every_bench_vconv_variant_was_parity_checked():
     """Each (epilogue, tile rows, tile frames, pipeline, taps) variant the bench step launches ran in
     a WHOLE-BATCH parity test above (estimator, encoder, generator), with a multi-tile grid whenever
     the bench runs it multi-tile (the bench steps themselves are only row-checked)."""
-    whole = ("decoder32", "decoder128", "encoder32", "encoder256", "generator")
+    whole = ("decoder32", "decoder128", "encoder32_bf16", "encoder256_bf16", "generator")
     if any(k not in LOGS for k in whole + ("bench32", "bench256")):
         pytest.skip("needs the whole module's run")
     checked = {}

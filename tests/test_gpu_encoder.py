@@ -1,7 +1,9 @@
 """Text encoder + duration predictor on the MI355X (mt_encoder) against the CPU
 oracle (oracle/matcha_oracle.py:text_encoder, pinned to the reference by tests/golden/g6_*).
 
-fp32 parity mode: mu / logw max-abs <= 1e-4, x_mask exact. bf16: rel-RMS <= 2e-2.
+fp32 parity mode: mu / logw max-abs <= 1e-4, x_mask exact. This fp32 encoder is what BOTH model precisions run
+(model.MatchaTTS: the index path is exact only on fp32 logw). The opt-in encoder_precision="bf16" mode, off the
+product path, is held to the 2e-2 it was built to (measured 1.1e-2), not to the §8c contract.
 Cases: LJ (single speaker) and VCTK (spk-embedding channels), ragged lengths including a length-1
 utterance, Tx crossing the attention kernel's 64-key chunks, B = 1.
 """

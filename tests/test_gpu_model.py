@@ -1,8 +1,9 @@
 """Model-level parity of the HIP path vs golden vectors from the reference (MI355X).
 
 fp32 mode (exact-fp32 MFMA): mel / estimator output atol 1e-4, waveform atol 1e-5
-(SURVEY.md §8c tolerances); bf16 mode: rel-RMS <= 2e-2 (the reference under autocast-bf16
-is ~3e-3 from fp32); duration/index path bit-exact.
+(SURVEY.md §8c tolerances); bf16 mode: rel-RMS <= 1e-2 (the SURVEY §8c bar; the reference's own
+autocast-bf16 on the same weights drifts 1.1e-2 for one estimator evaluation and 6.6e-3 on the Generator,
+tests/test_gpu_parity_bf16.py); duration/index path bit-exact.
 """
 import numpy as np
 import pytest
@@ -73,7 +74,7 @@ def test_decoder_step_bf16_close(tag):
     spks = t(g["spks"], DEV) if g["spks"].size else None
     x, mask, mu = t(g["x"], DEV), t(g["mask"], DEV), t(g["mu"], DEV)
     out = dec(x, mask, mu, torch.zeros(2, device=DEV), spks).cpu()
-    assert rel_rms(out, t(g["out_t0"])) < 2e-2
+    assert rel_rms(out, t(g["out_t0"])) < 1e-2
 
 
 # ---------------------------------------------------------------- CFM solver (G3)
@@ -128,7 +129,7 @@ def test_generator_fp32_matches_reference(fold):
 def test_generator_bf16_close():
     g, gen = _gen("bf16", True)
     wav = gen(t(g["mel"], DEV)).cpu()
-    assert rel_rms(wav, t(g["wav"])) < 2e-2
+    assert rel_rms(wav, t(g["wav"])) < 1e-2
 
 
 @pytest.mark.parametrize("T", [16, 37, 100])
@@ -303,7 +304,7 @@ def test_decoder_per_utterance_times(precision):
     if precision == "fp32":
         assert (out - ref).abs().max() < 2e-4
     else:
-        assert rel_rms(out, ref) < 2e-2
+        assert rel_rms(out, ref) < 1e-2
     same = torch.full((B,), 0.4)
     a = dec(x.cuda(), mask.cuda(), (mu * mask).cuda(), same.cuda())
     b = dec(x.cuda(), mask.cuda(), (mu * mask).cuda(), 0.4)
@@ -365,8 +366,8 @@ def test_decoder_bf16_vconv_path_vs_generic_and_oracle(T, lens):
     # as gn_apply stored it; the fp64 merge order and FMA contraction differ, and single-ulp flips propagate
     assert rel_rms(out, sep) < 1e-2, rel_rms(out, sep)  # bf16 rounding of a few elements propagates (measured 4.9e-3)
     assert rel_rms(out, gen) < 1e-2, rel_rms(out, gen)
-    assert rel_rms(out, ref) < 2e-2, rel_rms(out, ref)
-    assert rel_rms(gen, ref) < 2e-2
+    assert rel_rms(out, ref) < 1e-2, rel_rms(out, ref)
+    assert rel_rms(gen, ref) < 1e-2
 
 
 def test_vocoder_mid_size_vs_oracle():
@@ -429,7 +430,7 @@ def test_cfm_query_independent_attention_path(lens, T):
     """mt_cfm_solve_bounded (synthesize passes y_max): when every utterance has padded frames at a U-Net level the
     reference's +3.4e38 key fill (model.py:697) makes attention the same row for every query, and the bf16 solver
     replaces Q / K / softmax / per-frame out-projection there by a masked mean + two GEMVs. Against the general
-    path (rel-RMS 1e-2, bf16 rounding; measured 3.4e-3) and the fp32 oracle (2e-2; 5.2e-3) over 4 Euler steps.
+    path (rel-RMS 1e-2, bf16 rounding; measured 3.4e-3) and the fp32 oracle (1e-2; 5.2e-3) over 4 Euler steps.
     [728, ...] has an unpadded row at full resolution AND at half resolution (mask[:, ::2] keeps frame 726), so
     max_valid = T proves nothing and the solver must take the general path (bit-identical)."""
     from oracle import matcha_oracle as O
@@ -454,7 +455,7 @@ def test_cfm_query_independent_attention_path(lens, T):
     ref = O.cfm_solve(sd, mu, mask, 4, z)
     print(f"uniform vs general {rel_rms(uni, gen):.3e}, vs oracle {rel_rms(uni, ref):.3e}")
     assert rel_rms(uni, gen) < 1e-2, rel_rms(uni, gen)
-    assert rel_rms(uni, ref) < 2e-2, rel_rms(uni, ref)
+    assert rel_rms(uni, ref) < 1e-2, rel_rms(uni, ref)
     if max(lens) < T:
         assert not torch.equal(uni, gen)  # the path was actually taken
     else:

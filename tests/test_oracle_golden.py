@@ -49,8 +49,14 @@ def test_g2_decoder_forward_and_intermediates():
         x, mask, mu = t(g["x"]), t(g["mask"]), t(g["mu"])
         for ti in range(2):
             tt = torch.full((x.shape[0],), float(g[f"t{ti}"]))
-            out = O.decoder_forward(sd, x, mask, mu, tt, spks)
+            taps = {}
+            out = O.decoder_forward(sd, x, mask, mu, tt, spks, taps=taps)
             assert (out - t(g[f"out_t{ti}"])).abs().max() < 2e-5, tag
+            if ti == 0:  # make_golden.py kept the hooks of the t0 evaluation
+                for k in ("down0_res", "down0_tb", "mid1_tb", "up0_out", "up1_tb"):
+                    ref = t(g[k])
+                    got = taps[k].transpose(1, 2) if k.endswith("_tb") else taps[k]  # hooks saw b t c there
+                    assert (got - ref).abs().max() < 2e-5, (tag, k)
         # the first resnet block alone
         temb = O.time_mlp(O.sub(sd, "time_mlp"), torch.zeros(x.shape[0]), sd["time_mlp.linear_1.weight"].shape[1])
         xin = torch.cat([x, mu] + ([spks.unsqueeze(-1).expand(-1, -1, x.shape[-1])] if spks is not None else []), 1)

@@ -1,6 +1,6 @@
 """In-process A/B timing of conv tile variants on the dominant layer shapes (GPU only)."""
 import math, sys, os, json
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "matcha-tts_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "matcha-tts_amd"))
 import torch
 from matcha_hip import runtime as rt
 

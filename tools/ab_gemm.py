@@ -1,7 +1,7 @@
 """In-process A/B of conv tile variants on the decoder's GEMM shapes (B=32, T=728; GPU only).
-Usage: python tools_ab_gemm.py [variants]"""
+Usage: python tools/ab_gemm.py [variants]"""
 import math, sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "matcha-tts_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "matcha-tts_amd"))
 import torch
 from matcha_hip import runtime as rt
 

@@ -1,6 +1,6 @@
 """A/B: the 10-step CFM solve of the bench batch (B=32, T=728) as one solve vs two half-batch solves on two
 streams (separate workspaces), to see whether the decoder's per-launch ramp / tail time overlaps.
-Usage: python tools_dec_2stream.py [B] [T] [reps]"""
+Usage: python tools/dec_2stream.py [B] [T] [reps]"""
 import ctypes
 import sys
 import time

@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """In-process A/B of the bf16 CFM decoder (10-step Euler solve): ResnetBlock / k=3 convs on mt_vconv
 vs the generic conv kernel (interleaved rounds, one process, random data, full-length rows except one).
-Usage: python tools_dec_ab.py [B] [T] [rounds] [modes, e.g. 10 or 1]"""
+Usage: python tools/dec_ab.py [B] [T] [rounds] [modes, e.g. 10 or 1]"""
 import os
 import sys
 import time
 
-HERE = os.path.dirname(os.path.abspath(__file__))
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(HERE, "matcha-tts_amd"))
 sys.path.insert(0, os.path.join(HERE, "tests"))
 import torch  # noqa: E402

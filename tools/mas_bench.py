@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """MAS timing: mt_maximum_path on a training-shaped batch (B utterances, t_x tokens, 3 frames/token
 ragged like the bench) vs the oracle restatement of the reference's Python DP on one utterance (CPU).
-Usage: python tools_mas_bench.py [B] [Tx]"""
+Usage: python tools/mas_bench.py [B] [Tx]"""
 import os
 import sys
 import time
 
-HERE = os.path.dirname(os.path.abspath(__file__))
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(HERE, "matcha-tts_amd"))
 sys.path.insert(0, HERE)
 import torch  # noqa: E402

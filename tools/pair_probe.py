@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """Per-launch times of the vocoder's fused-pair / per-layer ResBlock launches (launch probe, PROBE_VCONV) at one
 batch shape, grouped by kernel kind and kernel size k (from the probe's FLOP count), after a warm-up call.
-Env knobs are read by the library (e.g. MT_VPAIR3); PAIR sets the vocoder pair mode. Usage: python tools_pair_probe.py [B] [T] [reps]"""
+Env knobs are read by the library (e.g. MT_VPAIR3); PAIR sets the vocoder pair mode. Usage: python tools/pair_probe.py [B] [T] [reps]"""
 import os
 import sys
 from collections import defaultdict
 
-HERE = os.path.dirname(os.path.abspath(__file__))
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(HERE, "matcha-tts_amd"))
 import torch  # noqa: E402
 

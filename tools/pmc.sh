@@ -1,6 +1,6 @@
 #!/bin/bash
 # Counter passes (one rocprofv3 run per counter group; --pmc never combined with other traces).
-# Usage: bash tools_pmc.sh TAG REGEX -- cmd...
+# Usage: bash tools/pmc.sh TAG REGEX -- cmd...
 TAG=$1; RE=$2; shift 3
 mkdir -p gpurun_out/$TAG
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

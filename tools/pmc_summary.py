@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise tools_pmc.sh passes: per kernel (and launch shape), mean counters per dispatch.
-Usage: python tools_pmc_summary.py gpurun_out/TAG [kernel-substring]"""
+"""Summarise tools/pmc.sh passes: per kernel (and launch shape), mean counters per dispatch.
+Usage: python tools/pmc_summary.py gpurun_out/TAG [kernel-substring]"""
 import csv
 import glob
 import os

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Per-kernel table from tools_pmc.sh passes: launch time, XCD clock, MFMA-busy fraction, VALU / LDS instructions
+"""Per-kernel table from tools/pmc.sh passes: launch time, XCD clock, MFMA-busy fraction, VALU / LDS instructions
 per wave, HBM bytes per launch. MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
 (GRBM_GUI_ACTIVE sums the 8 XCDs' GPU-busy cycles; MFMA-busy cycles sum over every SIMD).
-Usage: python tools_pmc_table.py gpurun_out/TAG > table.txt"""
+Usage: python tools/pmc_table.py gpurun_out/TAG > table.txt"""
 import csv
 import glob
 import os

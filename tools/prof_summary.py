@@ -1,6 +1,6 @@
 """Summarise a rocprofv3 kernel-trace CSV of bench.py: one synthesis step split into its components
 (text encoder | index path | CFM decoder | vocoder | denoiser) by boundary kernels, then the top kernels.
-Usage: python tools_prof_summary.py kernel_trace.csv [TOP]"""
+Usage: python tools/prof_summary.py kernel_trace.csv [TOP]"""
 import csv
 import subprocess
 import sys

@@ -4,7 +4,7 @@
 # RESID|DUAL, RESID[|ACCUM][|DIV][|DUAL]) and the fused ResBlock pairs (vpair128_kernel, vpair_kernel, vpair3_kernel,
 # vpair32_kernel); the
 # decoder's and the upsamplers' vconv launches are excluded.
-# Usage: bash tools_round_profile.sh TAG
+# Usage: bash tools/round_profile.sh TAG
 TAG=$1
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
@@ -13,6 +13,6 @@ CMD="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-north-star"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $CMD > $OUT/trace.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "vpair(32|128|3)?_kernel|vconv_kernel(ILi(8|17|1|3|5|7|21|23)ELi[0-9]+ELb0E|<(8|17|1|3|5|7|21|23), [0-9]+, false)" -d $OUT/fetch -o pmc --output-format csv -- $CMD > $OUT/fetch.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "vpair(32|128|3)?_kernel|vconv_kernel(ILi(8|17|1|3|5|7|21|23)ELi[0-9]+ELb0E|<(8|17|1|3|5|7|21|23), [0-9]+, false)" -d $OUT/write -o pmc --output-format csv -- $CMD > $OUT/write.log 2>&1 || exit $?
-python3 tools_pmc_traffic.py $OUT/fetch/pmc_counter_collection.csv $OUT/write/pmc_counter_collection.csv \
+python3 tools/pmc_traffic.py $OUT/fetch/pmc_counter_collection.csv $OUT/write/pmc_counter_collection.csv \
   "vpair(32|128|3)?_kernel|vconv_kernel(ILi(8|17|1|3|5|7|21|23)ELi[0-9]+ELb0E|<(8|17|1|3|5|7|21|23), [0-9]+, false)" $OUT/pmc_vconv.json "$CMD" || exit $?
 echo "profile done"

@@ -2,7 +2,7 @@
 (train_standalone.py:760), LJSpeech-like lengths (mel frames ~ N(566, 150), text 150-250 tokens), synthetic
 weights and data. Prints one JSON line: ms/step, mel frames/s, peak memory, and the per-phase split.
 
-    python tools_train_bench.py [--batch 64] [--steps 5] [--warmup 2] [--no-dropout]
+    python tools/train_bench.py [--batch 64] [--steps 5] [--warmup 2] [--no-dropout]
 """
 import argparse
 import json
@@ -12,7 +12,7 @@ import time
 
 import torch
 
-ROOT = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "matcha-tts_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 

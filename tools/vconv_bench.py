@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Op-level timing of mt_vconv on the HiFi-GAN v1 stage-1/2 shapes (B=32, T=728 mel frames), weights
-packed once, interleaved rounds in one process. Usage: python tools_vconv_bench.py [rounds]"""
+packed once, interleaved rounds in one process. Usage: python tools/vconv_bench.py [rounds]"""
 import math
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "matcha-tts_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "matcha-tts_amd"))
 import torch  # noqa: E402
 
 from matcha_hip import runtime as rt  # noqa: E402

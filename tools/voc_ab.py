@@ -2,12 +2,12 @@
 """In-process A/B of the bf16 vocoder (interleaved rounds, one process, random-data mel). MODES: digits of
 vconv modes (2: per-layer vconv incl. the 64-channel stage, 1: that stage on the fused rbfuse kernel, 0: generic);
 PAIR=1 adds "p" = mode 2 with the 64-channel stage's ResBlock pairs fused (mt_vpair).
-Usage: [MODES=210] [PAIR=1] python tools_voc_ab.py [B] [T] [rounds]"""
+Usage: [MODES=210] [PAIR=1] python tools/voc_ab.py [B] [T] [rounds]"""
 import os
 import sys
 import time
 
-HERE = os.path.dirname(os.path.abspath(__file__))
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(HERE, "matcha-tts_amd"))
 import torch  # noqa: E402
 
