@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--cpu-utterances", type=int, default=3, help="CPU baseline sample size (batch 1)")
     p.add_argument("--no-north-star", action="store_true", help="skip the B=256 single-GPU record")
     p.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode record")
+    p.add_argument("--quick", action="store_true", help="headline line only: no sub-record, no CPU baseline")
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--model", default="lj", choices=["lj", "vctk"],
                    help="lj: single speaker (configs[1..2]); vctk: 109 speakers with the speaker-embedding "
@@ -468,7 +469,9 @@ def main():
             out["roofline"] = roofline(probe, default_workload=default)
             out["roofline"]["by_kernel"] = roofline_by_kernel(detail)
             out["path_roofline"] = path_roofline(el / a.steps, yls, t_pad, a.n_timesteps)
-            if default:
+            if a.quick:
+                a.no_north_star = a.no_cpu_baseline = a.no_fp32 = True
+            if default and not a.quick:
                 out["general_attention"] = general_attention_record(m, g, den, a.batch, a.seed, a.n_timesteps,
                                                                     denoise)
                 out["batch1"] = batch1_record(m, g, den, a.seed, a.n_timesteps)

@@ -67,9 +67,12 @@ int mt_encoder_param_shape(const mt_encoder* e, int i, int64_t* shape, int maxdi
 size_t mt_encoder_packed_bytes(const mt_encoder* e);
 int mt_encoder_pack(const mt_encoder* e, const float* const* params, void* packed, void* stream);
 size_t mt_encoder_workspace_bytes(const mt_encoder* e, int B, int Tx);
-/* bf16 with 96-dim heads: the self-attention core on MFMA (1, default; probabilities enter P.V as bf16) or on
- * the fp32-VALU kernel (0). */
+/* 96-dim heads: the self-attention core on MFMA (1, default; bf16: probabilities enter P.V as bf16; fp32: exact-fp32
+ * v_mfma_f32_16x16x4_f32 throughout) or on the fp32-VALU kernel (0). */
 int mt_encoder_set_mfma_attention(mt_encoder* e, int enable);
+/* fp32: 1 (default) runs the prenet / attention-projection / FFN / duration-predictor convs on mt_vconv's fp32 mode
+ * (LDS-DMA staging, exact-fp32 MFMA); 0 = the generic implicit-GEMM kernel (A/B, tests). Same arithmetic. */
+int mt_encoder_set_vconv(mt_encoder* e, int enable);
 int mt_encoder_forward(const mt_encoder* e, const void* packed, const int64_t* x, const int64_t* x_lengths,
                        const float* spks, int B, int Tx, float* mu, float* logw, float* x_mask, void* ws,
                        size_t ws_bytes, void* stream);

@@ -86,6 +86,11 @@ int mt_encoder_set_mfma_attention(mt_encoder* e, int enable) {
   e->e.mfma_attn = enable ? 1 : 0;
   return 0;
 }
+int mt_encoder_set_vconv(mt_encoder* e, int enable) {
+  MT_REQUIRE(e, "null encoder");
+  e->e.f32vc = enable ? 1 : 0;
+  return 0;
+}
 int mt_encoder_forward(const mt_encoder* e, const void* packed, const int64_t* x, const int64_t* x_lengths,
                        const float* spks, int B, int Tx, float* mu, float* logw, float* x_mask, void* ws,
                        size_t ws_bytes, void* stream) {

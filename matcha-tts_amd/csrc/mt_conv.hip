@@ -596,11 +596,12 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
   X(PF_LRELU, EF_TANH | EF_OUTF32, CFG_16 | CFG_32)                                     \
   X(PF_LRELU, EF_DUAL, CFG_BIG | CFG_SMALLN)                                            \
   X(0, EF_RESID | EF_FMASK, CFG_BIG | CFG_SMALLN | CFG_G6)                               \
-  X(PF_MASK, EF_RELU, CFG_BIG | CFG_SMALLN | CFG_C5)                                     \
-  X(PF_MASK, EF_MASK | EF_RESID, CFG_BIG | CFG_SMALLN | CFG_C5)                          \
+  X(0, EF_RELU, CFG_BIG | CFG_SMALLN | CFG_C5)                                           \
+  X(0, EF_RELU | EF_MASK, CFG_BIG | CFG_SMALLN | CFG_C5)                                 \
+  X(0, EF_MASK | EF_RESID, CFG_BIG | CFG_SMALLN | CFG_C5)                                \
   X(0, EF_MASK, CFG_BIG | CFG_SMALLN | CFG_G6)                                           \
   X(0, EF_DUAL, CFG_BIG | CFG_SMALLN)                                                    \
-  X(PF_MASK, EF_MASK | EF_OUTF32, CFG_16 | CFG_32)
+  X(0, EF_MASK | EF_OUTF32, CFG_16 | CFG_32)
 
 #define MT_DEFINE_LAUNCH(PFV, EFV, CFGV)                                                    \
   template <>                                                                             \

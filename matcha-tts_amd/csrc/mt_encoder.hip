@@ -29,8 +29,11 @@ __global__ void embed_kernel(const long long* __restrict__ ids, const long long*
   long long id = ids[row];
   id = id < 0 ? 0 : (id >= nvocab ? nvocab - 1 : id);
   const float* e = emb + (size_t)id * C;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) out[(size_t)row * C + c] = from_f<E>(e[c] * scale);
-  if (threadIdx.x == 0) xmask[row] = (long long)t < xlen[b] ? 1.f : 0.f;
+  // stored masked: every consumer reads x * x_mask (the prenet's first conv, model.py:203; its residual x_org is
+  // masked again by the prenet's final `* x_mask`, model.py:208), so no conv needs a mask prologue
+  const float m = (long long)t < xlen[b] ? 1.f : 0.f;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) out[(size_t)row * C + c] = from_f<E>(e[c] * scale * m);
+  if (threadIdx.x == 0) xmask[row] = m;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -236,6 +239,111 @@ __global__ __launch_bounds__(256) void enc_attn_mfma96_kernel(const bf16* __rest
                           ((uint32_t)__builtin_bit_cast(uint16_t, (bf16)(o[db][3] * inv)) << 16);
       *reinterpret_cast<uint2*>(dst + 16 * db) = make_uint2(w0, w1);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// The attention core in fp32 and dk = 96 on exact-fp32 MFMA (v_mfma_f32_16x16x4_f32, 4 per mfma16): the text
+// encoder runs fp32 in both model precisions (its logw drives the exact index path). Workgroup = 64 queries
+// (4 waves x 16) of one (utterance, head); key tiles of 64 through LDS.
+//   S^T = K . Q^T: A = K rows (LDS, 416-byte rows), B = this wave's Q rows (registers, loaded once). The f32
+//   MFMA's output layout (lane (g, q) holds keys 4g..4g+3 of query q) IS its B-operand layout, so the
+//   probabilities feed O^T = V^T . P^T straight from registers, with A = V^T rows (LDS, transposed at staging,
+//   288-byte rows). Both strides make every ds_read_b128 lane group conflict-free for any 16-byte offset.
+// Softmax online in fp32 over the key tiles; masked (query, key) pairs := -1e4 as the reference
+// (model.py:353-354); all-padding key tiles and query tiles skipped exactly as in enc_attn_kernel.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void enc_attn_mfma96f_kernel(const float* __restrict__ qkv,
+                                                               const float* __restrict__ xmask, float sdiv, int Tx,
+                                                               int heads, float* __restrict__ out) {
+  constexpr int DK = 96, KRS = 104, VRS = 72;  // row strides in floats
+  __shared__ __attribute__((aligned(16))) float Ks[64 * KRS];
+  __shared__ __attribute__((aligned(16))) float Vt[DK * VRS];
+  __shared__ float km[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g4 = lane >> 4, l16 = lane & 15;
+  const int h = blockIdx.y, b = blockIdx.z, t0 = blockIdx.x * 64;
+  const int W = heads * DK, ld = 3 * W;
+  const float* base = qkv + (size_t)b * Tx * ld + h * DK;
+  const int tq = t0 + 16 * wave + l16;  // this lane's query (column of S^T / O^T)
+  f32x4 qf[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+    qf[j] = *reinterpret_cast<const f32x4*>(base + (size_t)min(tq, Tx - 1) * ld + 16 * j + 4 * g4);
+  const float mq = tq < Tx ? xmask[(size_t)b * Tx + tq] : 0.f;
+  f32x4 o[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float mrun = -INFINITY, lrun = 0.f;
+  const bool any_q = __syncthreads_or(mq != 0.f);
+  for (int k0 = 0; any_q && k0 < Tx; k0 += 64) {
+    const bool kval = tid < 64 && k0 + tid < Tx && xmask[(size_t)b * Tx + k0 + tid] != 0.f;
+    if (!__syncthreads_or(kval)) continue;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {  // 64 rows x 24 chunks of 4 floats
+      const int e = tid + 256 * i, r = e / 24, c = e - r * 24;
+      const int t = k0 + r;
+      f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+      if (t < Tx) {
+        const float* src = base + (size_t)t * ld + 4 * c;
+        kv = *reinterpret_cast<const f32x4*>(src + W);
+        vv = *reinterpret_cast<const f32x4*>(src + 2 * W);
+      }
+      *reinterpret_cast<f32x4*>(Ks + r * KRS + 4 * c) = kv;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Vt[(4 * c + j) * VRS + r] = vv[j];
+    }
+    if (tid < 64) km[tid] = k0 + tid < Tx ? xmask[(size_t)b * Tx + k0 + tid] : 0.f;
+    __syncthreads();
+    f32x4 s[4];  // block kb: keys 16 kb + 4 g4 + i of query tq
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* ak = Ks + (16 * kb + l16) * KRS + 4 * g4;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) s[kb] = mfma16(*reinterpret_cast<const f32x4*>(ak + 16 * j), qf[j], s[kb]);
+    }
+    float cmax = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kk = 16 * kb + 4 * g4 + r;
+        float sc = s[kb][r] / sdiv;
+        if (mq * km[kk] == 0.f) sc = -1e4f;
+        if (k0 + kk >= Tx) sc = -INFINITY;
+        s[kb][r] = sc;
+        cmax = fmaxf(cmax, sc);
+      }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    const float mnew = fmaxf(mrun, cmax);
+    const float corr = expf(mrun - mnew);
+    lrun *= corr;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) o[i] *= corr;
+    mrun = mnew;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      f32x4 p;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[r] = expf(s[kb][r] - mnew);
+        lrun += p[r];
+      }
+#pragma unroll
+      for (int db = 0; db < 6; ++db)
+        o[db] = mfma16(*reinterpret_cast<const f32x4*>(Vt + (16 * db + l16) * VRS + 16 * kb + 4 * g4), p, o[db]);
+    }
+    __syncthreads();
+  }
+  lrun += __shfl_xor(lrun, 16, 64);
+  lrun += __shfl_xor(lrun, 32, 64);
+  if (tq < Tx) {
+    const float inv = lrun > 0.f ? 1.f / lrun : 0.f;
+    float* dst = out + ((size_t)b * Tx + tq) * W + h * DK + 4 * g4;
+#pragma unroll
+    for (int db = 0; db < 6; ++db) *reinterpret_cast<f32x4*>(dst + 16 * db) = o[db] * inv;
   }
 }
 
@@ -464,6 +572,22 @@ int Encoder::init(int n_vocab_, int n_ch, int filt, int heads_, int layers_, int
     dn1_off = pk.take(2 * DF * 4);
     dn2_off = pk.take(2 * DF * 4);
   }
+  if (dtype == F32) {
+    // fp32: every conv / projection whose shapes mt_vconv's fp32 mode takes runs there (LDS-DMA operand staging,
+    // exact-fp32 MFMA); proj_m (80 rows) and the duration head (1 row) stay on the generic kernel
+    auto vc32 = [&](GemmW& g) {
+      if (!vconv_supported_f32(g.cin, g.cout, g.k, g.s) || g.kind != 0) return;
+      g.vc = true;
+      g.v_off = pk.take(vconv_packed_bytes_f32(g.cin, g.cout, g.k));
+      if (!ezero_off) ezero_off = pk.take(256);
+    };
+    for (Pre& q : pre) vc32(q.conv);
+    if (prenet) vc32(pre_proj);
+    for (Layer& l : lay)
+      for (GemmW* g : {&l.qkv, &l.o, &l.f1, &l.f2}) vc32(*g);
+    vc32(dp1);
+    vc32(dp2);
+  }
   theta = L.add("_rope_theta", {dk / 4});  // 1 / 10000^(arange(0, dk/2, 2) / (dk/2)), host-computed
   theta_off = pk.take(dk / 4 * 4);
   packed_bytes = pk.off;
@@ -503,6 +627,17 @@ int Encoder::pack(const float* const* p, void* packed, hipStream_t st) const {
   PK(pack_vec(p[dn2g], DF, DF, 0, (float*)(P + dn2_off), st));
   PK(pack_vec(p[dn2b], DF, DF, 0, (float*)(P + dn2_off) + DF, st));
   PK(pack_vec(p[theta], dk / 4, dk / 4, 0, (float*)(P + theta_off), st));
+  if (dtype == F32) {
+    auto rp = [&](const GemmW& g) -> int {
+      return g.vc ? vconv_repack_f32(P + g.w_off, g.Mpad, g.taps, g.cin_pad, g.cin, g.cout, P + g.v_off, st) : 0;
+    };
+    for (const Pre& q : pre) PK(rp(q.conv));
+    if (prenet) PK(rp(pre_proj));
+    for (const Layer& l : lay)
+      for (const GemmW* g : {&l.qkv, &l.o, &l.f1, &l.f2}) PK(rp(*g));
+    PK(rp(dp1));
+    PK(rp(dp2));
+  }
   if (ezero_off) PK(pack_vec(nullptr, 1, 64, 0, (float*)(P + ezero_off), st));
 #undef PK
   return 0;
@@ -528,6 +663,8 @@ static int rowln(const E* x, int rows, int C, const float* gb, float eps, const 
   return 0;
 }
 
+constexpr int kNotVc = 0x7fff0001;  // v32(): the layer is not on mt_vconv's fp32 mode (run the generic kernel)
+
 template <class E>
 int Encoder::forward_t(const char* P, const long long* ids, const long long* xlen, const float* spks, int B, int Tx,
                        float* mu, float* logw, float* xmask, char* ws, hipStream_t st) const {
@@ -542,6 +679,31 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
   char* Hh = ws + 4 * big;  // FFN hidden
   char* MU = ws + 5 * big;  // [B][Tx][80]
   const float eps = 1e-4f;
+  // fp32: a conv on mt_vconv's fp32 mode (its input stored masked where the reference masks it); kNotVc = not there
+  char* trash = MU + align256(n * 80 * esize) + align256(n * 4);
+  auto v32 = [&](const GemmW& g, const void* x, void* y, int ef, const void* resid) -> int {
+    if (!(std::is_same<E, float>::value && g.vc && f32vc)) return kNotVc;
+    VConvArgs a{};
+    a.f32 = 1;
+    a.x = (const bf16*)x;
+    a.B = B;
+    a.L = Tx;
+    a.cin = g.cin;
+    a.w = (const bf16*)(P + g.v_off);
+    a.bias = (const float*)(P + g.b_off);
+    a.M = a.Mpad = g.cout;
+    a.taps = g.k;
+    a.dil = 1;
+    a.pad = g.pad;
+    a.y = (bf16*)y;
+    a.resid = (const bf16*)resid;
+    a.emask = xmask;
+    a.div = 1.f;
+    a.zero = (const bf16*)(P + ezero_off);
+    a.trash = (bf16*)trash;
+    a.probe = -1;
+    return launch_vconv(ef, a, st);
+  };
   // embedding * sqrt(C) and x_mask
   hipLaunchKernelGGL((embed_kernel<E>), dim3((unsigned)n), dim3(256), 0, st, ids, xlen, Tx, (const float*)(P + emb_off),
                      n_vocab, C, sqrtf((float)C), (E*)Q, xmask);
@@ -552,23 +714,28 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
     const char* h = Q;
     char* bufs[2] = {A, Bb};
     for (int i = 0; i < 3; ++i) {
-      ConvArgs a = gemm_args(pre[i].conv, P, B, Tx);
-      a.x0 = h;
-      a.y = Hh;
-      a.pmask = xmask;
-      if ((rc = launch_conv<E, PF_MASK, 0>(a, st))) return rc;
-      if ((rc = rowln<E>((const E*)Hh, (int)n, C, (const float*)(P + pre[i].ln_off), eps, nullptr, 1, (E*)bufs[i & 1], st)))
+      if ((rc = v32(pre[i].conv, h, Hh, 0, nullptr)) != kNotVc && rc) return rc;
+      if (rc == kNotVc) {
+        ConvArgs a = gemm_args(pre[i].conv, P, B, Tx);
+        a.x0 = h;  // h * m as stored (masked embedding / masked LN output)
+        a.y = Hh;
+        if ((rc = launch_conv<E, 0, 0>(a, st))) return rc;
+      }
+      if ((rc = rowln<E>((const E*)Hh, (int)n, C, (const float*)(P + pre[i].ln_off), eps, xmask, 1, (E*)bufs[i & 1], st)))
         return rc;
       h = bufs[i & 1];
     }
-    ConvArgs a = gemm_args(pre_proj, P, B, Tx);
-    a.x0 = h;
-    a.y = W == C ? X : Hh;
-    a.ldy = C;
-    a.resid = Q;
-    a.ldr = C;
-    a.emask = xmask;
-    if ((rc = launch_conv<E, 0, EF_RESID | EF_FMASK>(a, st))) return rc;
+    if ((rc = v32(pre_proj, h, W == C ? X : Hh, VE_RESID | VE_MASK, Q)) != kNotVc && rc) return rc;
+    if (rc == kNotVc) {
+      ConvArgs a = gemm_args(pre_proj, P, B, Tx);
+      a.x0 = h;
+      a.y = W == C ? X : Hh;
+      a.ldy = C;
+      a.resid = Q;
+      a.ldr = C;
+      a.emask = xmask;
+      if ((rc = launch_conv<E, 0, EF_RESID | EF_FMASK>(a, st))) return rc;
+    }
     cur = W == C ? X : Hh;
   }
   if (W != C) {  // ++ speaker embedding channels (model.py:526-527), x*m
@@ -584,10 +751,13 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
   const float sdiv = sqrtf((float)dk);
   for (int i = 0; i < layers; ++i) {
     const Layer& l = lay[i];
-    ConvArgs q = gemm_args(l.qkv, P, B, Tx);
-    q.x0 = X;
-    q.y = Q;
-    if ((rc = launch_conv<E, 0, 0>(q, st))) return rc;
+    if ((rc = v32(l.qkv, X, Q, 0, nullptr)) != kNotVc && rc) return rc;
+    if (rc == kNotVc) {
+      ConvArgs q = gemm_args(l.qkv, P, B, Tx);
+      q.x0 = X;
+      q.y = Q;
+      if ((rc = launch_conv<E, 0, 0>(q, st))) return rc;
+    }
     {
       const size_t pairs = n * 2 * heads * (dk / 4);
       const int blocks = (int)std::min<size_t>((pairs + 255) / 256, 65535);
@@ -599,6 +769,9 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
     if (std::is_same<E, bf16>::value && dk == 96 && mfma_attn)
       hipLaunchKernelGGL(enc_attn_mfma96_kernel, ga, dim3(256), 0, st, (const bf16*)Q, xmask, sdiv, Tx, heads,
                          (bf16*)A);
+    else if (std::is_same<E, float>::value && dk == 96 && mfma_attn)
+      hipLaunchKernelGGL(enc_attn_mfma96f_kernel, ga, dim3(256), 0, st, (const float*)Q, xmask, sdiv, Tx, heads,
+                         (float*)A);
     else if (dk == 96)
       hipLaunchKernelGGL((enc_attn_kernel<E, 96>), ga, dim3(256), 0, st, (const E*)Q, xmask, sdiv, Tx, heads, (E*)A);
     else if (dk == 128)
@@ -606,17 +779,19 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
     else
       hipLaunchKernelGGL((enc_attn_kernel<E, 64>), ga, dim3(256), 0, st, (const E*)Q, xmask, sdiv, Tx, heads, (E*)A);
     MT_CHECK_HIP(hipGetLastError());
-    ConvArgs o = gemm_args(l.o, P, B, Tx);
-    o.x0 = A;
-    o.y = Bb;
-    o.resid = X;
-    o.ldr = W;
-    if ((rc = launch_conv<E, 0, EF_RESID>(o, st))) return rc;
+    if ((rc = v32(l.o, A, Bb, VE_RESID, X)) != kNotVc && rc) return rc;
+    if (rc == kNotVc) {
+      ConvArgs o = gemm_args(l.o, P, B, Tx);
+      o.x0 = A;
+      o.y = Bb;
+      o.resid = X;
+      o.ldr = W;
+      if ((rc = launch_conv<E, 0, EF_RESID>(o, st))) return rc;
+    }
     if constexpr (std::is_same<E, bf16>::value) {
       if (l.f1.vc && l.f2.vc) {
         // FFN on vconv (model.py:119-130): LN1 stores A masked, conv 1 stores relu(.) masked, conv 2 adds the
         // residual and masks (its padded frames differ from the generic order v*m + A, and LN2 masks them)
-        char* trash = MU + align256(n * 80 * esize) + align256(n * 4);
         if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n1_off), eps, xmask, 0, (E*)A, st)))
           return rc;
         auto vargs = [&](const GemmW& g, const void* x, void* y) {
@@ -648,20 +823,29 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
         continue;
       }
     }
-    if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n1_off), eps, nullptr, 0, (E*)A, st))) return rc;
-    ConvArgs f1 = gemm_args(l.f1, P, B, Tx);
-    f1.x0 = A;
-    f1.y = Hh;
-    f1.pmask = xmask;
-    if ((rc = launch_conv<E, PF_MASK, EF_RELU>(f1, st))) return rc;
-    ConvArgs f2 = gemm_args(l.f2, P, B, Tx);
-    f2.x0 = Hh;
-    f2.y = Bb;
-    f2.pmask = xmask;
-    f2.emask = xmask;
-    f2.resid = A;
-    f2.ldr = W;
-    if ((rc = launch_conv<E, PF_MASK, EF_MASK | EF_RESID>(f2, st))) return rc;
+    // FFN (model.py:375-393) on masked operands: LN1 stores x*m, conv 1 stores relu(.)*m, conv 2 adds the
+    // (masked) residual and masks; valid frames are unchanged (the reference's unmasked residual only reaches
+    // padded frames, which LN2's mask zeroes), and no conv needs a mask prologue
+    if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n1_off), eps, xmask, 0, (E*)A, st))) return rc;
+    if ((rc = v32(l.f1, A, Hh, VE_RELU | VE_MASK, nullptr)) != kNotVc && rc) return rc;
+    if (rc == kNotVc) {
+      ConvArgs f1 = gemm_args(l.f1, P, B, Tx);
+      f1.x0 = A;
+      f1.y = Hh;
+      f1.emask = xmask;
+      if ((rc = launch_conv<E, 0, EF_RELU | EF_MASK>(f1, st))) return rc;
+    }
+    // (v + A) * m on vconv, v * m + A generic: equal, A being masked
+    if ((rc = v32(l.f2, Hh, Bb, VE_RESID | VE_MASK, A)) != kNotVc && rc) return rc;
+    if (rc == kNotVc) {
+      ConvArgs f2 = gemm_args(l.f2, P, B, Tx);
+      f2.x0 = Hh;
+      f2.y = Bb;
+      f2.emask = xmask;
+      f2.resid = A;
+      f2.ldr = W;
+      if ((rc = launch_conv<E, 0, EF_MASK | EF_RESID>(f2, st))) return rc;
+    }
     // LN2, then the next layer's (or the final) x * x_mask
     if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n2_off), eps, xmask, 0, (E*)X, st))) return rc;
   }
@@ -676,25 +860,29 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
   }
   // duration predictor on x (model.py:217-229: conv -> relu -> LN, twice, then proj(h*m)*m)
   {
-    ConvArgs a = gemm_args(dp1, P, B, Tx);
-    a.x0 = X;
-    a.y = Hh;
-    a.pmask = xmask;
-    if ((rc = launch_conv<E, PF_MASK, EF_RELU>(a, st))) return rc;
-    if ((rc = rowln<E>((const E*)Hh, (int)n, DF, (const float*)(P + dn1_off), eps, nullptr, 0, (E*)A, st))) return rc;
-    ConvArgs b = gemm_args(dp2, P, B, Tx);
-    b.x0 = A;
-    b.y = Hh;
-    b.pmask = xmask;
-    if ((rc = launch_conv<E, PF_MASK, EF_RELU>(b, st))) return rc;
-    if ((rc = rowln<E>((const E*)Hh, (int)n, DF, (const float*)(P + dn2_off), eps, nullptr, 0, (E*)A, st))) return rc;
+    // every conv input stored masked (X is x*m; the LayerNorms store LN(.)*m), so no mask prologue
+    if ((rc = v32(dp1, X, Hh, VE_RELU, nullptr)) != kNotVc && rc) return rc;
+    if (rc == kNotVc) {
+      ConvArgs a = gemm_args(dp1, P, B, Tx);
+      a.x0 = X;
+      a.y = Hh;
+      if ((rc = launch_conv<E, 0, EF_RELU>(a, st))) return rc;
+    }
+    if ((rc = rowln<E>((const E*)Hh, (int)n, DF, (const float*)(P + dn1_off), eps, xmask, 0, (E*)A, st))) return rc;
+    if ((rc = v32(dp2, A, Hh, VE_RELU, nullptr)) != kNotVc && rc) return rc;
+    if (rc == kNotVc) {
+      ConvArgs b = gemm_args(dp2, P, B, Tx);
+      b.x0 = A;
+      b.y = Hh;
+      if ((rc = launch_conv<E, 0, EF_RELU>(b, st))) return rc;
+    }
+    if ((rc = rowln<E>((const E*)Hh, (int)n, DF, (const float*)(P + dn2_off), eps, xmask, 0, (E*)A, st))) return rc;
     ConvArgs c = gemm_args(dpp, P, B, Tx);
     c.x0 = A;
     c.y = logw;
     c.ldy = 1;
-    c.pmask = xmask;
     c.emask = xmask;
-    if ((rc = launch_conv<E, PF_MASK, EF_MASK | EF_OUTF32>(c, st))) return rc;
+    if ((rc = launch_conv<E, 0, EF_MASK | EF_OUTF32>(c, st))) return rc;
   }
   return 0;
 }

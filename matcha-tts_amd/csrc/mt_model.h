@@ -175,6 +175,7 @@ struct Encoder {
   int n_vocab = 0, C = 192, F = 768, heads = 2, layers = 6, k = 3, n_spks = 1, spk_dim = 0, W = 192;
   int DF = 256, dpk = 3, prenet = 1, dtype = F32, esize = 4, dk = 96;
   int mfma_attn = 1;  // bf16, dk = 96: the attention core on MFMA (enc_attn_mfma96_kernel); 0: the fp32-VALU kernel
+  int f32vc = 1;      // fp32: convs on mt_vconv's fp32 mode (1, default) or the generic conv kernel (0; A/B, tests)
   ParamList params;
   size_t packed_bytes = 0;
   int emb = -1;

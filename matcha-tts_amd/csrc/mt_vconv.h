@@ -71,6 +71,9 @@ struct VConvArgs {
   const float* gn_gamma;     // [M]
   const float* gn_beta;      // [M]
   float gn_eps;
+  // 1: fp32 operands and output (x, w, y, resid, trash hold floats; w is the vconv_repack_f32 image); epilogues
+  // 0 / VE_RELU / VE_MASK / VE_RESID and their combinations only; one source, plain [B][L][M] output
+  int f32;
 };
 
 // LayerNorm (mean, rstd) of a 256-channel frame from its 4 slab partials (mean_i, M2_i), 64 values each,
@@ -97,6 +100,10 @@ size_t vconv_packed_bytes(int cin, int cout, int k);
 int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st,
                  int cin_src = -1);
 int launch_vconv(int ef, const VConvArgs& a, hipStream_t st);
+// fp32 mode (VConvArgs::f32): [Mpad0][taps][cin_pad] fp32 -> [cin/32][taps][Mpad][32] fp32
+bool vconv_supported_f32(int cin, int cout, int k, int stride);
+size_t vconv_packed_bytes_f32(int cin, int cout, int k);
+int vconv_repack_f32(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st);
 // image of a k = 3, stride 2, pad 1 conv (generic [Mpad0][3][cin_pad] source) as a 2-tap stride-1 conv over
 // frame pairs (2C input channels): run it with L = T/2, cin = 2C, taps = 2, pad = 1 on the same [T][C] rows
 int vconv_repack_s2(const void* src, int cin_pad, int C, int cout, void* dst, hipStream_t st);

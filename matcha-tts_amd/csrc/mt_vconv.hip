@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <type_traits>
 
 #include "mt_probe.h"
 #include "mt_vconv.h"
@@ -101,7 +102,10 @@ constexpr int vc_npar() {  // per-channel LDS tables (MMAX floats each); VE_GNRE
   return 1 + ((EF & VE_LN) ? 1 : 0) + ((EF & VE_SNAKE) ? 2 : 0) + ((EF & VE_GNRES) ? 3 : 0);
 }
 
-template <int EF, int BMT, bool K1, int BNT = BN>
+// F32: fp32 operands (the text encoder, whose duration path must be the reference's fp32 arithmetic): a 128-byte
+// LDS row holds 32 channels, one 16-byte fragment per lane feeds 4 exact-fp32 v_mfma_f32_16x16x4_f32 (mfma16), and
+// the epilogue stores fp32 in the accumulator layout (bias, ReLU, residual, mask only).
+template <int EF, int BMT, bool K1, int BNT = BN, bool F32 = false>
 __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   using TT = VT<BMT, K1, vc_npar<EF>(), BNT>;
   constexpr int BN = TT::TBN;
@@ -116,7 +120,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % TT::WAVES_M, wn = wave / TT::WAVES_M;
   const int taps = a.taps, dil = a.dil, L = a.L, cin = a.cin;
-  const int nch = cin >> 6;
+  constexpr int ES = F32 ? 4 : 2, CHR = 128 / ES;  // element bytes, channels per 128-byte row
+  const int nch = cin / CHR;
   const int S = nch * taps;
   const int ntn = (a.Lout + BN - 1) / BN, ntm = a.Mpad / BM;
   const int ntiles = a.B * ntn * ntm;
@@ -153,23 +158,24 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   // staging of one step's weights / one chunk's rows; (b, n0, m0) of the cursor's tile are kept
   // decoded by the caller (no integer division per step)
   auto issue_w = [&](int m0, int c, int t, int slot) {
-    const bf16* base = a.w + ((size_t)(c * taps + t) * a.Mpad + m0) * 64;
+    const char* base = reinterpret_cast<const char*>(a.w) + ((size_t)(c * taps + t) * a.Mpad + m0) * 128;
     char* dst = smem + slot * WSLOT;
 #pragma unroll
     for (int i = 0; i < NWW; ++i) {
       const int j = wave * NWW + i;
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
-      glds16(base + r * 64 + q * 8, dst + j * 1024);
+      glds16(base + r * 128 + q * 16, dst + j * 1024);
     }
   };
   const int R = BN + (taps - 1) * dil;
   const int c0 = a.c0;
   auto issue_x = [&](int b, int n0, int c, int buf) {
     const int f0 = n0 - a.pad;
-    const bool lo = c * 64 < c0;  // chunk from the first or the second source (skip concatenation)
+    const bool lo = c * CHR < c0;  // chunk from the first or the second source (skip concatenation)
     const int ldx = lo ? c0 : cin - c0;
-    const bf16* xb = lo ? a.x + (size_t)b * L * c0 + c * 64 : a.x1 + (size_t)b * L * (cin - c0) + (c * 64 - c0);
+    const char* xb = lo ? reinterpret_cast<const char*>(a.x) + ((size_t)b * L * c0 + c * CHR) * ES
+                        : reinterpret_cast<const char*>(a.x1) + ((size_t)b * L * (cin - c0) + (c * CHR - c0)) * ES;
     char* dst = smem + NWSLOT * WSLOT + buf * XBUF;
 #pragma unroll
     for (int i = 0; i < NXW; ++i) {
@@ -178,7 +184,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
       const bool ok = r < R && f >= 0 && f < L;
-      const bf16* src = ok ? xb + (size_t)f * ldx + q * 8 : a.zero + q * 8;
+      const char* src = ok ? xb + (size_t)f * ldx * ES + q * 16 : reinterpret_cast<const char*>(a.zero) + q * 16;
       glds16(src, dst + j * 1024);
     }
   };
@@ -204,6 +210,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   // residual / accumulator values of the tile, 16 B per lane: loaded at the start of the tile's last
   // step, consumed after its MFMAs
   u32x4 rv[2][FN], yv[2][FN];
+  f32x4 rv32[F32 ? 4 : 1][FN];  // F32: the fp32 residual of each accumulator block (4 channels of one frame)
   float2 lns[FN];  // (mean, rstd) of each fragment column's frame (VE_LN)
   f32x4 lnr[FN][2];  // VE_LNP: raw per-slab partials (s0, q0, s1, q1), (s2, q2, s3, q3)
   float mk[FN];    // frame mask of each fragment column (VE_MASK)
@@ -217,7 +224,13 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       for (int fn = 0; fn < FN; ++fn) {
         const int n = min(n0 + wn * WNC + fn * 16 + l16, L - 1);  // clamped: no per-block branch
         const size_t o = (rowbase + n) * a.M + m0 + ch16 + fp * 32;
-        if constexpr ((EF & VE_RESID) != 0) rv[fp][fn] = *reinterpret_cast<const u32x4*>(a.resid + o);
+        if constexpr (F32 && (EF & VE_RESID) != 0) {
+          const float* rp = reinterpret_cast<const float*>(a.resid) + (rowbase + n) * a.M + m0 + wm * 64 + 4 * g4;
+          rv32[2 * fp][fn] = *reinterpret_cast<const f32x4*>(rp + (2 * fp) * 16);
+          rv32[2 * fp + 1][fn] = *reinterpret_cast<const f32x4*>(rp + (2 * fp + 1) * 16);
+        } else if constexpr ((EF & VE_RESID) != 0) {
+          rv[fp][fn] = *reinterpret_cast<const u32x4*>(a.resid + o);
+        }
         if constexpr ((EF & VE_ACCUM) != 0) yv[fp][fn] = *reinterpret_cast<const u32x4*>(a.y + o);
         if constexpr ((EF & VE_LN) != 0 && (EF & VE_LNP) == 0)
           if (fp == 0) lns[fn] = *reinterpret_cast<const float2*>(a.ln_stats + 2 * (rowbase + n));
@@ -233,7 +246,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   };
   // Every lane stores (frames past L go to a trash line), so the store count per tile is a constant the
   // vmcnt bookkeeping can add: NST younger VMEM operations the next steps' waits may leave in flight.
-  constexpr int NST = 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+  constexpr int NST = F32 ? 4 * FN : 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
   // epilogues without per-element transcendental / statistics work run as packed fp32 pairs
   constexpr bool PK = (EF & ~(VE_RESID | VE_ACCUM | VE_DIV | VE_ACT | VE_DUAL | VE_MASK | VE_PMASK)) == 0;
   constexpr bool PKS = (EF & VE_LN) != 0 && (EF & ~(VE_LN | VE_LNP | VE_SNAKE)) == 0;
@@ -244,6 +257,27 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   auto epilogue = [&](int ti) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
+    if constexpr (F32) {
+      // fp32 out in the accumulator layout: lane (g4, l16) of block (fm, fn) holds channels m..m+3 of frame n, one
+      // 16-byte store (frames past L go to the trash line, so the store count stays the constant NST)
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm) {
+        const int m = m0 + wm * 64 + fm * 16 + 4 * g4;
+        const f32x4 bias4 = *reinterpret_cast<const f32x4*>(smem + BIAS_OFF + 4 * m);
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int n = n0 + wn * WNC + fn * 16 + l16;
+          f32x4 v = acc[fm][fn] + bias4;
+          if constexpr ((EF & VE_RELU) != 0)
+            v = f32x4{fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
+          if constexpr ((EF & VE_RESID) != 0) v = v + rv32[fm][fn];
+          if constexpr ((EF & VE_MASK) != 0) v = v * mk[fn];
+          float* yp = reinterpret_cast<float*>(a.y) + ((size_t)b * L + n) * a.M + m;
+          *reinterpret_cast<f32x4*>(n < L ? yp : reinterpret_cast<float*>(a.trash) + 4 * lane) = v;
+        }
+      }
+      return;
+    }
     double gs[2] = {0.0, 0.0}, gq[2] = {0.0, 0.0};  // VE_GNSTATS: this lane's sums per 32-channel group
     float rmean[FN], rm2[FN];  // VE_ROWSTATS: Welford (mean, M2) of this lane's 16 channels of frame fn
 #pragma unroll
@@ -513,8 +547,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   };
 
   // Fragments of one K-slice (ks) of a step: 4 A (weights) + 4 B (frames) x 16 bytes per lane.
+  using FT = typename std::conditional<F32, f32x4, bf16x8>::type;  // one 16-byte fragment per lane
   struct Frag {
-    bf16x8 A[4], B[FN];
+    FT A[4], B[FN];
   };
   const int ha = l16 & 6;
   auto read_frag = [&](Frag& F, int ks, int slot, int xbuf, int tap) {
@@ -524,9 +559,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     const char* pb = smem + NWSLOT * WSLOT + xbuf * XBUF + rb0 * 128;
     const int oa = ((ks * 4 + g4) ^ ha) * 16, ob = ((ks * 4 + g4) ^ hb) * 16;
 #pragma unroll
-    for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048 + oa);
+    for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const FT*>(pa + f * 2048 + oa);
 #pragma unroll
-    for (int f = 0; f < FN; ++f) F.B[f] = *reinterpret_cast<const bf16x8*>(pb + f * 2048 + ob);
+    for (int f = 0; f < FN; ++f) F.B[f] = *reinterpret_cast<const FT*>(pb + f * 2048 + ob);
   };
   // 16 MFMAs of one K-slice with the 8 reads of another slice interleaved, one per MFMA issue slot
   auto mma_slice = [&](const Frag& F) {
@@ -534,7 +569,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
-    constexpr int NR = 4 + FN, NMF = 4 * FN;  // reads of the other slice, MFMAs of this one
+    constexpr int NR = 4 + FN, NMF = (F32 ? 16 : 4) * FN;  // reads of the other slice, MFMAs of this one
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -673,6 +708,41 @@ int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int
   return 0;
 }
 
+// fp32 image [cin/32][taps][Mpad][32] (128-byte rows of 32 channels) from the generic fp32 [Mpad0][taps][cin_pad]
+__global__ void vconv_repack_f32_kernel(const float* __restrict__ src, int Mpad0, int taps, int cin_pad, int cout,
+                                        int Mpad, size_t total, float* __restrict__ dst) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int cl = (int)(i & 31);
+    size_t r = i >> 5;
+    const int m = (int)(r % Mpad);
+    r /= Mpad;
+    const int t = (int)(r % taps);
+    const int c = (int)(r / taps);
+    const int ci = c * 32 + cl;
+    dst[i] = m < cout && m < Mpad0 && ci < cin_pad ? src[((size_t)m * taps + t) * cin_pad + ci] : 0.f;
+  }
+}
+
+size_t vconv_packed_bytes_f32(int cin, int cout, int k) {
+  const int Mpad = (cout + BMP - 1) / BMP * BMP;
+  return (size_t)(cin / 32) * k * Mpad * 32 * sizeof(float);
+}
+
+int vconv_repack_f32(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st) {
+  MT_REQUIRE(cin % 32 == 0 && cin_pad >= cin, "vconv_repack_f32: cin %d", cin);
+  const int Mpad = (cout + BMP - 1) / BMP * BMP;
+  const size_t total = (size_t)(cin / 32) * taps * Mpad * 32;
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 65535);
+  hipLaunchKernelGGL(vconv_repack_f32_kernel, dim3(blocks), dim3(256), 0, st, (const float*)src, Mpad0, taps, cin_pad,
+                     cout, Mpad, total, (float*)dst);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+bool vconv_supported_f32(int cin, int cout, int k, int stride) {
+  return stride == 1 && cin % 32 == 0 && cout % 64 == 0 && cout <= MMAX && (k == 1 || BN + (k - 1) <= 320);
+}
+
 static int cu_count() {
   static int n = 0;
   if (n == 0) {
@@ -726,8 +796,67 @@ int vconv_gn_parts_max(int L) { return (L + 127) / 128 * 4; }
 // VE_GNRES: a wave's 64 (or 32) frames must span at most 8 utterances (its GN table holds 16 pairs)
 int vconv_gnres_min_frames() { return 10; }
 
+// fp32 operands (mt_encoder): one launch of the F32 kernel; tiles of BM = 128 rows when C_out % 128 == 0, else 64,
+// and 128 frames (k >= 2: 64-row tiles hold 384 / 128 frames as in bf16; 1x1: the cost model's 128 / 192 / 256)
+static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
+  MT_REQUIRE(a0.cin % 32 == 0 && a0.M % 64 == 0 && a0.Mpad == a0.M && a0.M <= MMAX && a0.c0 == 0 && !a0.Lout &&
+                 !a0.ldy && (a0.taps == 1 || BN + (a0.taps - 1) * a0.dil <= 320),
+             "vconv f32: geometry (cin %d, M %d, taps %d)", a0.cin, a0.M, a0.taps);
+  MT_REQUIRE(!(ef & VE_RESID) || a0.resid, "vconv f32: resid");
+  MT_REQUIRE(!(ef & VE_MASK) || a0.emask, "vconv f32: mask");
+  VConvArgs a = a0;
+  a.c0 = a.cin;
+  const bool k1 = a.taps == 1;
+  if (k1) {
+    MT_REQUIRE(a0.pad == 0, "vconv f32: 1x1 conv with padding");
+    a.L = a0.B * a0.L;
+    a.B = 1;
+  }
+  a.Lout = a.L;
+  a.ldy = a.M;
+  a.ylim = a.L * a.M;
+  a.ystride = (long long)a.L * a.M;
+  const int BM = a.M % 128 == 0 ? 128 : 64;
+  const long cu = cu_count(), ntm = a.Mpad / BM;
+  // frames per tile by rounds of tiles over the CUs x frames (an fp32 tile is MFMA-bound: no fixed-cost weight)
+  auto rounds = [&](long f) { return ((long)a.B * ((a.L + f - 1) / f) * ntm + cu - 1) / cu * f; };
+  int bn = 128;
+  if (BM == 128 && rounds(256) < rounds(bn)) bn = 256;
+  const long ntiles = (long)a.B * ((a.L + bn - 1) / bn) * ntm;
+  const int G = (int)std::min<long>(ntiles, cu);
+  {
+    const int rec[VCLOG_FIELDS] = {ef | (1 << 20), BM, bn, (int)k1, (int)ntiles, G, a.taps, a.M, a.cin, a.B, a.L};
+    vclog_record(rec);
+  }
+#define MT_F32CASE(E)                                                                                              \
+  case E:                                                                                                          \
+    if (k1) {                                                                                                      \
+      if (BM == 128 && bn == 256) hipLaunchKernelGGL((vconv_kernel<E, 128, true, 256, true>), dim3(G), dim3(NT), 0, st, a); \
+      else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, true, 128, true>), dim3(G), dim3(NT), 0, st, a); \
+      else hipLaunchKernelGGL((vconv_kernel<E, 64, true, 128, true>), dim3(G), dim3(NT), 0, st, a);                \
+    } else {                                                                                                       \
+      if (BM == 128 && bn == 256) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 256, true>), dim3(G), dim3(NT), 0, st, a); \
+      else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 128, true>), dim3(G), dim3(NT), 0, st, a); \
+      else hipLaunchKernelGGL((vconv_kernel<E, 64, false, 128, true>), dim3(G), dim3(NT), 0, st, a);               \
+    }                                                                                                              \
+    break;
+  switch (ef) {
+    MT_F32CASE(0)
+    MT_F32CASE(VE_RELU)
+    MT_F32CASE(VE_RELU | VE_MASK)
+    MT_F32CASE(VE_MASK)
+    MT_F32CASE(VE_RESID)
+    MT_F32CASE(VE_RESID | VE_MASK)
+    default: set_error("vconv f32: epilogue %d not compiled in", ef); return -1;
+  }
+#undef MT_F32CASE
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(a0.x && a0.w && a0.bias && a0.y && a0.zero && a0.trash, "vconv: null pointer");
+  if (a0.f32) return launch_vconv_f32(ef, a0, st);
   MT_REQUIRE(a0.B > 0 && a0.L > 0 && a0.cin % 64 == 0 && a0.M % 64 == 0 && a0.Mpad == a0.M && a0.M <= MMAX,
              "vconv: geometry");
   MT_REQUIRE(a0.taps >= 1 && a0.dil >= 1 && (a0.taps == 1 || BN + (a0.taps - 1) * a0.dil <= 320),

@@ -171,6 +171,10 @@ class EncoderEngine:
         """bf16, 96-dim heads: attention core on MFMA (1, default) or on the fp32-VALU kernel (0)."""
         check(lib().mt_encoder_set_mfma_attention(self.h, int(bool(enable))), "encoder_set_mfma_attention")
 
+    def set_vconv(self, enable) -> None:
+        """fp32: convs on mt_vconv's fp32 mode (1, default) or on the generic conv kernel (0)."""
+        check(lib().mt_encoder_set_vconv(self.h, int(bool(enable))), "encoder_set_vconv")
+
     def pack(self, params: Dict[str, torch.Tensor], device: torch.device) -> torch.Tensor:
         """params: TextEncoder-relative reference keys -> tensors."""
         tensors = []

@@ -21,7 +21,9 @@ DEV = torch.device("cuda", 0)
 
 
 def _model(n_spks, precision, seed):
+    """precision: the TEXT ENCODER's (bf16 = the opt-in encoder_precision="bf16" mode)"""
     m = make_matcha(n_spks, precision)
+    m.set_precision(precision, encoder_precision=precision)
     sd = {k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(
         [(k, tuple(v.shape)) for k, v in m.state_dict().items()], seed).items()}
     m.load_state_dict(sd)
@@ -116,3 +118,27 @@ def test_text_encoder_forced_duration_head_exact():
         _, logw, xm = m.encoder(x.to(DEV), xl.to(DEV))
         ref = torch.full_like(logw, math.log(2.5)) * xm
         assert torch.equal(logw, ref.to(torch.float32)), precision
+
+
+@pytest.mark.parametrize("name,n_spks,lengths", CASES[:3], ids=[c[0] for c in CASES[:3]])
+def test_text_encoder_fp32_vconv_matches_generic_kernel(name, n_spks, lengths):
+    """fp32: the convs on mt_vconv's fp32 mode and the attention core on exact-fp32 MFMA (defaults) against the
+    generic conv kernel and the VALU attention (mt_encoder_set_vconv(0), set_mfma_attention(0)) on the same inputs:
+    same arithmetic, different accumulation order -> within fp32 rounding (both vs the oracle in the test above)."""
+    m, sd = _model(n_spks, "fp32", 11 + n_spks)
+    x, xl = _inputs(lengths, len(lengths) * 7 + n_spks)
+    spks = torch.randn(len(lengths), 64, generator=torch.Generator().manual_seed(5)) if n_spks > 1 else None
+    args = (x.to(DEV), xl.to(DEV), None if spks is None else spks.to(DEV))
+    eng = m.encoder.engine()
+    mu1, logw1, xm1 = m.encoder(*args)
+    eng.set_vconv(0)
+    eng.set_mfma_attention(0)
+    try:
+        mu0, logw0, xm0 = m.encoder(*args)
+    finally:
+        eng.set_vconv(1)
+        eng.set_mfma_attention(1)
+    assert torch.equal(xm0, xm1)
+    e_mu, e_logw = (mu1 - mu0).abs().max().item(), (logw1 - logw0).abs().max().item()
+    print(f"{name}: fp32 vconv vs generic: mu max|d| {e_mu:.2e}, logw max|d| {e_logw:.2e}")
+    assert e_mu < 2e-5 and e_logw < 2e-5, (e_mu, e_logw)
