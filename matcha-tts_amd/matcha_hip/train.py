@@ -814,11 +814,17 @@ class MatchaTrainer:
 
     def __init__(self, state: Dict[str, torch.Tensor], hp: dict, device, lr: float = 1e-4, sigma_min: float = 1e-4,
                  prior_loss: bool = True, dropout: bool = True, grad_clip: float = 5.0, heads: int = 2,
-                 process_group=None, bucket_bytes: int = 25 << 20, seed: int = 0):
+                 process_group=None, bucket_bytes: int = 25 << 20, seed: int = 0,
+                 p_dropout: Optional[Dict[str, float]] = None):
+        """p_dropout: the configs' rates {"encoder", "duration_predictor", "decoder"} (train_standalone.py:772-800:
+        encoder_params.p_dropout, duration_predictor_params.p_dropout, decoder_params.dropout; defaults 0.1 / 0.1 /
+        0.05); the prenet's 0.5 is fixed in the reference (model.py:481). On a DDP group (world > 1) rank 0's
+        parameters are broadcast at construction, as DistributedDataParallel does when it wraps the module."""
         if int(hp.get("n_spks", 1)) > 1:
             raise NotImplementedError("multi-speaker training (spk_emb conditioning) is not built")
         names = [k for k, v in state.items() if k.startswith(("encoder.", "decoder.estimator."))
                  and torch.is_floating_point(v)]
+        self.names = names
         shapes = [(k, tuple(state[k].shape)) for k in reversed(names)]  # the backward fills the buffer in order
         dev = torch.device(device)
         self.params, self.grads = FlatBuffer(shapes, dev), FlatBuffer(shapes, dev)
@@ -827,28 +833,53 @@ class MatchaTrainer:
         self.m = torch.zeros_like(self.params.flat)
         self.v = torch.zeros_like(self.params.flat)
         self.buckets = GradBuckets(self.grads.spans, self.grads.flat, bucket_bytes, process_group)
-        self.world = self.buckets.world
+        self.world, self.group = self.buckets.world, process_group
+        if self.world > 1:  # DDP's start-up broadcast: every rank begins from rank 0's weights
+            dist.broadcast(self.params.flat, src=dist.get_global_rank(process_group, 0) if process_group else 0,
+                           group=process_group)
         enc_P = {k[len("encoder."):]: v for k, v in self.params.view.items() if k.startswith("encoder.")}
         est_P = {k[len("decoder.estimator."):]: v for k, v in self.params.view.items()
                  if k.startswith("decoder.estimator.")}
         self.enc = EncoderTrainer(enc_P, int(hp["n_layers"]), int(hp["n_heads"]))
         self.est = EstimatorTrainer(est_P, heads)
+        pd = {"encoder": 0.1, "duration_predictor": 0.1, "decoder": 0.05}
+        pd.update(p_dropout or {})
+        self.p_dropout = pd
         self.set_dropout(dropout)
         self.lr, self.sigma_min, self.prior, self.clip = lr, sigma_min, prior_loss, grad_clip
         self.step_count, self.seed = 0, seed
         self.last: Dict[str, torch.Tensor] = {}
 
     def set_dropout(self, enabled: bool):
-        """train (True: p = 0.1 encoder / 0.5 prenet / 0.1 duration predictor / 0.05 estimator, train_standalone.py:
-        775-800, model.py:481) or eval (False: identity) dropout"""
+        """train (True: the configured rates, train_standalone.py:775-800, and the prenet's fixed 0.5, model.py:481)
+        or eval (False: identity) dropout"""
         on = 1.0 if enabled else 0.0
-        self.enc.p, self.enc.p_pre, self.enc.p_dp = 0.1 * on, 0.5 * on, 0.1 * on
-        self.est.p_drop = 0.05 * on
+        pd = self.p_dropout
+        self.enc.p, self.enc.p_pre, self.enc.p_dp = pd["encoder"] * on, 0.5 * on, pd["duration_predictor"] * on
+        self.est.p_drop = pd["decoder"] * on
         self.dropout = bool(enabled)
         return self
 
     def parameters(self) -> Dict[str, torch.Tensor]:
         return dict(self.params.view)
+
+    @torch.no_grad()
+    def load_parameters(self, state: Dict[str, torch.Tensor]):
+        """overwrite the flat parameters from reference-named tensors (a checkpoint loaded into the module);
+        the Adam moments and the step count are kept"""
+        for k in self.names:
+            self.params.view[k].copy_(state[k].detach().to(device=self.params.flat.device, dtype=torch.float32))
+
+    def optimizer_state(self) -> Dict[str, object]:
+        """Adam's exp_avg / exp_avg_sq (flat, parameter order of ``self.grads.names``), step count and lr"""
+        return {"exp_avg": self.m, "exp_avg_sq": self.v, "step": self.step_count, "lr": self.lr}
+
+    @torch.no_grad()
+    def load_optimizer_state(self, st: Dict[str, object]):
+        self.m.copy_(st["exp_avg"])
+        self.v.copy_(st["exp_avg_sq"])
+        self.step_count = int(st["step"])
+        self.lr = float(st.get("lr", self.lr))
 
     def gradients(self) -> Dict[str, torch.Tensor]:
         return dict(self.grads.view)
@@ -861,6 +892,10 @@ class MatchaTrainer:
         gradients in the flat buffer; returns the losses as device scalars. backward=False: losses only
         (validation_step)."""
         rt.require_gpu(x, y, what="MatchaTrainer")
+        lo, hi = (int(v) for v in torch.aminmax(x))  # nn.Embedding raises on an out-of-vocabulary id
+        n_vocab = self.params.view["encoder.emb.weight"].shape[0]
+        if lo < 0 or hi >= n_vocab:
+            raise IndexError(f"token id out of range [0, {n_vocab}): min {lo}, max {hi}")
         B, Tx = x.shape
         F, Ty = y.shape[1], y.shape[2]
         if Ty % 4:

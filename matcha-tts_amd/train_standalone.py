@@ -22,6 +22,7 @@ from __future__ import annotations
 from typing import Optional
 
 import torch
+import torch.distributed as dist
 
 import model as _model
 from hifigan.meldataset import mel_spectrogram, normalize  # noqa: F401  (train_standalone.py:164-224)
@@ -46,11 +47,15 @@ def _get(p, k, default=None):
 
 class _FusedAdam:
     """configure_optimizers' Adam(lr) with Lightning's gradient_clip_val = 5.0 folded in: one clip-factor kernel
-    and one Adam kernel over the flat parameter buffer."""
+    and one Adam kernel over the flat parameter buffer. ``state_dict`` / ``load_state_dict`` use torch.optim.Adam's
+    format over ``module.parameters()`` (per-parameter exp_avg / exp_avg_sq / step), so a resumed run continues with
+    the moments and the step count it saved."""
 
     def __init__(self, module: "MatchaLightningModule"):
         self.module = module
-        self.param_groups = [{"lr": module.learning_rate, "betas": (0.9, 0.999), "eps": 1e-8, "weight_decay": 0}]
+        self.param_groups = [{"lr": module.learning_rate, "betas": (0.9, 0.999), "eps": 1e-8, "weight_decay": 0,
+                              "amsgrad": False, "maximize": False}]
+        self._pending = None  # a loaded state not yet applied (the trainer is built on first use)
 
     def step(self, closure=None):
         if closure is not None:
@@ -62,6 +67,50 @@ class _FusedAdam:
 
     def zero_grad(self, set_to_none: bool = True):
         pass  # every backward overwrites the whole flat gradient buffer
+
+    def _index(self):
+        """module.parameters() order -> trainer parameter name (the reference's Adam state is keyed by it)"""
+        names = [n for n, _ in self.module.named_parameters()]
+        return [n[len("model."):] if n.startswith("model.") else n for n in names]
+
+    def state_dict(self):
+        tr = self.module.trainer()
+        st = tr.optimizer_state()
+        m_view = {n: st["exp_avg"][o:o + k] for n, o, k in tr.grads.spans}
+        v_view = {n: st["exp_avg_sq"][o:o + k] for n, o, k in tr.grads.spans}
+        state = {}
+        for i, n in enumerate(self._index()):
+            if n in m_view and st["step"] > 0:
+                shape = tr.params.view[n].shape
+                state[i] = {"step": torch.tensor(float(st["step"])), "exp_avg": m_view[n].view(shape).clone(),
+                            "exp_avg_sq": v_view[n].view(shape).clone()}
+        groups = [dict(self.param_groups[0], params=list(range(len(self._index()))))]
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, sd):
+        """applied to the training engine before its next use (it is built on the device on first use)"""
+        self.param_groups[0].update({k: v for k, v in sd["param_groups"][0].items() if k != "params"})
+        self._pending = sd
+        self.module._pending_opt = self
+
+    @torch.no_grad()
+    def _apply_pending(self, tr):
+        if self._pending is None:
+            return
+        sd, self._pending = self._pending, None
+        m, v = torch.zeros_like(tr.m), torch.zeros_like(tr.v)
+        spans = {n: (o, k) for n, o, k in tr.grads.spans}
+        step = 0
+        for i, n in enumerate(self._index()):
+            st = sd["state"].get(i) if isinstance(sd["state"], dict) else None
+            if st is None or n not in spans:
+                continue
+            o, k = spans[n]
+            m[o:o + k].copy_(st["exp_avg"].reshape(-1))
+            v[o:o + k].copy_(st["exp_avg_sq"].reshape(-1))
+            step = int(float(st["step"]))
+        tr.load_optimizer_state({"exp_avg": m, "exp_avg_sq": v, "step": step,
+                                 "lr": self.param_groups[0]["lr"]})
 
 
 class MatchaLightningModule(torch.nn.Module):
@@ -77,6 +126,10 @@ class MatchaLightningModule(torch.nn.Module):
         self.learning_rate, self.n_vocab, self.n_spks = learning_rate, n_vocab, n_spks
         self.n_feats = _get(encoder_params, "n_feats")
         self.prior_loss = prior_loss
+        # dropout rates of the configs (train_standalone.py:772-800); the prenet's 0.5 is fixed (model.py:481)
+        self.p_dropout = {"encoder": float(_get(encoder_params, "p_dropout", 0.1)),
+                          "duration_predictor": float(_get(duration_predictor_params, "p_dropout", 0.1)),
+                          "decoder": float(_get(decoder_params, "dropout", 0.05))}
         self.hp = {"n_layers": _get(encoder_params, "n_layers"), "n_heads": _get(encoder_params, "n_heads"),
                    "n_spks": n_spks}
         self.heads = _get(decoder_params, "num_heads", 2)
@@ -89,16 +142,35 @@ class MatchaLightningModule(torch.nn.Module):
         self.model.mel_std = self.mel_std
         self.process_group = process_group
         self._tr: Optional[MatchaTrainer] = None
+        self._fp = None  # (address, version) of the model's tensors when the trainer last matched them
+        self._pending_opt: Optional[_FusedAdam] = None  # an optimizer state loaded before the engine existed
         self.logged = {}
 
+    def _world(self) -> int:
+        return dist.get_world_size(self.process_group) if dist.is_available() and dist.is_initialized() else 1
+
+    def _model_fp(self):
+        return [(t.data_ptr(), t._version) for t in self.model.state_dict(keep_vars=True).values()]
+
     def trainer(self) -> MatchaTrainer:
-        """the GPU training engine, built from the model's current weights on first use"""
+        """the GPU training engine, built from the model's current weights on first use; a later change of the
+        model's weights from outside (load_state_dict on this module or on .model, an in-place edit) is copied
+        into it before its next use (the Adam moments are kept)"""
         dev = self.mel_mean.device
         if self._tr is None or self._tr.params.flat.device != dev:
             rt.require_gpu(self.mel_mean, what="MatchaLightningModule")
             self._tr = MatchaTrainer(self.model.state_dict(), self.hp, dev, lr=self.learning_rate,
                                      sigma_min=self.sigma_min, prior_loss=self.prior_loss, heads=self.heads,
-                                     process_group=self.process_group)
+                                     process_group=self.process_group, p_dropout=self.p_dropout)
+            if self._tr.world > 1:
+                self._sync_model()  # the ranks' modules hold rank 0's weights, as under DDP
+            self._fp = self._model_fp()
+        elif self._model_fp() != self._fp:
+            self._tr.load_parameters(self.model.state_dict())
+            self._fp = self._model_fp()
+        if self._pending_opt is not None:
+            opt, self._pending_opt = self._pending_opt, None
+            opt._apply_pending(self._tr)
         return self._tr
 
     @torch.no_grad()
@@ -106,21 +178,42 @@ class MatchaLightningModule(torch.nn.Module):
         sd = self.model.state_dict(keep_vars=True)
         for k, v in self._tr.parameters().items():
             sd[k].data.copy_(v)
+        self._fp = self._model_fp()
+
+    @torch.no_grad()
+    def _broadcast_buffers(self):
+        """DDP broadcast_buffers (default True): rank 0's mel_mean / mel_std before every forward"""
+        if self._world() > 1:
+            src = dist.get_global_rank(self.process_group, 0) if self.process_group else 0
+            buf = torch.stack([self.mel_mean, self.mel_std]).float()
+            dist.broadcast(buf, src=src, group=self.process_group)
+            self.mel_mean.copy_(buf[0])
+            self.mel_std.copy_(buf[1])
+
+    def _log(self, prefix, loss, dur, prior, cfm):
+        """self.log(..., sync_dist=True) (train_standalone.py:680-683, 698-701): the mean over the DDP ranks"""
+        vals = torch.stack([loss, dur, prior, cfm]).detach().float()
+        if self._world() > 1:
+            dist.all_reduce(vals, op=dist.ReduceOp.SUM, group=self.process_group)
+            vals = vals / self._world()
+        self.logged.update({f"{prefix}/loss": vals[0], f"{prefix}/dur_loss": vals[1],
+                            f"{prefix}/prior_loss": vals[2], f"{prefix}/cfm_loss": vals[3]})
 
     def forward(self, x, x_lengths, y, y_lengths, spks=None):
         if spks is not None and self.n_spks > 1:
             raise NotImplementedError("multi-speaker training (spk_emb conditioning) is not built")
+        self._broadcast_buffers()
         tr = self.trainer().set_dropout(self.training)
         out = tr.forward_backward(x, x_lengths, y, y_lengths, backward=self.training)
-        return out["dur_loss"][0], out["prior_loss"][0], out["cfm_loss"][0], out["attn"].unsqueeze(1)
+        # attn: maximum_path's [B, T_x, T_y] as the reference returns it (train_standalone.py:646, 667)
+        return out["dur_loss"][0], out["prior_loss"][0], out["cfm_loss"][0], out["attn"]
 
     def training_step(self, batch, batch_idx):
         """train_standalone.py:669-685 -> loss; logs train/{loss,dur_loss,prior_loss,cfm_loss} into self.logged"""
         self.train()
         dur, prior, cfm, _ = self(batch["x"], batch["x_lengths"], batch["y"], batch["y_lengths"], batch.get("spks"))
         loss = dur + prior + cfm
-        self.logged.update({"train/loss": loss, "train/dur_loss": dur, "train/prior_loss": prior,
-                            "train/cfm_loss": cfm})
+        self._log("train", loss, dur, prior, cfm)
         return loss
 
     @torch.no_grad()
@@ -134,7 +227,7 @@ class MatchaLightningModule(torch.nn.Module):
         finally:
             self.train(was)
         loss = dur + prior + cfm
-        self.logged.update({"val/loss": loss, "val/dur_loss": dur, "val/prior_loss": prior, "val/cfm_loss": cfm})
+        self._log("val", loss, dur, prior, cfm)
         return loss
 
     def configure_optimizers(self):

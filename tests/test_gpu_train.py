@@ -376,3 +376,52 @@ def test_lightning_module_drop_in():
     w1 = mod.model.state_dict()["decoder.estimator.final_proj.weight"]
     assert not torch.equal(w0, w1)
     assert torch.equal(w1, mod.trainer().parameters()["decoder.estimator.final_proj.weight"])
+    # forward returns maximum_path's [B, T_x, T_y] (train_standalone.py:646, 667)
+    assert mod(batch["x"], batch["x_lengths"], batch["y"], batch["y_lengths"])[3].shape == (3, x.shape[1], y.shape[2])
+
+
+def _lightning(sd):
+    from types import SimpleNamespace
+
+    import train_standalone as TS
+    from conftest import DEC, DP, ENC
+    mod = TS.MatchaLightningModule(178, 1, 64, SimpleNamespace(**ENC), SimpleNamespace(**DEC),
+                                   {"solver": "euler", "sigma_min": 1e-4}, SimpleNamespace(**DP),
+                                   {"mel_mean": 0.0, "mel_std": 1.0})
+    mod.model.load_state_dict(sd)
+    return mod.to(DEV)
+
+
+def test_lightning_module_resume_and_reload():
+    """Checkpoint / resume (train_standalone.py:850-857, 882): module.state_dict() + optimizer.state_dict() saved after
+    a step and loaded into a FRESH module and optimizer continue bit-identically (the Adam moments, the step count
+    and thus the dropout stream come back); a state dict loaded into a live module's .model is what its next step
+    trains (the engine's flat parameters are refreshed from it)."""
+    sd, x, xl, y, yl, _, _ = _setup(seed=25)
+    batch = {"x": x.to(DEV), "x_lengths": xl.to(DEV), "y": y.to(DEV), "y_lengths": yl.to(DEV)}
+    a = _lightning(sd)
+    opt_a = a.configure_optimizers()
+    torch.manual_seed(1)
+    a.training_step(batch, 0)
+    opt_a.step()
+    msd = {k: v.detach().clone() for k, v in a.state_dict().items()}
+    osd = opt_a.state_dict()
+    assert len(osd["state"]) == len(list(a.parameters())) and float(osd["state"][0]["step"]) == 1.0
+    torch.manual_seed(2)
+    la = a.training_step(batch, 1).item()
+    opt_a.step()
+    wa = {k: v.detach().clone() for k, v in a.model.state_dict().items()}
+    b = _lightning(sd)
+    b.load_state_dict(msd)
+    opt_b = b.configure_optimizers()
+    opt_b.load_state_dict(osd)
+    torch.manual_seed(2)
+    lb = b.training_step(batch, 1).item()
+    opt_b.step()
+    assert la == lb
+    for k, v in b.model.state_dict().items():
+        assert torch.equal(v, wa[k]), k
+    # reload into a live module: the next step starts from the loaded weights
+    a.model.load_state_dict(sd)
+    tp = a.trainer().parameters()
+    assert all(torch.equal(tp[k].cpu(), sd[k].float()) for k in tp)
