@@ -5,7 +5,11 @@ The filterbank is librosa's Slaney mel basis (``librosa.filters.mel(sr, n_fft, n
 htk=False, norm="slaney", float32): librosa is not a dependency here, so ``librosa_mel_fn`` restates
 its published algorithm (host numpy, a constant per configuration, cached per device). The spectrogram
 itself (reflect pad, STFT, magnitude, filterbank, log, normalisation) is ONE HIP launch
-(``mt_log_mel``); there is no CPU fallback.
+(``mt_log_mel``); there is no CPU fallback, so featurization runs in the main (GPU) process: the reference's
+DataLoader CPU workers (train_standalone.py:408-411, num_workers=8) cannot call it.
+The module's host helpers keep the reference's names (MAX_WAV_VALUE, load_wav, dynamic_range_*,
+spectral_*normalize_torch, normalize = librosa.util.normalize for audio); ``MelDataset`` (HiFi-GAN GAN training
+data, out of scope) raises.
 """
 from __future__ import annotations
 
@@ -14,6 +18,70 @@ import torch
 
 from matcha_hip._lib import check, lib, stream_handle
 from matcha_hip.runtime import require_gpu
+
+MAX_WAV_VALUE = 32768.0  # hifigan/meldataset.py:13
+
+
+def load_wav(full_path):
+    """hifigan/meldataset.py:16-18 -> (data, sampling_rate) via scipy.io.wavfile.read"""
+    from scipy.io.wavfile import read
+    sampling_rate, data = read(full_path)
+    return data, sampling_rate
+
+
+def dynamic_range_compression(x, C=1, clip_val=1e-5):
+    return np.log(np.clip(x, a_min=clip_val, a_max=None) * C)
+
+
+def dynamic_range_decompression(x, C=1):
+    return np.exp(x) / C
+
+
+def dynamic_range_compression_torch(x, C=1, clip_val=1e-5):
+    return torch.log(torch.clamp(x, min=clip_val) * C)
+
+
+def dynamic_range_decompression_torch(x, C=1):
+    return torch.exp(x) / C
+
+
+def spectral_normalize_torch(magnitudes):
+    return dynamic_range_compression_torch(magnitudes)
+
+
+def spectral_de_normalize_torch(magnitudes):
+    return dynamic_range_decompression_torch(magnitudes)
+
+
+def normalize(S, norm=np.inf, axis=0, threshold=None, fill=None):
+    """librosa.util.normalize as hifigan/meldataset.py imports it (peak-normalising audio before featurizing):
+    S scaled so that its `norm` along `axis` is 1; slices whose norm is below `threshold` (default: the smallest
+    positive normal of the dtype) are left unscaled (fill=None). numpy in, numpy out."""
+    if fill is not None:
+        raise NotImplementedError("normalize(fill=...) is not used by the reference")
+    S = np.asarray(S)
+    mag = np.abs(S).astype(np.float64)
+    if threshold is None:
+        threshold = np.finfo(S.dtype if np.issubdtype(S.dtype, np.floating) else np.float32).tiny
+    if norm == np.inf:
+        length = np.max(mag, axis=axis, keepdims=True)
+    elif norm == -np.inf:
+        length = np.min(mag, axis=axis, keepdims=True)
+    elif norm == 0:
+        length = np.sum(mag > 0, axis=axis, keepdims=True).astype(mag.dtype)
+    else:
+        length = np.sum(mag ** norm, axis=axis, keepdims=True) ** (1.0 / norm)
+    length = np.where(length < threshold, 1.0, length)
+    return (S / length).astype(S.dtype) if np.issubdtype(S.dtype, np.floating) else S / length
+
+
+class MelDataset:
+    """hifigan/meldataset.py:105-217 (the GAN vocoder's training data) is out of scope."""
+
+    def __init__(self, *a, **k):
+        raise NotImplementedError("MelDataset (HiFi-GAN GAN training data) is not part of the MI355X path; featurize "
+                                  "in the main process with mel_spectrogram(...) on GPU tensors (INTEGRATION.md)")
+
 
 _F_SP, _MIN_LOG_HZ = 200.0 / 3, 1000.0
 _MIN_LOG_MEL = _MIN_LOG_HZ / _F_SP
@@ -77,7 +145,3 @@ def mel_spectrogram(y, n_fft, num_mels, sampling_rate, hop_size, win_size, fmin,
                            stream_handle(y.device)), "log_mel")
     return out[0] if squeeze else out
 
-
-def normalize(data, mu, std):
-    """train_standalone.py:204-210 (for mel tensors produced elsewhere)."""
-    return (data - mu) / std

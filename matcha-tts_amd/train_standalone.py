@@ -25,10 +25,28 @@ import torch
 import torch.distributed as dist
 
 import model as _model
-from hifigan.meldataset import mel_spectrogram, normalize  # noqa: F401  (train_standalone.py:164-224)
+from hifigan.meldataset import mel_spectrogram  # noqa: F401  (train_standalone.py:164-201, on the GPU)
 from matcha_hip import runtime as rt
 from matcha_hip.train import MatchaTrainer
 from model import fix_len_compatibility, sequence_mask  # noqa: F401  (train_standalone.py:227-234, 328-333)
+
+
+def normalize(data, mu, std):
+    """train_standalone.py:204-224: (data - mu) / std, mu / std scalars or per-channel lists / tensors / arrays"""
+    import numpy as np
+
+    def per_channel(v):
+        if isinstance(v, (float, int)):
+            return v
+        if isinstance(v, list):
+            v = torch.tensor(v, dtype=data.dtype, device=data.device)
+        elif isinstance(v, np.ndarray):
+            v = torch.from_numpy(v).to(data.device)
+        elif isinstance(v, torch.Tensor):
+            v = v.to(data.device)
+        return v.unsqueeze(-1)
+
+    return (data - per_channel(mu)) / per_channel(std)
 
 
 def duration_loss(logw, logw_, lengths):
@@ -182,13 +200,17 @@ class MatchaLightningModule(torch.nn.Module):
 
     @torch.no_grad()
     def _broadcast_buffers(self):
-        """DDP broadcast_buffers (default True): rank 0's mel_mean / mel_std before every forward"""
+        """DDP broadcast_buffers (default True): rank 0's buffers before every forward — every buffer of the module
+        tree (mel_mean / mel_std here and in .model: `.to()` gives each module its own copy), as one message"""
         if self._world() > 1:
             src = dist.get_global_rank(self.process_group, 0) if self.process_group else 0
-            buf = torch.stack([self.mel_mean, self.mel_std]).float()
-            dist.broadcast(buf, src=src, group=self.process_group)
-            self.mel_mean.copy_(buf[0])
-            self.mel_std.copy_(buf[1])
+            bufs = list(self.buffers())
+            flat = torch.cat([b.detach().reshape(-1).to(torch.float32) for b in bufs])
+            dist.broadcast(flat, src=src, group=self.process_group)
+            o = 0
+            for b in bufs:
+                b.copy_(flat[o:o + b.numel()].view(b.shape))
+                o += b.numel()
 
     def _log(self, prefix, loss, dur, prior, cfm):
         """self.log(..., sync_dist=True) (train_standalone.py:680-683, 698-701): the mean over the DDP ranks"""

@@ -72,3 +72,26 @@ def test_hip_log_mel_matches_oracle(L):
     outn = mel_spectrogram(y.cuda(), NFFT, NMEL, SR, HOP, 1024, FMIN, FMAX, mel_mean=-5.536622,
                            mel_std=2.116101).cpu()
     assert (outn - (ref + 5.536622) / 2.116101).abs().max().item() < 1e-4
+
+
+def test_meldataset_host_helpers_and_normalize():
+    """The reference module's host names (hifigan/meldataset.py:13-48) and train_standalone.normalize (:204-224)."""
+    import numpy as np
+    import pytest
+    import torch
+    from hifigan import meldataset as M
+    assert M.MAX_WAV_VALUE == 32768.0
+    x = np.array([0.5, -2.0, 1e-7], np.float32)
+    assert np.allclose(M.dynamic_range_decompression(M.dynamic_range_compression(x)), np.maximum(x, 1e-5))
+    t = torch.tensor([3.0, 1e-9])
+    assert torch.allclose(M.spectral_de_normalize_torch(M.spectral_normalize_torch(t)), torch.tensor([3.0, 1e-5]))
+    a = np.array([0.25, -0.5, 0.1], np.float32)
+    assert np.allclose(M.normalize(a), a / 0.5) and M.normalize(a).dtype == np.float32  # librosa.util.normalize
+    assert np.array_equal(M.normalize(np.zeros(3, np.float32)), np.zeros(3, np.float32))
+    with pytest.raises(NotImplementedError):
+        M.MelDataset([], 8192, 1024, 80, 256, 1024, 22050, 0, 8000)
+    import train_standalone as TS
+    mel = torch.randn(2, 80, 5)
+    assert torch.allclose(TS.normalize(mel, -5.5, 2.1), (mel + 5.5) / 2.1)
+    mu, sd = [float(i) for i in range(80)], np.full(80, 2.0, np.float32)
+    assert torch.allclose(TS.normalize(mel, mu, sd), (mel - torch.arange(80.0)[:, None]) / 2.0)
