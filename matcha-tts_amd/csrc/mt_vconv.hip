@@ -418,10 +418,12 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
             }
             if constexpr ((EF & VE_RELU) != 0) v = fmaxf(v, 0.f);
             if constexpr ((EF & VE_GNRES) != 0) {
-              // gn_apply's arithmetic: scale = rstd * gamma, shift = -scale * mean + beta, mish, * mask, bf16
+              // gn_apply's arithmetic: scale = rstd * gamma, shift = -scale * mean + beta, mish, * mask; the block
+              // output h stays fp32 into h + res(x) (as under the reference's autocast: GroupNorm / Mish run in
+              // fp32 and the sum rounds once)
               const float sc = ggs * gam4[r], sh = -sc * gga + bet4[r];
               const float hv = mish_f(bf2(rr[r >> 1], r & 1) * sc + sh) * mk[fn];
-              v = v + (float)(bf16)hv;
+              v = v + hv;
             } else if constexpr ((EF & VE_RESID) != 0) {
               v = v + bf2(rr[r >> 1], r & 1);
             }
