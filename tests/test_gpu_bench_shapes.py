@@ -268,7 +268,8 @@ def test_every_bench_vconv_variant_was_parity_checked():
     """Each (epilogue, tile rows, tile frames, pipeline, taps) variant the bench step launches ran in
     a WHOLE-BATCH parity test above (estimator, encoder, generator), with a multi-tile grid whenever
     the bench runs it multi-tile (the bench steps themselves are only row-checked)."""
-    whole = ("decoder32", "decoder128", "encoder32_bf16", "encoder256_bf16", "generator")
+    whole = ("decoder32", "decoder128", "encoder32_fp32", "encoder256_fp32", "encoder32_bf16", "encoder256_bf16",
+             "generator")
     if any(k not in LOGS for k in whole + ("bench32", "bench256")):
         pytest.skip("needs the whole module's run")
     checked = {}
