@@ -112,6 +112,13 @@ __device__ __forceinline__ f32x2 lrelu2(f32x2 t, float slope) {
 }
 // lrelu of the two bf16 of a packed word, rounded back (the producer-side activated copy's rounding)
 __device__ __forceinline__ uint32_t lrelu_pk(uint32_t w, float slope) { return pk_bf16(lrelu2(unpk_bf16(w), slope)); }
+// lrelu of two fp32 values rounded ONCE to packed bf16 (a conv epilogue's activated output: the reference's fp32
+// arithmetic rounds nothing there; rounding the pre-activation first as well only adds error and VALU work)
+__device__ __forceinline__ uint32_t lrelu_pk_f(f32x2 v, float slope) { return pk_bf16(lrelu2(v, slope)); }
+__device__ __forceinline__ uint32_t lrelu_pk_f_sel(f32x2 v, float slope) {
+  const f32x2 m = v * slope;
+  return pk_bf16(f32x2{v.x > 0.f ? v.x : m.x, v.y > 0.f ? v.y : m.y});
+}
 // the same with the compare / select lrelu (for files built with IEEE mode on, where a max needs a canonicalize)
 __device__ __forceinline__ uint32_t lrelu_pk_sel(uint32_t w, float slope) {
   const f32x2 t = unpk_bf16(w), m = t * slope;

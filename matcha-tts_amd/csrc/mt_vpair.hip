@@ -16,9 +16,10 @@
 // step's weights too, so the next step's first K-slice fragments are read under this step's MFMAs (the mt_vconv pipeline: counted vmcnt, one
 // s_barrier per step, XOR-swizzled 128-byte rows).
 // HBM traffic per pair: x read once (+ halo) and y written once, instead of the per-layer path's x_act read, t written and read back, x read, y and y_act written.
-// Rounding points are the per-layer path's (every stored tensor rounded to bf16, lrelu of the rounded value)
-// and the MFMA accumulation order per output is the same (taps ascending, one 64-channel chunk, two K-slices),
-// so the results are the same bits. The epilogues and the in-place lrelu pass run as packed fp32 pairs (the
+// Rounding points are mt_vconv's per-layer ones (every stored tensor rounded to bf16 once: conv1's activated
+// output lrelu(acc + b1), y = acc + b2 + x and its activated copy lrelu(acc + b2 + x)) and the MFMA accumulation
+// order per output is the same (taps ascending, one 64-channel chunk, two K-slices), so the results are the
+// same bits as the per-layer vconv path. The epilogues and the in-place lrelu pass run as packed fp32 pairs (the
 // kernels are VALU-issue-bound: DESIGN.md §4), and each conv's first K-slice starts from the MFMA's zero C
 // operand. k = 3 pairs run vpair3_kernel below (weights resident, double-buffered rows).
 #include <algorithm>
@@ -274,11 +275,9 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         for (int h = 0; h < 2; ++h) {
           const int fm = 2 * fp + h;
           const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + fm * 16 + 4 * g4);
-          // lrelu(round(acc + b1)), rounded again; zero outside [0, L)
-          const uint32_t t0 = pk_bf16(f32x2{acc[fm][fn][0], acc[fm][fn][1]} + f32x2{b4[0], b4[1]});
-          const uint32_t t1 = pk_bf16(f32x2{acc[fm][fn][2], acc[fm][fn][3]} + f32x2{b4[2], b4[3]});
-          o[h][0] = ok ? lrelu_pk(t0, a.slope) : 0u;
-          o[h][1] = ok ? lrelu_pk(t1, a.slope) : 0u;
+          // lrelu(acc + b1) rounded once to bf16 (conv2's operand); zero outside [0, L)
+          o[h][0] = ok ? lrelu_pk_f(f32x2{acc[fm][fn][0], acc[fm][fn][1]} + f32x2{b4[0], b4[1]}, a.slope) : 0u;
+          o[h][1] = ok ? lrelu_pk_f(f32x2{acc[fm][fn][2], acc[fm][fn][3]} + f32x2{b4[2], b4[3]}, a.slope) : 0u;
         }
         swap16(o[0][0], o[1][0]);
         swap16(o[0][1], o[1][1]);
@@ -328,7 +327,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
             if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
             o1[h][u] = pk_bf16(v);
-            o2[h][u] = lrelu_pk(o1[h][u], a.slope);
+            o2[h][u] = lrelu_pk_f(v, a.slope);  // the activated copy, rounded once
           }
         }
         swap16(o1[0][0], o1[1][0]);
@@ -529,11 +528,9 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
         for (int h = 0; h < 2; ++h) {
           const int fm = 2 * fp + h;
           const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + fm * 16 + 4 * g4);
-          // lrelu(round(acc + b1)), rounded again; zero outside [0, L)
-          const uint32_t t0 = pk_bf16(f32x2{acc[fm][fn][0], acc[fm][fn][1]} + f32x2{b4[0], b4[1]});
-          const uint32_t t1 = pk_bf16(f32x2{acc[fm][fn][2], acc[fm][fn][3]} + f32x2{b4[2], b4[3]});
-          o[h][0] = ok ? lrelu_pk(t0, a.slope) : 0u;
-          o[h][1] = ok ? lrelu_pk(t1, a.slope) : 0u;
+          // lrelu(acc + b1) rounded once to bf16 (conv2's operand); zero outside [0, L)
+          o[h][0] = ok ? lrelu_pk_f(f32x2{acc[fm][fn][0], acc[fm][fn][1]} + f32x2{b4[0], b4[1]}, a.slope) : 0u;
+          o[h][1] = ok ? lrelu_pk_f(f32x2{acc[fm][fn][2], acc[fm][fn][3]} + f32x2{b4[2], b4[3]}, a.slope) : 0u;
         }
         swap16(o[0][0], o[1][0]);
         swap16(o[0][1], o[1][1]);
@@ -581,7 +578,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
             if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
             o1[h][u] = pk_bf16(v);
-            o2[h][u] = lrelu_pk(o1[h][u], a.slope);
+            o2[h][u] = lrelu_pk_f(v, a.slope);  // the activated copy, rounded once
           }
         }
         swap16(o1[0][0], o1[1][0]);

@@ -20,9 +20,9 @@
 //      (+ lrelu(y)).
 // A step is one (64-channel chunk, tap) pair: a 16 KiB weight slot of the mt_vconv image [2][k][128][64]
 // (3-slot LDS ring, two steps in flight) and 24 MFMAs per wave. Steps run chunk-major, taps ascending, two
-// K = 32 slices each: the per-output MFMA accumulation order of mt_vconv's K loop, and the rounding points of
-// the per-layer path (every stored tensor rounded to bf16, lrelu of the rounded value), so the results are
-// the same bits as the per-layer mt_vconv path.
+// K = 32 slices each: the per-output MFMA accumulation order of mt_vconv's K loop, and its rounding points
+// (every stored tensor rounded to bf16 once, activated outputs lrelu'd in fp32 first), so the results are the
+// same bits as the per-layer mt_vconv path.
 // LDS (162,816 B): T planes (2 x 192 rows) | X planes (2 x 248 rows) | weight ring | biases. Rows are 128 B
 // with the 16-byte unit XOR-swizzled by (row & 6) (mt_vconv's conflict-free layout). conv2's discarded last
 // fragments read up to 2 h2 rows past a T plane: into the next plane / the X planes, never outside LDS.
@@ -271,11 +271,9 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
         for (int h = 0; h < 2; ++h) {
           const int fm = 2 * fp + h;
           const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + wm * 64 + fm * 16 + 4 * g4);
-          // lrelu(round(acc + b1)), rounded again; zero outside [0, L)
-          const uint32_t t0 = pk_bf16(f32x2{acc[fm][fn][0], acc[fm][fn][1]} + f32x2{b4[0], b4[1]});
-          const uint32_t t1 = pk_bf16(f32x2{acc[fm][fn][2], acc[fm][fn][3]} + f32x2{b4[2], b4[3]});
-          o[h][0] = ok ? lrelu_pk(t0, a.slope) : 0u;
-          o[h][1] = ok ? lrelu_pk(t1, a.slope) : 0u;
+          // lrelu(acc + b1) rounded once to bf16 (conv2's operand); zero outside [0, L)
+          o[h][0] = ok ? lrelu_pk_f(f32x2{acc[fm][fn][0], acc[fm][fn][1]} + f32x2{b4[0], b4[1]}, a.slope) : 0u;
+          o[h][1] = ok ? lrelu_pk_f(f32x2{acc[fm][fn][2], acc[fm][fn][3]} + f32x2{b4[2], b4[3]}, a.slope) : 0u;
         }
         swap16(o[0][0], o[1][0]);
         swap16(o[0][1], o[1][1]);
@@ -325,7 +323,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
             if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
             o1[h][u] = pk_bf16(v);
-            o2[h][u] = lrelu_pk(o1[h][u], a.slope);
+            o2[h][u] = lrelu_pk_f(v, a.slope);  // the activated copy, rounded once
           }
         }
         swap16(o1[0][0], o1[1][0]);

@@ -20,8 +20,9 @@
 // ds_read_b128 lane groups ({0-3,12-15,20-27}, ...; MI355X_MICROARCH.md §LDS) every B-fragment read (16
 // consecutive rows from any start row, chunk g4) and every A-fragment read is conflict-free, and so are the
 // 8-lane groups of the epilogue's ds_write_b128 (checked exhaustively over start rows when the layout was chosen).
-// Rounding points and the per-output accumulation order (taps ascending, one K = 32 slice per tap) equal the
-// generic per-layer conv path's (mt_conv.hip: 32-channel chunks, taps in order), so the results are the same bits.
+// The per-output accumulation order (taps ascending, one K = 32 slice per tap) equals the generic per-layer conv
+// path's (mt_conv.hip); the rounding points are mt_vconv's (conv1's activated output and y's activated copy rounded
+// once from fp32), so against the generic path (which activates the rounded t) results agree to bf16 rounding.
 #include <algorithm>
 #include <type_traits>
 
@@ -244,11 +245,9 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + h * 16 + 4 * g4);
-        // lrelu(round(acc + b1)), rounded again; zero outside [0, L)
-        const uint32_t t0 = pk_bf16(f32x2{acc[h][fn][0], acc[h][fn][1]} + f32x2{b4[0], b4[1]});
-        const uint32_t t1 = pk_bf16(f32x2{acc[h][fn][2], acc[h][fn][3]} + f32x2{b4[2], b4[3]});
-        o[h][0] = ok ? lrelu_pk(t0, a.slope) : 0u;
-        o[h][1] = ok ? lrelu_pk(t1, a.slope) : 0u;
+        // lrelu(acc + b1) rounded once to bf16 (conv2's operand); zero outside [0, L)
+        o[h][0] = ok ? lrelu_pk_f(f32x2{acc[h][fn][0], acc[h][fn][1]} + f32x2{b4[0], b4[1]}, a.slope) : 0u;
+        o[h][1] = ok ? lrelu_pk_f(f32x2{acc[h][fn][2], acc[h][fn][3]} + f32x2{b4[2], b4[3]}, a.slope) : 0u;
       }
       swap16(o[0][0], o[1][0]);
       swap16(o[0][1], o[1][1]);
@@ -290,7 +289,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
           if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
           if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
           o1[h][u] = pk_bf16(v);
-          o2[h][u] = lrelu_pk(o1[h][u], a.slope);
+          o2[h][u] = lrelu_pk_f(v, a.slope);  // the activated copy, rounded once
         }
       }
       swap16(o1[0][0], o1[1][0]);

@@ -174,14 +174,17 @@ def test_vconv_stages_match_generic_per_layer(T):
 # (5, 200): every fused-pair kernel has more tiles than CUs (mt_vpair128 340, vpair3 505, vpair32 345), so workgroups
 # walk several tiles (cross-tile row prefetch, double buffers) under the bit-exact comparison
 @pytest.mark.parametrize("B,T", [(2, 37), (3, 200), (5, 200)])
-def test_fused_pair_stage_bit_identical_to_per_layer(B, T):
+def test_fused_pair_stage_matches_per_layer(B, T):
     """bf16: the 128-, 64- and 32-channel stages as fused ResBlock pairs (mt_vpair128 / mt_vpair / mt_vpair32:
-    intermediate in LDS, input activation applied on chip, ping-pong chain state) reproduce the per-layer paths
-    bit for bit (same rounding points, same MFMA accumulation order), including tile edges and utterance ends.
-    References: pair 0 (128- and 64-channel stages per layer on mt_vconv, 32-channel stage on the fused-stage
-    kernel mt_rbfuse), pair 2 / 4 (128-channel stage per layer / every pair fused; default 1 fuses its k = 3
-    resblock) and fusion 0 (32-channel stage on the generic
-    per-layer conv kernel)."""
+    intermediate in LDS, input activation applied on chip, ping-pong chain state).
+    * Bit for bit against mt_vconv's per-layer convs for the 128-channel stage (pair 2: that stage per layer; pair 4:
+      every 128-channel pair fused; default 1 fuses its k = 3 resblock): the same rounding points (conv1's
+      activated output lrelu(acc + b) rounded once, y and its activated copy rounded once) and MFMA order.
+    * Within rel-RMS 1e-2 of the paths that round conv1's output twice (round(lrelu(round(t)))), pair 0 (the 32-channel
+      stage on the fused-stage kernel mt_rbfuse) and fusion 0 (the generic per-layer kernel), and all within the
+      §8c bar of the fp32 oracle; including tile edges and utterance ends."""
+    from hifigan.config import v1
+    from oracle import matcha_oracle as O
     g, gen = _gen("bf16", True)
     mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(7 + T)) * 2 - 5
     mel = mel.to(DEV)
@@ -198,10 +201,14 @@ def test_fused_pair_stage_bit_identical_to_per_layer(B, T):
     eng.set_fusion(1)
     b = gen(mel)
     assert torch.isfinite(b).all()
-    assert torch.equal(a, b), (a - b).abs().max().item()
     assert torch.equal(d, b), (d - b).abs().max().item()
     assert torch.equal(e, b), (e - b).abs().max().item()
-    assert torch.equal(c, b), (c - b).abs().max().item()
+    assert not torch.equal(a, b) and not torch.equal(c, b)
+    assert rel_rms(a.cpu(), b.cpu()) < 1e-2 and rel_rms(c.cpu(), b.cpu()) < 1e-2
+    ref = O.generator_forward({k: v.cpu() for k, v in gen.state_dict().items()}, mel.cpu(), v1)
+    errs = {k: rel_rms(v.cpu(), ref) for k, v in (("pairs", b), ("pair0", a), ("generic", c))}
+    print(f"B={B} T={T} vs fp32 oracle: " + ", ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    assert all(v < 1e-2 for v in errs.values()), errs
 
 
 def test_packed_weights_follow_weight_updates():
