@@ -447,119 +447,6 @@ __global__ __launch_bounds__(256) void attn_uni_vec_kernel(int SP, const float* 
   }
 }
 
-// part + o_b in ONE launch (grid B): the utterance's masked frames are its padded ones (a suffix in synthesize, ~20 %
-// of T), so one workgroup per utterance reads only those rows. The frame mask is staged in LDS first (no dependent
-// global mask loads in the scan); frame group fr (32 lanes x 8 channels) sums the normalised rows of the masked frames
-// j = fr, fr + 8, ... in increasing order (4 loads in flight), the 8 groups are merged in a fixed order, then the two
-// GEMVs of attn_uni_vec_kernel. Deterministic; ~3x faster than the slice-parallel part pass + the vec launch.
-constexpr int UNI_TMAX = 4096;  // frames per utterance the mask table holds
-__global__ __launch_bounds__(256) void attn_uni_ovec_kernel(const bf16* __restrict__ x, const float* __restrict__ mask,
-                                                            int T, const bf16* __restrict__ wqkv, int mq,
-                                                            const float* __restrict__ bqkv, const bf16* __restrict__ wout,
-                                                            const float* __restrict__ bout, float* __restrict__ ovec) {
-  __shared__ float red[8][UNI_C + 1];
-  __shared__ float zb[UNI_C], vb[128];
-  __shared__ unsigned char mk[UNI_TMAX];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  for (int j = tid; j < T; j += 256) mk[j] = mask[(size_t)b * T + j] == 0.f;
-  __syncthreads();
-  const int fr = tid >> 5, cl = tid & 31, c = cl * 8;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, n = 0.f;
-  constexpr int FB = 4;
-  int j = fr;
-  for (;;) {
-    int js[FB];
-    int got = 0;
-#pragma unroll
-    for (int i = 0; i < FB; ++i) {  // the next FB masked frames of this group
-      while (j < T && !mk[j]) j += 8;
-      js[i] = j;
-      got += j < T;
-      j += 8;
-    }
-    if (got == 0) break;
-    u32x4 wv[FB];
-#pragma unroll
-    for (int i = 0; i < FB; ++i)
-      wv[i] = js[i] < T ? *reinterpret_cast<const u32x4*>(x + ((size_t)b * T + js[i]) * UNI_C + c) : u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int i = 0; i < FB; ++i) {
-      if (js[i] >= T) continue;
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[2 * e] = __uint_as_float(wv[i][e] << 16);
-        v[2 * e + 1] = __uint_as_float(wv[i][e] & 0xffff0000u);
-      }
-      float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) sm += __shfl_xor(sm, o, 64);
-      const float mu = sm * (1.f / UNI_C);
-      float q = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) q += (v[e] - mu) * (v[e] - mu);
-#pragma unroll
-      for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);
-      const float rs = rsqrtf(q * (1.f / UNI_C) + 1e-5f);  // nn.LayerNorm eps (BasicTransformerBlock.norm1)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += (v[e] - mu) * rs;
-      n += 1.f;
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) red[fr][c + e] = acc[e];
-  if (cl == 0) red[fr][UNI_C] = n;
-  __syncthreads();
-  {
-    float z = 0.f, nn = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      z += red[k][tid];
-      nn += red[k][UNI_C];
-    }
-    zb[tid] = z / nn;
-  }
-  __syncthreads();
-  const int q4 = tid & 3, rq = tid >> 2;
-  auto dot8 = [](u32x4 w, const float* z) {
-    float a = 0.f;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      a += __uint_as_float(w[e] << 16) * z[2 * e] + __uint_as_float(w[e] & 0xffff0000u) * z[2 * e + 1];
-    return a;
-  };
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {  // V rows of the LN-folded QKV image, as attn_uni_vec_kernel
-    const int r = rq + 64 * pass;
-    const bf16* wr = wqkv + ((size_t)q4 * mq + 256 + r) * 64;
-    u32x4 w[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = *reinterpret_cast<const u32x4*>(wr + 8 * i);
-    float v = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v += dot8(w[i], zb + q4 * 64 + 8 * i);
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
-    if (q4 == 0) vb[r] = (float)(bf16)(v + bqkv[256 + r]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int pass = 0; pass < 4; ++pass) {
-    const int r = rq + 64 * pass;
-    const int ck = q4 >> 1, k0 = (q4 & 1) * 32;
-    const bf16* wr = wout + ((size_t)ck * UNI_C + r) * 64 + k0;
-    u32x4 w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = *reinterpret_cast<const u32x4*>(wr + 8 * i);
-    float o = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o += dot8(w[i], vb + ck * 64 + k0 + 8 * i);
-    o += __shfl_xor(o, 1, 64);
-    o += __shfl_xor(o, 2, 64);
-    if (q4 == 0) ovec[(size_t)b * UNI_C + r] = o + bout[r];
-  }
-}
-
 // x += o_b on every frame of the slice, + the next LayerNorm's per-slab (mean, M2) (grid slices x B)
 __global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ x, int T, const float* __restrict__ ovec,
                                                              float* __restrict__ row_out) {
@@ -607,15 +494,6 @@ __global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ 
   }
 }
 
-// MT_UNI_FUSED=0 (A/B knob, read once): the two-launch part + vec form
-static bool uni_fused() {
-  static const bool on = [] {
-    const char* e = getenv("MT_UNI_FUSED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // the masked-sum pass streams x once: finer slices (up to 32 per utterance) for more workgroups in flight
 int uniform_part_slices(int T) { return std::max(1, std::min(UNI_PSMAX, T / 24)); }
 size_t uniform_attention_floats(int B) { return (size_t)B * (UNI_PSMAX * UNI_PART + UNI_C); }
@@ -626,14 +504,9 @@ int launch_uniform_attention(void* x, const float* mask, int B, int T, const voi
              "uniform attention: arguments (C = 256, 2 heads x 64)");
   const int SP = uniform_part_slices(T);
   float* ovec = part + (size_t)B * UNI_PSMAX * UNI_PART;  // [B][256] after the slice sums (uniform_attention_floats)
-  if (T <= UNI_TMAX && uni_fused()) {  // one workgroup per utterance over its masked rows, GEMVs included
-    hipLaunchKernelGGL(attn_uni_ovec_kernel, dim3(B), dim3(256), 0, st, (const bf16*)x, mask, T, (const bf16*)wqkv, mq,
-                       bqkv, (const bf16*)wout, bout, ovec);
-  } else {
-    hipLaunchKernelGGL(attn_uni_part_kernel, dim3(SP, B), dim3(256), 0, st, (const bf16*)x, mask, T, part);
-    hipLaunchKernelGGL(attn_uni_vec_kernel, dim3(B), dim3(256), 0, st, SP, (const float*)part, (const bf16*)wqkv, mq,
-                       bqkv, (const bf16*)wout, bout, ovec);
-  }
+  hipLaunchKernelGGL(attn_uni_part_kernel, dim3(SP, B), dim3(256), 0, st, (const bf16*)x, mask, T, part);
+  hipLaunchKernelGGL(attn_uni_vec_kernel, dim3(B), dim3(256), 0, st, SP, (const float*)part, (const bf16*)wqkv, mq,
+                     bqkv, (const bf16*)wout, bout, ovec);
   hipLaunchKernelGGL(attn_uni_apply_kernel, dim3(SP, B), dim3(256), 0, st, (bf16*)x, T, (const float*)ovec, row_out);
   MT_CHECK_HIP(hipGetLastError());
   return 0;

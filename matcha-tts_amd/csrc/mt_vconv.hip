@@ -382,8 +382,11 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
               if constexpr ((EF & VE_MASK) != 0) v = v * mk[fn];
               if constexpr ((EF & VE_PMASK) != 0) v = v * pmk;
               const uint32_t rb = pk_bf16(v);
-              // the activated output rounded once from fp32 (VE_ACT: conv1's lrelu(t); VE_DUAL: the next conv1's input)
-              const uint32_t av = (EF & (VE_ACT | VE_DUAL)) ? lrelu_pk_f_sel(v, a.slope) : 0u;
+              // VE_ACT (conv1's only output): lrelu(t) rounded once from fp32; VE_DUAL: the activated copy of the STORED
+              // chain state, lrelu(round(v)) — what a consumer activating the stored tensor itself (the fused pairs'
+              // in-place pass) computes
+              const uint32_t av = (EF & VE_ACT) ? lrelu_pk_f_sel(v, a.slope)
+                                  : (EF & VE_DUAL) ? lrelu_pk_sel(rb, a.slope) : 0u;
               o1[h][u] = (EF & VE_ACT) ? av : rb;
               o2[h][u] = av;
             }
@@ -444,7 +447,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
               rmean[fn] += dl * (1.f / (float)(fp * 8 + h * 4 + r + 1));
               rm2[fn] += dl * (fr - rmean[fn]);
             }
-            const bf16 av = (bf16)lrelu_f(v, a.slope);
+            const bf16 av = (bf16)lrelu_f((EF & VE_ACT) ? v : (float)rb, a.slope);
             ob[r] = (EF & VE_ACT) ? av : rb;
             ab[r] = av;
           }

@@ -16,8 +16,8 @@
 // step's weights too, so the next step's first K-slice fragments are read under this step's MFMAs (the mt_vconv pipeline: counted vmcnt, one
 // s_barrier per step, XOR-swizzled 128-byte rows).
 // HBM traffic per pair: x read once (+ halo) and y written once, instead of the per-layer path's x_act read, t written and read back, x read, y and y_act written.
-// Rounding points are mt_vconv's per-layer ones (every stored tensor rounded to bf16 once: conv1's activated
-// output lrelu(acc + b1), y = acc + b2 + x and its activated copy lrelu(acc + b2 + x)) and the MFMA accumulation
+// Rounding points are mt_vconv's per-layer ones (conv1's activated output lrelu(acc + b1) rounded once from fp32,
+// y = round(acc + b2 + x) and its activated copy lrelu(y), rounded) and the MFMA accumulation
 // order per output is the same (taps ascending, one 64-channel chunk, two K-slices), so the results are the
 // same bits as the per-layer vconv path. The epilogues and the in-place lrelu pass run as packed fp32 pairs (the
 // kernels are VALU-issue-bound: DESIGN.md §4), and each conv's first K-slice starts from the MFMA's zero C
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
             if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
             o1[h][u] = pk_bf16(v);
-            o2[h][u] = lrelu_pk_f(v, a.slope);  // the activated copy, rounded once
+            o2[h][u] = lrelu_pk(o1[h][u], a.slope);  // the stored state's activated copy
           }
         }
         swap16(o1[0][0], o1[1][0]);
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
             if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
             o1[h][u] = pk_bf16(v);
-            o2[h][u] = lrelu_pk_f(v, a.slope);  // the activated copy, rounded once
+            o2[h][u] = lrelu_pk(o1[h][u], a.slope);  // the stored state's activated copy
           }
         }
         swap16(o1[0][0], o1[1][0]);

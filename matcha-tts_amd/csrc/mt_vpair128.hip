@@ -323,7 +323,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
             if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
             o1[h][u] = pk_bf16(v);
-            o2[h][u] = lrelu_pk_f(v, a.slope);  // the activated copy, rounded once
+            o2[h][u] = lrelu_pk(o1[h][u], a.slope);  // the stored state's activated copy
           }
         }
         swap16(o1[0][0], o1[1][0]);

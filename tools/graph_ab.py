@@ -4,6 +4,12 @@ import statistics
 import sys
 import time
 
+import os as _os
+
+_ROOT = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+sys.path.insert(0, _ROOT)
+sys.path.insert(0, _os.path.join(_ROOT, "matcha-tts_amd"))
+
 import torch
 
 sys.path.insert(0, ".")
