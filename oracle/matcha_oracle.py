@@ -514,8 +514,46 @@ def maximum_path(neg_cent: Tensor, mask: Tensor) -> Tensor:
     return torch.from_numpy(paths)
 
 
+def maximum_path_diag(neg_cent: Tensor, mask: Tensor) -> Tensor:
+    """maximum_path above evaluated one anti-diagonal at a time (numpy vectors instead of Python loops over
+    cells), for the configs[4]-sized test. Cell (x, y) reads (x-1, y) and (x, y-1), both on diagonal
+    x + y - 1, and only cells of the same valid band (unvisited cells read 0) — the identical float32
+    max-then-add per cell, so the table and the path equal maximum_path's (tests/test_oracle_golden.py)."""
+    import numpy as np
+    value = neg_cent.detach().cpu().numpy().astype(np.float32)
+    m = mask.detach().cpu().numpy()
+    b, tx_max, ty_max = value.shape
+    t_xs = m.sum(axis=1)[:, 0].astype(np.int32)
+    t_ys = m.sum(axis=2)[:, 0].astype(np.int32)
+    paths = np.zeros((b, tx_max, ty_max), dtype=np.float32)
+    for i in range(b):
+        tx, ty = int(t_xs[i]), int(t_ys[i])
+        p = np.zeros((tx + 1, ty + 1), dtype=np.float32)  # row / column 0 = the "outside" zeros
+        v = value[i, :tx, :ty]
+        for d in range(tx + ty - 1):
+            # the loop's band for column y = d - x: max(0, tx + y - ty) <= x <= min(tx - 1, y)
+            xs = np.arange(max(0, d - ty + 1), min(tx - 1, d) + 1)
+            ys = d - xs
+            keep = (xs >= tx + ys - ty) & (xs <= ys)
+            xs, ys = xs[keep], ys[keep]
+            if xs.size == 0:
+                continue
+            up = p[xs, ys + 1]  # (x-1, y): p is shifted by one in both axes
+            left = p[xs + 1, ys]  # (x, y-1)
+            vp = np.where(xs == 0, np.where(ys == 0, np.float32(0.0), left),
+                          np.where(ys == 0, up, np.maximum(up, left)))
+            p[xs + 1, ys + 1] = vp + v[xs, ys]
+        q = p[1:, 1:]
+        index = tx - 1
+        for y in range(ty - 1, -1, -1):
+            paths[i, index, y] = 1.0
+            if y > 0 and index > 0 and q[index - 1, y - 1] > q[index, y - 1]:
+                index -= 1
+    return torch.from_numpy(paths)
+
+
 def training_losses(sd: SD, x: Tensor, x_lengths: Tensor, y: Tensor, y_lengths: Tensor, t: Tensor, z: Tensor, hp,
-                    sigma_min: float = 1e-4, heads: int = 2):
+                    sigma_min: float = 1e-4, heads: int = 2, mas=None):
     """train_standalone.py:623-667 (MatchaLightningModule.forward, single speaker, prior_loss on) with
     CFM.compute_loss model.py:1147-1162, duration_loss :79-81; dropout off (eval-mode modules), the noise
     t [B] ~ rand and z ~ randn_like(y) passed in. sd: full model state dict ("encoder.*",
@@ -532,7 +570,7 @@ def training_losses(sd: SD, x: Tensor, x_lengths: Tensor, y: Tensor, y_lengths: 
         y_mu_double = torch.matmul(2.0 * (factor * mu_x).transpose(1, 2), y)
         mu_square = torch.sum(factor * (mu_x ** 2), 1).unsqueeze(-1)
         log_prior = y_square - y_mu_double + mu_square + const
-        attn = maximum_path(log_prior, attn_mask.squeeze(1)).to(y.device)
+        attn = (mas or maximum_path)(log_prior, attn_mask.squeeze(1)).to(y.device)
     logw_ = torch.log(1e-8 + torch.sum(attn.unsqueeze(1), -1)) * x_mask  # :650-651
     dur_loss = torch.sum((logw - logw_) ** 2) / torch.sum(x_lengths)
     mu_y = torch.matmul(attn.transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)  # :654-655

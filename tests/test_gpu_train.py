@@ -262,11 +262,23 @@ def _setup(seed=21, B=3, Tx=17, Ty=64, x_len=(17, 12, 9), y_len=(64, 50, 33)):
     return sd, x, xl, y, yl, t, z
 
 
-def _oracle_grads(sd, x, xl, y, yl, t, z):
+def _configs4_batch(seed=41, B=64, Tx=200, Ty=868):
+    """configs[4]'s batch: 64 LJSpeech-shaped utterances (train_standalone.py's batch_size 64), text 80..200
+    tokens, mel ≈ 4.3 frames per token, the longest at T_y = 868 (T_y % 4 == 0, no fix_len padding needed)."""
+    rs = np.random.RandomState(seed)
+    x_len = rs.randint(80, Tx + 1, B)
+    x_len[0] = Tx
+    y_len = np.minimum(Ty, np.round(x_len * rs.uniform(3.6, 4.34, B))).astype(int)
+    y_len[0] = Ty
+    return _setup(seed=seed, B=B, Tx=Tx, Ty=Ty, x_len=tuple(int(v) for v in x_len),
+                  y_len=tuple(int(v) for v in y_len))
+
+
+def _oracle_grads(sd, x, xl, y, yl, t, z, mas=None):
     import oracle.matcha_oracle as O
     params = {k: v.clone().float().requires_grad_(True) for k, v in sd.items()
               if k.startswith(("encoder.", "decoder.estimator."))}
-    dur, prior, cfm, attn, lp = O.training_losses(params, x, xl, y, yl, t, z, HP)
+    dur, prior, cfm, attn, lp = O.training_losses(params, x, xl, y, yl, t, z, HP, mas=mas)
     grads = torch.autograd.grad(dur + prior + cfm, list(params.values()), allow_unused=True)
     return (dur, prior, cfm, attn, lp), {k: (gr if gr is not None else torch.zeros_like(p))
                                          for (k, p), gr in zip(params.items(), grads)}
@@ -277,9 +289,38 @@ def test_training_step_matches_autograd():
     L2 error < 2e-3 per tensor, < 5e-4 over the whole flat gradient) of the fp32 GPU step against fp32 torch
     autograd through the oracle on the CPU (the reference's arithmetic order for the time embedding and the
     log-prior) on the same weights, batch, t and z (dropout off: eval-mode modules)."""
+    _check_step(*_setup())
+
+
+def test_training_step_configs4_size_matches_autograd():
+    """The same checks at configs[4]'s per-GPU size: B = 64, T_x = 200, T_y = 868 (55.5 k mel frames), where the
+    long-K weight gradients take the split-K GEMM path and every GEMM runs multi-tile. The oracle runs on the
+    host CPU (the MAS in its anti-diagonal form, equal to the loop form: tests/test_mas.py)."""
+    import oracle.matcha_oracle as O
+    _check_step(*_configs4_batch(), mas=O.maximum_path_diag)
+
+
+def test_training_configs4_size_dropout_deterministic():
+    """Dropout on at configs[4]'s size: two trainers from the same weights and seed give bit-identical losses and
+    gradients (fixed-order reductions, split-K included), and the masks change the loss against eval mode."""
     from matcha_hip.train import MatchaTrainer
-    sd, x, xl, y, yl, t, z = _setup()
-    (dur, prior, cfm, attn, lp), gref = _oracle_grads(sd, x, xl, y, yl, t, z)
+    sd, x, xl, y, yl, t, z = _configs4_batch(seed=42)
+    args = (x.to(DEV), xl.to(DEV), y.to(DEV), yl.to(DEV))
+    kw = dict(t=t.to(DEV), z=z.to(DEV))
+    outs, grads = [], []
+    for _ in range(2):
+        tr = MatchaTrainer(sd, HP, DEV, seed=9)
+        outs.append(tr.forward_backward(*args, **kw)["loss"].item())
+        grads.append(tr.grads.flat.detach().cpu().clone())
+        del tr
+    ev = MatchaTrainer(sd, HP, DEV, dropout=False).forward_backward(*args, **kw)["loss"].item()
+    assert outs[0] == outs[1] and torch.equal(grads[0], grads[1])
+    assert math.isfinite(outs[0]) and outs[0] != ev
+
+
+def _check_step(sd, x, xl, y, yl, t, z, mas=None):
+    from matcha_hip.train import MatchaTrainer
+    (dur, prior, cfm, attn, lp), gref = _oracle_grads(sd, x, xl, y, yl, t, z, mas=mas)
     tr = MatchaTrainer(sd, HP, DEV, dropout=False)
     out = tr.forward_backward(x.to(DEV), xl.to(DEV), y.to(DEV), yl.to(DEV), t=t.to(DEV), z=z.to(DEV))
     torch.cuda.synchronize()
