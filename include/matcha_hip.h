@@ -238,6 +238,12 @@ int mt_maximum_path(const float* neg_cent, const int32_t* t_xs, const int32_t* t
 int mtt_gemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda, long long sA,
              const float* B, int ldb, long long sB, float beta, float* C, int ldc, long long sC, int batch,
              const float* bias, const float* row_mask, float* ws, size_t ws_bytes, void* stream);
+/* mtt_gemm with the operands rounded (RNE) to a 16-bit format before 16-bit MFMA with fp32 accumulation:
+ * opfmt 0 none (= mtt_gemm), 1 fp16 (the reference Trainer's precision="16-mixed", train_standalone.py:868, under
+ * which autocast runs conv1d / linear / matmul on fp16 operands), 2 bf16 ("bf16-mixed"). The output stays fp32. */
+int mtt_gemm_ex(int opfmt, int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda,
+                long long sA, const float* B, int ldb, long long sB, float beta, float* C, int ldc, long long sC,
+                int batch, const float* bias, const float* row_mask, float* ws, size_t ws_bytes, void* stream);
 /* device workspace mtt_gemm uses to split a long K over slices (0: never splits this shape); with less, it runs
  * unsplit */
 size_t mtt_gemm_workspace_bytes(int M, int N, int K, int batch);

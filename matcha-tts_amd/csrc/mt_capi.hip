@@ -402,8 +402,14 @@ int mt_probe_stop(int* launches, double* total_ms, double* flops, double* bytes,
 int mtt_gemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda, long long sA,
              const float* B, int ldb, long long sB, float beta, float* C, int ldc, long long sC, int batch,
              const float* bias, const float* row_mask, float* ws, size_t ws_bytes, void* stream) {
+  return mtt_gemm_ex(0, transA, transB, M, N, K, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, bias,
+                     row_mask, ws, ws_bytes, stream);
+}
+int mtt_gemm_ex(int opfmt, int transA, int transB, int M, int N, int K, float alpha, const float* A, int lda,
+                long long sA, const float* B, int ldb, long long sB, float beta, float* C, int ldc, long long sC,
+                int batch, const float* bias, const float* row_mask, float* ws, size_t ws_bytes, void* stream) {
   mt::GemmF32 g{transA, transB, M, N, K, alpha, beta, A, lda, sA, B, ldb, sB, C, ldc, sC, batch, bias, row_mask, ws,
-                ws_bytes / sizeof(float)};
+                ws_bytes / sizeof(float), opfmt};
   return mt::gemm_f32(g, (hipStream_t)stream);
 }
 size_t mtt_gemm_workspace_bytes(int M, int N, int K, int batch) {

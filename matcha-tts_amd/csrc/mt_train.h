@@ -23,6 +23,7 @@ struct GemmF32 {  // C[z] = alpha op(A[z]) op(B[z]) + beta C[z]; op(A) is M x K,
   const float* rmask;  // optional, per output row of each batch [batch][M]: C *= rmask[m] (last)
   float* ws;           // split-K partials (gemm_f32_workspace_floats); NULL: no split
   size_t ws_floats;
+  int opfmt;  // operands rounded to: 0 none (exact fp32 MFMA), 1 fp16, 2 bf16 (16-bit MFMA, fp32 accumulation)
 };
 size_t gemm_f32_workspace_floats(int M, int N, int K, int batch);
 int gemm_f32(const GemmF32& g, hipStream_t st);

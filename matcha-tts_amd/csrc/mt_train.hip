@@ -145,6 +145,112 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmF32 g, int kchunk, in
       }
 }
 
+// Mixed-precision GEMM (the "16-mixed" / "bf16-mixed" training modes): the same 128 x 128 tile, register-staged
+// fp32 loads and epilogue as gemm_f32_kernel, but the operands are rounded (RNE) to fp16 (FMT 1) or bf16 (FMT 2)
+// when they are written to LDS, and the K loop runs v_mfma_f32_32x32x16_{f16,bf16} with fp32 accumulation —
+// autocast's matmul arithmetic (16-bit operands, fp32 sums). LDS holds op(A) as [m][k] and op(B) as [n][k] with
+// k contiguous (40-element rows: 80 B, so the 8 lanes of a ds_read_b128 phase hit distinct banks), which is
+// each lane's operand fragment (row l & 31, k = 8 (l >> 5) + j) as one 16-byte read.
+namespace {
+constexpr int GKH = GBK + 8;
+template <int FMT> struct Half;
+template <> struct Half<1> { typedef _Float16 T; };
+template <> struct Half<2> { typedef __bf16 T; };
+
+// the A-shaped tile of gemm_load_a (128 rows x 32 k) into LDS as [row][k] in 16-bit
+template <int TA, typename H>
+__device__ __forceinline__ void gemm_store_h(H (*As)[GKH], const f32x4 (&r)[4]) {
+  typedef H h4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    if (TA) {  // 4 consecutive rows at one k
+#pragma unroll
+      for (int j = 0; j < 4; ++j) As[(e & 31) * 4 + j][e >> 5] = (H)r[i][j];
+    } else {  // 4 consecutive k of one row
+      h4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (H)r[i][j];
+      *reinterpret_cast<h4*>(&As[e >> 3][(e & 7) * 4]) = v;
+    }
+  }
+}
+}  // namespace
+
+template <int TA, int TB, int FMT>
+__global__ __launch_bounds__(256) void gemm_h_kernel(GemmF32 g, int kchunk, int split, bool va, bool vb) {
+  typedef typename Half<FMT>::T H;
+  typedef H h8 __attribute__((ext_vector_type(8)));
+  __shared__ __attribute__((aligned(16))) H As[GBM][GKH];
+  __shared__ __attribute__((aligned(16))) H Bs[GBM][GKH];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBM, z = blockIdx.z;
+  const float* A = g.A + (split ? 0 : (size_t)z * g.sA);
+  const float* B = g.B + (split ? 0 : (size_t)z * g.sB);
+  float* Cm = g.C + (size_t)z * g.sC;
+  const int kbeg = split ? z * kchunk : 0, kend = split ? min(g.K, kbeg + kchunk) : g.K;
+  GemmF32 gb = g;
+  gb.M = g.N;
+  gb.lda = g.ldb;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  f32x4 ra[4], rb[4];
+  gemm_load_a<TA>(g, A, m0, kbeg, kend, va, ra);
+  gemm_load_a<1 - TB>(gb, B, n0, kbeg, kend, vb, rb);
+  const int fr = lane & 31, fk = 8 * (lane >> 5);
+  for (int kb = kbeg; kb < kend; kb += GBK) {
+    gemm_store_h<TA>(As, ra);
+    gemm_store_h<1 - TB>(Bs, rb);
+    __syncthreads();
+    if (kb + GBK < kend) {
+      gemm_load_a<TA>(g, A, m0, kb + GBK, kend, va, ra);
+      gemm_load_a<1 - TB>(gb, B, n0, kb + GBK, kend, vb, rb);
+    }
+#pragma unroll
+    for (int s = 0; s < GBK; s += 16) {
+      h8 a[2], b[2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        a[f] = *reinterpret_cast<const h8*>(&As[wm * 64 + f * 32 + fr][s + fk]);
+        b[f] = *reinterpret_cast<const h8*>(&Bs[wn * 64 + f * 32 + fr][s + fk]);
+      }
+#pragma unroll
+      for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 2; ++fn) {
+          if constexpr (FMT == 1)
+            acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[fm], b[fn], acc[fm][fn], 0, 0, 0);
+          else
+            acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[fm], b[fn], acc[fm][fn], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+  }
+  const float alpha = split ? 1.f : g.alpha, beta = split ? 0.f : g.beta;
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int gm = m0 + wm * 64 + fm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int gn = n0 + wn * 64 + fn * 32 + (lane & 31);
+        if (gm >= g.M || gn >= g.N) continue;
+        float* c = Cm + (size_t)gm * (split ? g.N : g.ldc) + gn;
+        float v = alpha * acc[fm][fn][r];
+        if (beta != 0.f) v += beta * *c;
+        if (!split && g.bias) v += g.bias[gn];
+        if (!split && g.rmask) v *= g.rmask[(size_t)z * g.M + gm];
+        *c = v;
+      }
+}
+
 // C = alpha * sum_z P[z] + beta * C, slices in order
 __global__ void splitk_reduce_kernel(const float* __restrict__ P, int S, int M, int N, float alpha, float beta,
                                      const float* __restrict__ bias, const float* __restrict__ rmask,
@@ -206,8 +312,15 @@ int gemm_f32(const GemmF32& g, hipStream_t st) {
     }
   }
   dim3 grid(gx, gy, S);
+  MT_REQUIRE(g.opfmt >= 0 && g.opfmt <= 2, "gemm: operand format (0 fp32, 1 fp16, 2 bf16)");
   auto kern = g.transA ? (g.transB ? gemm_f32_kernel<1, 1> : gemm_f32_kernel<1, 0>)
                        : (g.transB ? gemm_f32_kernel<0, 1> : gemm_f32_kernel<0, 0>);
+  if (g.opfmt == 1)
+    kern = g.transA ? (g.transB ? gemm_h_kernel<1, 1, 1> : gemm_h_kernel<1, 0, 1>)
+                    : (g.transB ? gemm_h_kernel<0, 1, 1> : gemm_h_kernel<0, 0, 1>);
+  else if (g.opfmt == 2)
+    kern = g.transA ? (g.transB ? gemm_h_kernel<1, 1, 2> : gemm_h_kernel<1, 0, 2>)
+                    : (g.transB ? gemm_h_kernel<0, 1, 2> : gemm_h_kernel<0, 0, 2>);
   hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, k, kchunk, split, va, vb);
   if (split)
     hipLaunchKernelGGL(splitk_reduce_kernel, ew_grid((size_t)g.M * g.N), dim3(256), 0, st, (const float*)g.ws,

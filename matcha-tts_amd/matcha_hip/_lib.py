@@ -92,6 +92,8 @@ SIGNATURES = {
     "mt_probe_stop": (c_int, [P, P, P, P, c_double, c_double, P]),
     "mtt_gemm": (c_int, [c_int, c_int, c_int, c_int, c_int, c_float, P, c_int, c_int64, P, c_int, c_int64, c_float,
                          P, c_int, c_int64, c_int, P, P, P, c_size_t, P]),
+    "mtt_gemm_ex": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, c_int, c_int64, P, c_int, c_int64,
+                            c_float, P, c_int, c_int64, c_int, P, P, P, c_size_t, P]),
     "mtt_gemm_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "mtt_im2col": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "mtt_col2im": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, P]),

@@ -58,19 +58,39 @@ class _GemmWS(_Scratch):
     buf: Optional[torch.Tensor] = None
 
 
+# GEMM operand format of the model's conv / linear / attention products (forward and backward): 0 exact fp32
+# (precision "32"), 1 fp16 ("16-mixed"), 2 bf16 ("bf16-mixed") — set per step by MatchaTrainer (operand_format).
+_OPFMT = [0]
+PRECISIONS = {"32": 0, "32-true": 0, "fp32": 0, "16-mixed": 1, "bf16-mixed": 2}
+
+
+class operand_format:
+    """with operand_format(f): the layer products below round their GEMM operands to format f"""
+
+    def __init__(self, fmt: int):
+        self.fmt = fmt
+
+    def __enter__(self):
+        self.prev, _OPFMT[0] = _OPFMT[0], self.fmt
+
+    def __exit__(self, *exc):
+        _OPFMT[0] = self.prev
+
+
 def gemm(A, B, M, N, K, out, ta=0, tb=0, alpha=1.0, beta=0.0, lda=None, ldb=None, ldc=None, batch=1, sA=0, sB=0,
-         sC=0, a_off=0, b_off=0, c_off=0, bias=None, rmask=None):
+         sC=0, a_off=0, b_off=0, c_off=0, bias=None, rmask=None, fmt=0):
     """out = (alpha op(A) op(B) + beta out + bias[n]) * rmask[m], row-major; op(A) M x K, op(B) K x N; offsets in
-    elements. Long-K / few-tile shapes split K over slices in a workspace (summed in slice order)."""
+    elements. Long-K / few-tile shapes split K over slices in a workspace (summed in slice order). fmt: operands
+    rounded to fp16 (1) / bf16 (2) for 16-bit MFMA with fp32 sums; 0 exact fp32."""
     lda = lda if lda is not None else (M if ta else K)
     ldb = ldb if ldb is not None else (K if tb else N)
     ldc = ldc if ldc is not None else N
     L = lib()
     wsb = L.mtt_gemm_workspace_bytes(M, N, K, batch)
     ws = _GemmWS.get(wsb // 4, out) if wsb else None
-    check(L.mtt_gemm(int(ta), int(tb), M, N, K, float(alpha), A.data_ptr() + 4 * a_off, lda, sA,
-                     B.data_ptr() + 4 * b_off, ldb, sB, float(beta), out.data_ptr() + 4 * c_off, ldc, sC, batch,
-                     ptr(bias), ptr(rmask), ptr(ws), wsb, _s(out)), "gemm")
+    check(L.mtt_gemm_ex(int(fmt), int(ta), int(tb), M, N, K, float(alpha), A.data_ptr() + 4 * a_off, lda, sA,
+                        B.data_ptr() + 4 * b_off, ldb, sB, float(beta), out.data_ptr() + 4 * c_off, ldc, sC, batch,
+                        ptr(bias), ptr(rmask), ptr(ws), wsb, _s(out)), "gemm")
     return out
 
 
@@ -209,16 +229,16 @@ def linear_fwd(x, W, b, rmask=None):
     in the GEMM epilogue)"""
     I = x.shape[-1]
     N, O = x.numel() // I, W.shape[0]
-    return mm(x, W, N, O, I, tb=1, bias=b, rmask=rmask)
+    return mm(x, W, N, O, I, tb=1, bias=b, rmask=rmask, fmt=_OPFMT[0])
 
 
 def linear_bwd(dy, x, W, gW, gb, need_dx=True):
     I = x.shape[-1]
     N, O = x.numel() // I, W.shape[0]
-    gemm(dy, x, O, I, N, gW, ta=1)
+    gemm(dy, x, O, I, N, gW, ta=1, fmt=_OPFMT[0])
     if gb is not None:
         colsum(dy, O, gb)
-    return mm(dy, W, N, I, O) if need_dx else None
+    return mm(dy, W, N, I, O, fmt=_OPFMT[0]) if need_dx else None
 
 
 def conv_fwd(x, W, b, stride=1, pad=0, dil=1, mask=None, out_mask=None):
@@ -230,7 +250,7 @@ def conv_fwd(x, W, b, stride=1, pad=0, dil=1, mask=None, out_mask=None):
     cols = empty(B * Tout, Cin * k, like=x)
     check(lib().mtt_im2col(x.data_ptr(), ptr(mask), B, T, Cin, k, stride, pad, dil, Tout, cols.data_ptr(), _s(x)),
           "im2col")
-    y = mm(cols, W, B * Tout, Cout, Cin * k, tb=1, bias=b, rmask=out_mask).view(B, Tout, Cout)
+    y = mm(cols, W, B * Tout, Cout, Cin * k, tb=1, bias=b, rmask=out_mask, fmt=_OPFMT[0]).view(B, Tout, Cout)
     return y, (cols, B, T, Cin, k, stride, pad, dil, Tout, mask)
 
 
@@ -238,12 +258,12 @@ def conv_bwd(dy, ctx, W, gW, gb, need_dx=True):
     """-> d x (times the forward's input mask); weight / bias gradients into gW / gb"""
     cols, B, T, Cin, k, stride, pad, dil, Tout, mask = ctx
     Cout = W.shape[0]
-    gemm(dy, cols, Cout, Cin * k, B * Tout, gW, ta=1)
+    gemm(dy, cols, Cout, Cin * k, B * Tout, gW, ta=1, fmt=_OPFMT[0])
     if gb is not None:
         colsum(dy, Cout, gb)
     if not need_dx:
         return None
-    dcols = mm(dy, W, B * Tout, Cin * k, Cout)
+    dcols = mm(dy, W, B * Tout, Cin * k, Cout, fmt=_OPFMT[0])
     dx = empty(B, T, Cin, like=dy)
     check(lib().mtt_col2im(dcols.data_ptr(), ptr(mask), B, T, Cin, k, stride, pad, dil, Tout, dx.data_ptr(), 0,
                            _s(dy)), "col2im")
@@ -256,7 +276,7 @@ def convT_fwd(x, W, b, stride, pad):
     B, Tin, Cin = x.shape
     _, Cout, k = W.shape
     Tout = (Tin - 1) * stride - 2 * pad + k
-    dcols = mm(x, W, B * Tin, Cout * k, Cin)
+    dcols = mm(x, W, B * Tin, Cout * k, Cin, fmt=_OPFMT[0])
     y = empty(B, Tout, Cout, like=x)
     check(lib().mtt_col2im(dcols.data_ptr(), None, B, Tout, Cout, k, stride, pad, 1, Tin, y.data_ptr(), 0, _s(x)),
           "col2im")
@@ -270,10 +290,10 @@ def convT_bwd(dy, ctx, W, gW, gb):
     cols = empty(B * Tin, Cout * k, like=dy)
     check(lib().mtt_im2col(dy.data_ptr(), None, B, Tout, Cout, k, stride, pad, 1, Tin, cols.data_ptr(), _s(dy)),
           "im2col")
-    gemm(x, cols, Cin, Cout * k, B * Tin, gW, ta=1)
+    gemm(x, cols, Cin, Cout * k, B * Tin, gW, ta=1, fmt=_OPFMT[0])
     if gb is not None:
         colsum(dy, Cout, gb)
-    return mm(cols, W, B * Tin, Cin, Cout * k, tb=1).view(B, Tin, Cin)
+    return mm(cols, W, B * Tin, Cin, Cout * k, tb=1, fmt=_OPFMT[0]).view(B, Tin, Cin)
 
 
 def ln_fwd(x, g, b, eps):
@@ -334,7 +354,7 @@ def attention_fwd(q, k, v, kmask, qmask, H, dh, scale, mode, p_drop=0.0, seed=0)
     S = empty(B * H, T, T, like=q)
     for h in range(H):
         gemm(q, k, T, T, dh, S, tb=1, lda=D, ldb=D, ldc=T, batch=B, sA=T * D, sB=T * D, sC=H * T * T, a_off=h * dh,
-             b_off=h * dh, c_off=h * T * T)
+             b_off=h * dh, c_off=h * T * T, fmt=_OPFMT[0])
     P = empty(B * H, T, T, like=q)
     check(lib().mtt_softmax_fwd(S.data_ptr(), kmask.data_ptr(), ptr(qmask), B * H, H, T, T, float(scale), mode,
                                 P.data_ptr(), _s(q)), "softmax")
@@ -343,7 +363,7 @@ def attention_fwd(q, k, v, kmask, qmask, H, dh, scale, mode, p_drop=0.0, seed=0)
     o = empty(B, T, D, like=q)
     for h in range(H):
         gemm(Pd, v, T, dh, T, o, lda=T, ldb=D, ldc=D, batch=B, sA=H * T * T, sB=T * D, sC=T * D, a_off=h * T * T,
-             b_off=h * dh, c_off=h * dh)
+             b_off=h * dh, c_off=h * dh, fmt=_OPFMT[0])
     return o, (q, k, v, P, Pd, kmask, qmask, H, dh, scale, p_drop, seed)
 
 
@@ -354,18 +374,18 @@ def attention_bwd(do, ctx):
     dq, dk, dv = like_(q), like_(q), like_(q)
     for h in range(H):
         gemm(do, v, T, T, dh, dPd, tb=1, lda=D, ldb=D, ldc=T, batch=B, sA=T * D, sB=T * D, sC=H * T * T,
-             a_off=h * dh, b_off=h * dh, c_off=h * T * T)
+             a_off=h * dh, b_off=h * dh, c_off=h * T * T, fmt=_OPFMT[0])
         gemm(Pd, do, T, dh, T, dv, ta=1, lda=T, ldb=D, ldc=D, batch=B, sA=H * T * T, sB=T * D, sC=T * D,
-             a_off=h * T * T, b_off=h * dh, c_off=h * dh)
+             a_off=h * T * T, b_off=h * dh, c_off=h * dh, fmt=_OPFMT[0])
     dP = dropout(dPd, p_drop, seed)
     dS = like_(P)
     check(lib().mtt_softmax_bwd(P.data_ptr(), dP.data_ptr(), kmask.data_ptr(), ptr(qmask), B * H, H, T, T,
                                 float(scale), dS.data_ptr(), _s(q)), "softmax_bwd")
     for h in range(H):
         gemm(dS, k, T, dh, T, dq, lda=T, ldb=D, ldc=D, batch=B, sA=H * T * T, sB=T * D, sC=T * D, a_off=h * T * T,
-             b_off=h * dh, c_off=h * dh)
+             b_off=h * dh, c_off=h * dh, fmt=_OPFMT[0])
         gemm(dS, q, T, dh, T, dk, ta=1, lda=T, ldb=D, ldc=D, batch=B, sA=H * T * T, sB=T * D, sC=T * D,
-             a_off=h * T * T, b_off=h * dh, c_off=h * dh)
+             a_off=h * T * T, b_off=h * dh, c_off=h * dh, fmt=_OPFMT[0])
     return dq, dk, dv
 
 
@@ -815,11 +835,18 @@ class MatchaTrainer:
     def __init__(self, state: Dict[str, torch.Tensor], hp: dict, device, lr: float = 1e-4, sigma_min: float = 1e-4,
                  prior_loss: bool = True, dropout: bool = True, grad_clip: float = 5.0, heads: int = 2,
                  process_group=None, bucket_bytes: int = 25 << 20, seed: int = 0,
-                 p_dropout: Optional[Dict[str, float]] = None):
+                 p_dropout: Optional[Dict[str, float]] = None, precision: str = "32"):
         """p_dropout: the configs' rates {"encoder", "duration_predictor", "decoder"} (train_standalone.py:772-800:
         encoder_params.p_dropout, duration_predictor_params.p_dropout, decoder_params.dropout; defaults 0.1 / 0.1 /
         0.05); the prenet's 0.5 is fixed in the reference (model.py:481). On a DDP group (world > 1) rank 0's
-        parameters are broadcast at construction, as DistributedDataParallel does when it wraps the module."""
+        parameters are broadcast at construction, as DistributedDataParallel does when it wraps the module.
+
+        precision: Lightning's Trainer precision (train_standalone.py:868 trains with "16-mixed"). "32": exact fp32
+        MFMA everywhere. "16-mixed": every conv / linear / attention product, forward and backward, on fp16-rounded
+        operands (16-bit MFMA, fp32 sums), with torch.cuda.amp.GradScaler's dynamic loss scale (init 2^16, x0.5
+        and the step skipped on an inf / NaN gradient, x2 after 2000 finite steps); "bf16-mixed": bf16 operands, no
+        scaler. Activations, norms, softmax, losses and the Adam state stay fp32 in every mode; the log-prior / MAS
+        products and the alignment GEMMs (0/1 attn) stay exact fp32."""
         if int(hp.get("n_spks", 1)) > 1:
             raise NotImplementedError("multi-speaker training (spk_emb conditioning) is not built")
         names = [k for k, v in state.items() if k.startswith(("encoder.", "decoder.estimator."))
@@ -847,8 +874,14 @@ class MatchaTrainer:
         self.p_dropout = pd
         self.set_dropout(dropout)
         self.lr, self.sigma_min, self.prior, self.clip = lr, sigma_min, prior_loss, grad_clip
-        self.step_count, self.seed = 0, seed
+        self.step_count, self.seed, self.calls = 0, seed, 0
         self.last: Dict[str, torch.Tensor] = {}
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision {precision!r}: one of {sorted(PRECISIONS)}")
+        self.precision, self.opfmt = precision, PRECISIONS[precision]
+        # torch.cuda.amp.GradScaler defaults (Lightning's MixedPrecision plugin for "16-mixed")
+        self.scaler = {"scale": 65536.0, "growth_factor": 2.0, "backoff_factor": 0.5, "growth_interval": 2000,
+                       "_growth_tracker": 0} if self.opfmt == 1 else None
 
     def set_dropout(self, enabled: bool):
         """train (True: the configured rates, train_standalone.py:775-800, and the prenet's fixed 0.5, model.py:481)
@@ -872,7 +905,10 @@ class MatchaTrainer:
 
     def optimizer_state(self) -> Dict[str, object]:
         """Adam's exp_avg / exp_avg_sq (flat, parameter order of ``self.grads.names``), step count and lr"""
-        return {"exp_avg": self.m, "exp_avg_sq": self.v, "step": self.step_count, "lr": self.lr}
+        st = {"exp_avg": self.m, "exp_avg_sq": self.v, "step": self.step_count, "lr": self.lr}
+        if self.scaler is not None:  # GradScaler.state_dict() keys
+            st["scaler"] = dict(self.scaler)
+        return st
 
     @torch.no_grad()
     def load_optimizer_state(self, st: Dict[str, object]):
@@ -880,6 +916,8 @@ class MatchaTrainer:
         self.v.copy_(st["exp_avg_sq"])
         self.step_count = int(st["step"])
         self.lr = float(st.get("lr", self.lr))
+        if self.scaler is not None and st.get("scaler"):
+            self.scaler.update({k: st["scaler"][k] for k in self.scaler if k in st["scaler"]})
 
     def gradients(self) -> Dict[str, torch.Tensor]:
         return dict(self.grads.view)
@@ -908,8 +946,17 @@ class MatchaTrainer:
         if z is None:
             z = torch.randn_like(y)
         t, z = t.reshape(B).to(torch.float32).contiguous(), z.to(torch.float32).contiguous()
-        seed = ((self.seed * 1000003 + self.step_count) * 256) & 0xFFFFFFFF
+        # dropout streams advance per call (a step the loss scaler skips does not reuse its masks)
+        seed = ((self.seed * 1000003 + self.calls) * 256) & 0xFFFFFFFF
+        self.calls += 1
         self.buckets.reset()
+        with operand_format(self.opfmt):
+            return self._forward_backward(x, xl, y, yl, t, z, seed, backward)
+
+    def _forward_backward(self, x, xl, y, yl, t, z, seed, backward):
+        B, Tx = x.shape
+        F, Ty = y.shape[1], y.shape[2]
+        S = self.scaler["scale"] if self.scaler else 1.0  # the loss scale seeds the backward
         # ---- forward
         mu_x, logw, xm, ectx = self.enc.forward(x, xl, seed)
         ym = seq_mask(yl, Ty, y)
@@ -932,7 +979,7 @@ class MatchaTrainer:
         inv_n80 = ew(RECIP, empty(1, like=y), n80, alpha=1.0)
         diff = add(pred, u_t, beta=-1.0)
         cfm = mul_scalar(total(diff, diff), inv_n80)
-        dpred = mul_scalar(diff, inv_n80, alpha=2.0)
+        dpred = mul_scalar(diff, inv_n80, alpha=2.0 * S)
         # prior loss (train_standalone.py:661-663)
         ymu = add(y_btc, mu_y, beta=-1.0)
         if self.prior:
@@ -946,7 +993,7 @@ class MatchaTrainer:
         dl = add(logw, lw_, beta=-1.0)
         inv_nx = ew(RECIP, empty(1, like=y), total(xm), alpha=1.0)
         dur = mul_scalar(total(dl, dl), inv_nx)
-        dlogw = mul_scalar(dl, inv_nx, alpha=2.0)
+        dlogw = mul_scalar(dl, inv_nx, alpha=2.0 * S)
         if not backward:
             loss = add(add(dur, prior), cfm)
             self.last = {"loss": loss, "dur_loss": dur, "prior_loss": prior, "cfm_loss": cfm, "attn": attn,
@@ -955,7 +1002,7 @@ class MatchaTrainer:
         # ---- backward
         dmu_y = self.est.backward(dpred, dctx, Grads(self.grads, "decoder.estimator.", self.buckets))
         if self.prior:
-            add(dmu_y, mul_scalar(mul_rows(ymu, ym, alpha=-1.0), inv_n80), out=dmu_y)
+            add(dmu_y, mul_scalar(mul_rows(ymu, ym, alpha=-S), inv_n80), out=dmu_y)
         dmu_x = empty(B, Tx, F, like=y)
         gemm(attn, dmu_y, Tx, F, Ty, dmu_x, batch=B, sA=Tx * Ty, sB=Ty * F, sC=Tx * F)
         self.enc.backward(dmu_x, dlogw, ectx, Grads(self.grads, "encoder.", self.buckets))
@@ -966,15 +1013,32 @@ class MatchaTrainer:
         return self.last
 
     def optimizer_step(self):
-        """gradient_clip_val 5.0 (norm of the world-averaged gradient) then torch.optim.Adam (lr, defaults)."""
-        self.step_count += 1
+        """gradient_clip_val 5.0 (norm of the world-averaged gradient) then torch.optim.Adam (lr, defaults).
+        "16-mixed": the gradient holds loss-scale x the true one; the unscale is folded into the clip factor, and an
+        inf / NaN anywhere (the all-reduced buffer is the same on every rank) skips the update and halves the scale
+        (GradScaler.unscale_ / step / update; its found-inf check syncs with the host, as here)."""
         g = self.grads.flat
         scale, sumsq = empty(2, like=g), total(g, g)
-        check(lib().mtt_clip_factor(sumsq.data_ptr(), float(self.clip), 1.0 / self.world, scale.data_ptr(),
+        S = self.scaler["scale"] if self.scaler else 1.0
+        if self.scaler is not None:
+            sc = self.scaler
+            if not math.isfinite(sumsq.item()):
+                sc["scale"] *= sc["backoff_factor"]
+                sc["_growth_tracker"] = 0
+                self.last["grad_norm"] = sumsq.sqrt()
+                self.last["skipped"] = True
+                return self.last
+            sc["_growth_tracker"] += 1
+            if sc["_growth_tracker"] == sc["growth_interval"]:
+                sc["scale"] *= sc["growth_factor"]
+                sc["_growth_tracker"] = 0
+        self.step_count += 1
+        check(lib().mtt_clip_factor(sumsq.data_ptr(), float(self.clip), 1.0 / (self.world * S), scale.data_ptr(),
                                     scale[1:].data_ptr(), _s(g)), "clip_factor")
         check(lib().mtt_adam(self.params.flat.data_ptr(), g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), g.numel(),
                              scale.data_ptr(), float(self.lr), 0.9, 0.999, 1e-8, self.step_count, _s(g)), "adam")
         self.last["grad_norm"] = scale[1:]
+        self.last["skipped"] = False
         return self.last
 
     def training_step(self, batch: dict):

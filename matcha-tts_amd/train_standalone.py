@@ -137,7 +137,7 @@ class MatchaLightningModule(torch.nn.Module):
 
     def __init__(self, n_vocab, n_spks, spk_emb_dim, encoder_params, decoder_params, cfm_params,
                  duration_predictor_params, data_statistics, learning_rate=1e-4, prior_loss=True,
-                 process_group=None):
+                 process_group=None, precision="32"):
         super().__init__()
         if n_spks > 1:
             raise NotImplementedError("multi-speaker training (spk_emb conditioning) is not built")
@@ -159,6 +159,9 @@ class MatchaLightningModule(torch.nn.Module):
         self.model.mel_mean = self.mel_mean
         self.model.mel_std = self.mel_std
         self.process_group = process_group
+        # the reference sets this on pl.Trainer (precision="16-mixed", train_standalone.py:868); the engine lives
+        # here, so the module takes it: "32", "16-mixed" (fp16 operands + dynamic loss scale) or "bf16-mixed"
+        self.precision = str(precision)
         self._tr: Optional[MatchaTrainer] = None
         self._fp = None  # (address, version) of the model's tensors when the trainer last matched them
         self._pending_opt: Optional[_FusedAdam] = None  # an optimizer state loaded before the engine existed
@@ -179,7 +182,8 @@ class MatchaLightningModule(torch.nn.Module):
             rt.require_gpu(self.mel_mean, what="MatchaLightningModule")
             self._tr = MatchaTrainer(self.model.state_dict(), self.hp, dev, lr=self.learning_rate,
                                      sigma_min=self.sigma_min, prior_loss=self.prior_loss, heads=self.heads,
-                                     process_group=self.process_group, p_dropout=self.p_dropout)
+                                     process_group=self.process_group, p_dropout=self.p_dropout,
+                                     precision=self.precision)
             if self._tr.world > 1:
                 self._sync_model()  # the ranks' modules hold rank 0's weights, as under DDP
             self._fp = self._model_fp()

@@ -53,6 +53,35 @@ def test_gemm_f32(ta, tb, M, N, K, batch):
     assert _rel(out, ref) < 2e-6
 
 
+@pytest.mark.parametrize("fmt,dt", [(1, torch.float16), (2, torch.bfloat16)])
+@pytest.mark.parametrize("ta,tb,M,N,K,batch", [(0, 0, 70, 33, 19, 1), (1, 0, 64, 64, 100, 3), (0, 1, 5, 130, 64, 2),
+                                               (1, 1, 17, 9, 3, 1), (0, 0, 300, 260, 132, 2),
+                                               (1, 0, 40, 70, 5000, 1), (0, 1, 200, 96, 3001, 1)])
+def test_gemm_16bit_operands(fmt, dt, ta, tb, M, N, K, batch):
+    """the mixed-precision GEMM ("16-mixed" fp16 / "bf16-mixed" bf16 operands, fp32 sums and fp32 output): equal,
+    up to fp32 summation order, to the fp64 product of the RNE-rounded operands (autocast's matmul arithmetic
+    without its 16-bit output rounding), on the same shapes, epilogue and split-K cases as the fp32 GEMM"""
+    tr = _tr()
+    g = torch.Generator().manual_seed(M * N + K + fmt)
+    A = torch.randn(batch, *((K, M) if ta else (M, K)), generator=g) * 3.0
+    B = torch.randn(batch, *((N, K) if tb else (K, N)), generator=g)
+    C0 = torch.randn(batch, M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    rmask = (torch.rand(batch, M, generator=g) > 0.3).float()
+    out = C0.clone().to(DEV)
+    tr.gemm(A.to(DEV), B.to(DEV), M, N, K, out, ta=ta, tb=tb, alpha=0.5, beta=-1.0, batch=batch,
+            sA=A[0].numel(), sB=B[0].numel(), sC=M * N, bias=bias.to(DEV), rmask=rmask.to(DEV), fmt=fmt)
+    Ar, Br = A.to(dt).double(), B.to(dt).double()
+    Ad = Ar.transpose(1, 2) if ta else Ar
+    Bd = Br.transpose(1, 2) if tb else Br
+    ref = (0.5 * Ad @ Bd - C0.double() + bias.double()) * rmask.double()[:, :, None]
+    assert _rel(out, ref) < 2e-6
+    # and it is not the fp32 product: the operand rounding is visible
+    exact = (0.5 * (A.double().transpose(1, 2) if ta else A.double()) @ (B.double().transpose(1, 2) if tb
+             else B.double()) - C0.double() + bias.double()) * rmask.double()[:, :, None]
+    assert _rel(out, exact) > 1e-5
+
+
 @pytest.mark.parametrize("k,stride,pad,dil", [(3, 1, 1, 1), (3, 2, 1, 1), (5, 1, 2, 1), (3, 1, 2, 2), (1, 1, 0, 1)])
 def test_conv_fwd_bwd(k, stride, pad, dil):
     tr = _tr()

@@ -2,7 +2,7 @@
 (train_standalone.py:760), LJSpeech-like lengths (mel frames ~ N(566, 150), text 150-250 tokens), synthetic
 weights and data. Prints one JSON line: ms/step, mel frames/s, peak memory, and the per-phase split.
 
-    python tools/train_bench.py [--batch 64] [--steps 5] [--warmup 2] [--no-dropout]
+    python tools/train_bench.py [--batch 64] [--steps 5] [--warmup 2] [--no-dropout] [--precision 32|16-mixed|bf16-mixed]
 """
 import argparse
 import json
@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-dropout", action="store_true")
+    ap.add_argument("--precision", default="32")
     a = ap.parse_args()
     from conftest import HP, make_matcha
     from matcha_hip import synthetic
@@ -39,7 +40,7 @@ def main():
     x = torch.randint(1, 178, (B, Tx), generator=g) * (torch.arange(Tx)[None] < xl[:, None])
     y = torch.randn(B, 80, Ty, generator=g) * (torch.arange(Ty)[None, None] < yl[:, None, None])
     args = [t.to(dev) for t in (x, xl, y, yl)]
-    tr = MatchaTrainer(sd, HP, dev, dropout=not a.no_dropout)
+    tr = MatchaTrainer(sd, HP, dev, dropout=not a.no_dropout, precision=a.precision)
     for _ in range(a.warmup):
         tr.forward_backward(*args)
         tr.optimizer_step()
@@ -55,7 +56,8 @@ def main():
     print(json.dumps({"what": "cfm_training_step", "batch": B, "Tx": Tx, "Ty": Ty, "mel_frames": frames,
                       "ms_per_step": round(ms, 2), "mel_frames_per_s": round(frames / ms * 1e3, 1),
                       "params": int(tr.params.flat.numel()), "peak_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2),
-                      "loss": round(float(tr.last["loss"]), 4), "dropout": not a.no_dropout}))
+                      "loss": round(float(tr.last["loss"]), 4), "dropout": not a.no_dropout,
+                      "precision": a.precision, "loss_scale": tr.scaler["scale"] if tr.scaler else None}))
 
 
 if __name__ == "__main__":
