@@ -74,6 +74,10 @@ struct VConvArgs {
   // 1: fp32 operands and output (x, w, y, resid, trash hold floats; w is the vconv_repack_f32 image); epilogues
   // 0 / VE_RELU / VE_MASK / VE_RESID and their combinations only; one source, plain [B][L][M] output
   int f32;
+  // diagnostic builds (-DVCONV_TS) only: per-workgroup phase timestamps (s_memrealtime, 100 MHz) of this launch go
+  // to ts[(ts_slot * 256 + workgroup) * 4 + 0..3]; set by launch_vconv, unused otherwise
+  unsigned long long* ts;
+  int ts_slot;
 };
 
 // LayerNorm (mean, rstd) of a 256-channel frame from its 4 slab partials (mean_i, M2_i), 64 values each,

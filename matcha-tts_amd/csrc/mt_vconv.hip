@@ -130,6 +130,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
   const int Q = nmine * S;
   if (Q == 0) return;
+#if defined(VCONV_TS)
+  unsigned long long ts_v[4] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0};
+#endif
   // per-channel epilogue tables in LDS (one array with the staging images: a second __shared__ object
   // costs vmcnt(0) waits)
   for (int i = tid; i < a.M; i += NT) {
@@ -592,6 +595,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   int mWb = NWSLOT > 3 ? stage_w() : 0;      // ... of step qq+2 (ring of 4)
   wait_vmcnt(issued - max(m0w, pop_x()));
   raw_barrier();
+#if defined(VCONV_TS)
+  ts_v[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   Frag F0, F1;  // F0: slice 0 of the step being computed (read one step ahead), F1: its slice 1
   read_frag(F0, 0, 0, 0, 0);
 
@@ -629,6 +635,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       if (++ub == NXB) ub = 0;
       if (++c == nch) {
         c = 0;
+#if defined(VCONV_TS)
+        if (ti == 0) ts_v[2] = __builtin_amdgcn_s_memrealtime();
+#endif
         epilogue(ti);
         issued += NST;  // its stores join the counted VMEM stream
 #pragma unroll
@@ -641,6 +650,12 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   }
 #if defined(VCONV_EXP)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+#if defined(VCONV_TS)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores have landed
+  __syncthreads();
+  ts_v[3] = __builtin_amdgcn_s_memrealtime();
+  if (a.ts && tid < 4) a.ts[((size_t)a.ts_slot * 256 + blockIdx.x) * 4 + tid] = ts_v[tid];
 #endif
 }
 
@@ -802,6 +817,21 @@ int vconv_gn_parts_max(int L) { return (L + 127) / 128 * 4; }
 // VE_GNRES: a wave's 64 (or 32) frames must span at most 8 utterances (its GN table holds 16 pairs)
 int vconv_gnres_min_frames() { return 10; }
 
+#if defined(VCONV_TS)
+// diagnostic: phase timestamps of the last TS_SLOTS launches (see VConvArgs::ts); meta per slot = the vclog record
+constexpr int TS_SLOTS = 4096;
+static unsigned long long* g_ts = nullptr;
+static int g_ts_next = 0;
+static int g_ts_meta[TS_SLOTS][VCLOG_FIELDS];
+static void ts_assign(VConvArgs& a, const int* rec) {
+  if (!g_ts && hipMalloc(&g_ts, sizeof(unsigned long long) * TS_SLOTS * 256 * 4) != hipSuccess) g_ts = nullptr;
+  a.ts = g_ts;
+  a.ts_slot = g_ts_next % TS_SLOTS;
+  for (int i = 0; i < VCLOG_FIELDS; ++i) g_ts_meta[a.ts_slot][i] = rec[i];
+  ++g_ts_next;
+}
+#endif
+
 // fp32 operands (mt_encoder): one launch of the F32 kernel; tiles of BM = 128 rows when C_out % 128 == 0, else 64,
 // and 128 frames (k >= 2: 64-row tiles hold 384 / 128 frames as in bf16; 1x1: the cost model's 128 / 192 / 256)
 static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
@@ -833,6 +863,9 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
   {
     const int rec[VCLOG_FIELDS] = {ef | (1 << 20), BM, bn, (int)k1, (int)ntiles, G, a.taps, a.M, a.cin, a.B, a.L};
     vclog_record(rec);
+#if defined(VCONV_TS)
+    ts_assign(a, rec);
+#endif
   }
 #define MT_F32CASE(E)                                                                                              \
   case E:                                                                                                          \
@@ -859,6 +892,7 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }
+
 
 int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(a0.x && a0.w && a0.bias && a0.y && a0.zero && a0.trash, "vconv: null pointer");
@@ -950,6 +984,9 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
     const int bn = k1 ? tf1 : (BM == 64 ? (bm64_128 ? 128 : 384) : tf);
     const int rec[VCLOG_FIELDS] = {ef, BM, bn, (int)k1, (int)ntiles, G, a.taps, a.M, a.cin, a.B, a.L};
     vclog_record(rec);
+#if defined(VCONV_TS)
+    ts_assign(a, rec);
+#endif
   }
   const double flops = 2.0 * a.M * a.cin * a.taps * (double)a.B * a.Lout;
   // algorithmic bytes by SURVEY.md §8d's layer-boundary definition: the conv reads its input once and writes
@@ -1030,3 +1067,19 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
 }
 
 }  // namespace mt
+
+#if defined(VCONV_TS)
+// diagnostic export (not in include/matcha_hip.h; only the -DVCONV_TS build has it): copies the timestamps and the
+// per-launch records of the launches since the last call (at most TS_SLOTS); returns their count
+extern "C" int mt_vconv_ts_dump(unsigned long long* ts, int* meta, int max_slots) {
+  const int n = std::min(std::min(mt::g_ts_next, mt::TS_SLOTS), max_slots);
+  if (n > 0 && mt::g_ts) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpy(ts, mt::g_ts, sizeof(unsigned long long) * n * 256 * 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < mt::VCLOG_FIELDS; ++j) meta[i * mt::VCLOG_FIELDS + j] = mt::g_ts_meta[i][j];
+  }
+  mt::g_ts_next = 0;
+  return n;
+}
+#endif
