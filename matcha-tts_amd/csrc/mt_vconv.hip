@@ -134,7 +134,24 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   unsigned long long ts_v[4] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0};
 #endif
   // per-channel epilogue tables in LDS (one array with the staging images: a second __shared__ object
-  // costs vmcnt(0) waits)
+  // costs vmcnt(0) waits). With 16-byte aligned tables (every packed weight blob) they arrive by LDS-DMA issued
+  // ahead of the prologue's staging (below), so their latency overlaps it; else by VGPR loads and a barrier.
+  const float* tabs[6];
+  int toff[6], ntab = 0;
+  tabs[ntab] = a.bias, toff[ntab++] = BIAS_OFF;
+  if constexpr ((EF & VE_LN) != 0) tabs[ntab] = a.wsum, toff[ntab++] = WSUM_OFF;
+  if constexpr ((EF & VE_SNAKE) != 0) {
+    tabs[ntab] = a.snake_alpha, toff[ntab++] = SNAKE_OFF;
+    tabs[ntab] = a.snake_ibeta, toff[ntab++] = SNAKE_OFF + MMAX * 4;
+  }
+  if constexpr ((EF & VE_GNRES) != 0) {
+    tabs[ntab] = a.gn_gamma, toff[ntab++] = GNP_OFF;
+    tabs[ntab] = a.gn_beta, toff[ntab++] = GNP_OFF + MMAX * 4;
+  }
+  uintptr_t tor = 0;
+  for (int i = 0; i < ntab; ++i) tor |= reinterpret_cast<uintptr_t>(tabs[i]);
+  const bool tab_dma = (tor & 15) == 0;
+  if (!tab_dma) {
   for (int i = tid; i < a.M; i += NT) {
     reinterpret_cast<float*>(smem + BIAS_OFF)[i] = a.bias[i];
     if constexpr ((EF & VE_LN) != 0) reinterpret_cast<float*>(smem + WSUM_OFF)[i] = a.wsum[i];
@@ -148,6 +165,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     }
   }
   __syncthreads();
+  }
 
   auto tile_of = [&](int ti, int& b, int& n0, int& m0) {
     const int tile = gl + ti * G;
@@ -587,7 +605,20 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     __builtin_amdgcn_sched_group_barrier(0x008, NMF - NR, 0);
   };
 
-  // ---- prologue: rows of chunks 0 .. NXB-2, weights of steps 0..2, K-slice 0 of step 0 ----
+  // ---- prologue: (the tables,) rows of chunks 0 .. NXB-2, weights of steps 0..2, K-slice 0 of step 0 ----
+  if (tab_dma) {
+    // 1 KiB per wave-instruction (lane-linear), instructions dealt round-robin over the waves; lanes past the
+    // table's end read the zero page. Loads retire in order, so the first counted wait covers them.
+    const int per = (a.M * 4 + 1023) >> 10;
+    for (int j = wave; j < ntab * per; j += 8) {
+      const int ti = j / per, part = j - ti * per;
+      const int byte = part * 1024 + lane * 16;
+      const char* src = byte < a.M * 4 ? reinterpret_cast<const char*>(tabs[ti]) + byte
+                                       : reinterpret_cast<const char*>(a.zero) + (lane & 7) * 16;
+      glds16(src, smem + toff[ti] + part * 1024);
+      ++issued;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NXB - 1; ++i) stage_x();
   const int m0w = stage_w();

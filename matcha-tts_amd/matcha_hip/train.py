@@ -905,7 +905,7 @@ class MatchaTrainer:
 
     def optimizer_state(self) -> Dict[str, object]:
         """Adam's exp_avg / exp_avg_sq (flat, parameter order of ``self.grads.names``), step count and lr"""
-        st = {"exp_avg": self.m, "exp_avg_sq": self.v, "step": self.step_count, "lr": self.lr}
+        st = {"exp_avg": self.m, "exp_avg_sq": self.v, "step": self.step_count, "lr": self.lr, "calls": self.calls}
         if self.scaler is not None:  # GradScaler.state_dict() keys
             st["scaler"] = dict(self.scaler)
         return st
@@ -915,6 +915,8 @@ class MatchaTrainer:
         self.m.copy_(st["exp_avg"])
         self.v.copy_(st["exp_avg_sq"])
         self.step_count = int(st["step"])
+        # the dropout stream's position (one per forward_backward call; a step the scaler skipped still advanced it)
+        self.calls = int(st["calls"]) if st.get("calls") is not None else self.step_count
         self.lr = float(st.get("lr", self.lr))
         if self.scaler is not None and st.get("scaler"):
             self.scaler.update({k: st["scaler"][k] for k in self.scaler if k in st["scaler"]})

@@ -102,7 +102,9 @@ class _FusedAdam:
                 shape = tr.params.view[n].shape
                 state[i] = {"step": torch.tensor(float(st["step"])), "exp_avg": m_view[n].view(shape).clone(),
                             "exp_avg_sq": v_view[n].view(shape).clone()}
-        groups = [dict(self.param_groups[0], params=list(range(len(self._index()))))]
+        # the engine's dropout-stream position rides in the param group (torch's Adam keeps only hyper-parameters
+        # there; an extra key is carried through load_state_dict unchanged)
+        groups = [dict(self.param_groups[0], params=list(range(len(self._index()))), dropout_calls=int(st["calls"]))]
         return {"state": state, "param_groups": groups}
 
     def load_state_dict(self, sd):
@@ -128,7 +130,8 @@ class _FusedAdam:
             v[o:o + k].copy_(st["exp_avg_sq"].reshape(-1))
             step = int(float(st["step"]))
         tr.load_optimizer_state({"exp_avg": m, "exp_avg_sq": v, "step": step,
-                                 "lr": self.param_groups[0]["lr"]})
+                                 "lr": self.param_groups[0]["lr"],
+                                 "calls": sd["param_groups"][0].get("dropout_calls")})
 
 
 class MatchaLightningModule(torch.nn.Module):
