@@ -10,7 +10,10 @@ synchronize brackets the timed region and the MAX over ranks is reported.
 One step = the reference's text->wav call sequence on a batch (main.py:181-198 plus the
 notebook denoiser, MOS_audiou_generator.ipynb:277): ``MatchaTTS.synthesize`` (HIP text encoder +
 duration predictor in fp32, HIP duration/alignment path, HIP CFM 10-step Euler U-Net solver in bf16,
-denormalize) -> ``Generator(mel).clamp(-1, 1)`` (HIP HiFi-GAN v1, bf16) -> ``Denoiser`` (HIP).
+denormalize) -> ``Generator(mel).clamp(-1, 1)`` (HIP HiFi-GAN v1, bf16) -> ``Denoiser`` (HIP). The reference
+vocodes and denoises one utterance per call on the mel `synthesize` cropped to it; the batched step does the same
+for every utterance of the batch in one launch chain (``lengths=y_lengths``: each utterance at its own length,
+identical to its one-utterance call, no columns past it computed).
 Workload (configs[1] of BASELINE.json): 32 utterances/GPU, 10 ODE steps, bf16 MFMA;
 synthetic LJSpeech-shaped text (x_len ~ U[150,251] with blanks) and synthetic weights
 with the duration head forced to 3 frames/token -> 450..753 frames each.
@@ -118,9 +121,11 @@ def reduce_over_ranks(elapsed, frames, dist, device):
 def step(m, g, den, x, xl, n_ts, denoise, spk=None):
     spks = m.spk_emb(spk) if spk is not None else None  # main.py: the speaker embedding of the requested ids
     mel, yl, attn = m.synthesize(x, xl, n_timesteps=n_ts, temperature=0.667, spks=spks, length_scale=1.0)
-    wav = g(mel).clamp(-1, 1)
+    # the reference's per-utterance vocoder + denoiser calls (main.py:198, MOS_audiou_generator.ipynb:276-277) for
+    # the whole batch: utterance b at its own yl[b] frames
+    wav = g(mel, lengths=yl).clamp(-1, 1)
     if denoise:
-        wav = den(wav.squeeze(1), strength=0.00025)
+        wav = den(wav.squeeze(1), strength=0.00025, lengths=yl)
     return mel, yl, wav
 
 
@@ -141,10 +146,11 @@ def dec_flops_per_frame_step(t_pad):
 def path_roofline(sec_per_step, y_lengths, t_pad, n_ts):
     """Whole hot path (mu_y, mask, z -> wav): the roofline time of one step's work =
     max(FLOPs / MFMA peak, layer-boundary bytes / HBM peak), the decoder on B*T_pad frames x n_ts steps
-    and the vocoder on B*T_y frames, over the measured step time. Also the verdict's useful-frames form:
+    and the vocoder on its sum(y_lengths) frames (each utterance vocoded at its own length), over the measured
+    step time. Also the verdict's useful-frames form:
     useful mel-frames/s over the bf16 HBM ceiling at T=576 (8e12 / 2,576,864 B = 3.10 M frames/s)."""
     B, t_y = len(y_lengths), max(y_lengths)
-    dec_frames, voc_frames = B * t_pad, B * t_y
+    dec_frames, voc_frames = B * t_pad, sum(y_lengths)
     flops = dec_frames * n_ts * dec_flops_per_frame_step(t_pad) + voc_frames * VOC_FLOPS_PER_FRAME
     nbytes = dec_frames * n_ts * DEC_BYTES_PER_FRAME_STEP + voc_frames * VOC_BYTES_PER_FRAME
     t_roof = max(flops / PEAK_FLOPS, nbytes / PEAK_BW)
@@ -153,7 +159,7 @@ def path_roofline(sec_per_step, y_lengths, t_pad, n_ts):
     return {"bound": "hbm" if nbytes / PEAK_BW >= flops / PEAK_FLOPS else "mfma",
             "roof_ms_per_step": round(t_roof * 1e3, 3), "frac": round(t_roof / sec_per_step, 4),
             "tflops": round(flops / sec_per_step / 1e12, 1), "hbm_gbs": round(nbytes / sec_per_step / 1e9, 1),
-            "padded_frames_per_s": round(voc_frames / sec_per_step, 1),
+            "decoder_frames_per_s": round(dec_frames / sec_per_step, 1),
             "useful_frames_per_s": round(useful, 1), "ceiling_frames_per_s_T576": round(ceiling, 1),
             "useful_frac_of_ceiling": round(useful / ceiling, 4), "padding_efficiency": round(sum(y_lengths) / dec_frames, 4),
             "scope": "hot path (decoder n_ts steps + vocoder); encoder and denoiser excluded as in SURVEY §8d"}
@@ -165,7 +171,7 @@ def _latest_profile(name):
     return files[-1] if files else None
 
 
-def roofline_by_kernel(detail):
+def roofline_by_kernel(detail, frame_scale=1.0):
     """The family's launches split by kernel (mt_vconv: stage 1 and stage 2's k = 7 / 11 resblocks per layer;
     mt_vpair128: stage 2's k = 3 resblock as fused pairs; mt_vpair / mt_vpair32: stage 3 / 4
     pairs, priced as their two convs): mean launch ms, algorithmic rate on both sides and the fraction of the
@@ -176,8 +182,8 @@ def roofline_by_kernel(detail):
         if not ls:
             continue
         ms = sum(d["ms"] for d in ls)
-        fl = sum(d["flops"] for d in ls)
-        by = sum(d["bytes"] for d in ls)
+        fl = sum(d["flops"] for d in ls) * frame_scale
+        by = sum(d["bytes"] for d in ls) * frame_scale
         tf, gbs = fl / (ms * 1e-3) / 1e12, by / (ms * 1e-3) / 1e9
         mfma = fl / by >= PEAK_FLOPS / PEAK_BW
         out[kind] = {"launches": len(ls), "launch_ms": round(ms / len(ls), 4), "tflops": round(tf, 1),
@@ -187,7 +193,7 @@ def roofline_by_kernel(detail):
     return out
 
 
-def roofline(probe, default_workload=True):
+def roofline(probe, default_workload=True, frame_scale=1.0):
     """Dominant kernel family of the step: the LDS-DMA persistent implicit-GEMM convs that run every ResBlock
     conv of HiFi-GAN (51 launches per step): per layer on mt_vconv, stage 1 and stage 2's k = 7 / 11 resblocks
     (30 convs; C = 256/128 on B x 8/64 * T_y frames); as fused conv pairs, stage 2's k = 3 resblock on
@@ -198,7 +204,10 @@ def roofline(probe, default_workload=True):
     algorithmic bytes = layer-boundary bytes 2 * B * L * (C_in + C_out) (bf16 input read once, output
     written once) + weights. The family's intensity decides the bound against the bf16 ridge (2.5 PFLOP/s /
     8 TB/s = 312.5 FLOP/B). `roof_frac` = the summed per-launch roofline time max(F/P_mfma, B/P_hbm) over
-    the measured time. `traffic` = HBM bytes per launch from rocprofv3 FETCH_SIZE (x2, gfx950 correction)
+    the measured time. The launches run ragged (each utterance at its own length): the host prices a launch on
+    the padded B x L, so FLOPs, bytes and roof time are scaled by frame_scale = sum(y_lengths) / (B x T_y), the
+    frames actually computed (the weight bytes, < 0.1 % of a launch's, scale with them).
+    `traffic` = HBM bytes per launch from rocprofv3 FETCH_SIZE (x2, gfx950 correction)
     + WRITE_SIZE on this same bench command (profiles/rNN_pmc_vconv.json), `traffic_ratio` = traffic /
     algorithmic bytes (> 1: bytes this implementation moves beyond the layer boundaries)."""
     if probe is None or probe["launches"] == 0:
@@ -206,8 +215,8 @@ def roofline(probe, default_workload=True):
                 "traffic": None, "kernel": "vconv_kernel (bf16 path only)"}
     n = probe["launches"]
     ms = probe["ms"] / n
-    flops = probe["flops"] / n
-    nbytes = probe["bytes"] / n
+    flops = probe["flops"] / n * frame_scale
+    nbytes = probe["bytes"] / n * frame_scale
     intensity = flops / nbytes
     tflops = flops / (ms * 1e-3) / 1e12
     gbs = nbytes / (ms * 1e-3) / 1e9
@@ -232,7 +241,7 @@ def roofline(probe, default_workload=True):
             "algo_bytes_per_launch": nbytes, "intensity_flop_per_byte": round(intensity, 1),
             "tflops": round(tflops, 2), "mfma_frac": round(tflops / peak_f, 4),
             "gbs": round(gbs, 1), "hbm_frac": round(gbs / peak_b, 4),
-            "roof_frac": round(probe["roof_ms"] / probe["ms"], 4)}
+            "roof_frac": round(probe["roof_ms"] * frame_scale / probe["ms"], 4), "frame_scale": round(frame_scale, 4)}
 
 
 def _cpu_info():
@@ -459,15 +468,16 @@ def main():
                                + (" (VCTK, speaker-embedding condition)" if vctk else ""),
                    "global_batch": a.batch * world, "batch_per_gpu": a.batch, "n_timesteps": a.n_timesteps,
                    "seq_len": t_pad, "frames_per_step": tot_frames, "parallelism": f"dp{world} (utterance shards)",
-                   "denoiser": denoise},
+                   "denoiser": denoise, "vocoder": "each utterance at its own length (ragged batch, = its one-utterance call)"},
         "rtf": round((el / a.steps) / audio_s, 6),
     }
     if rank == 0:
         if world == 1:
             default = (a.batch, a.n_timesteps, a.seed, a.no_denoise, a.precision, a.model) == \
                 (32, 10, 1234, False, "bf16", "lj")
-            out["roofline"] = roofline(probe, default_workload=default)
-            out["roofline"]["by_kernel"] = roofline_by_kernel(detail)
+            fs = sum(yls) / (len(yls) * max(yls))  # ragged vocoder: frames computed / padded frames priced
+            out["roofline"] = roofline(probe, default_workload=default, frame_scale=fs)
+            out["roofline"]["by_kernel"] = roofline_by_kernel(detail, frame_scale=fs)
             out["path_roofline"] = path_roofline(el / a.steps, yls, t_pad, a.n_timesteps)
             if a.quick:
                 a.no_north_star = a.no_cpu_baseline = a.no_fp32 = True

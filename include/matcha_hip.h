@@ -13,6 +13,9 @@
  *   mt_denorm_crop               <- denormalize + crop  model.py:106-125, 1295-1298
  *   mt_vocoder_forward           <- hifigan.models.Generator.forward  hifigan/models.py:181-197
  *   mt_denoise                   <- hifigan.denoiser.Denoiser.forward hifigan/denoiser.py:62-68
+ *   mt_vocoder_forward_ragged,   <- the reference pipeline's per-utterance vocoder + denoiser calls (one utterance
+ *   mt_denoise_ragged               per call, mel cropped to its y_length: main.py:181-198,
+ *                                   MOS_audiou_generator.ipynb:265-277) for a whole padded batch in one launch chain
  *   mt_maximum_path              <- train_standalone.maximum_path train_standalone.py:280-325 (MAS)
  *
  * Conventions
@@ -177,6 +180,14 @@ size_t mt_vocoder_workspace_bytes(const mt_vocoder* v, int B, int T);
 /* mel [B,80,T] fp32 -> wav [B,1,T*prod(up_rates)] fp32 */
 int mt_vocoder_forward(const mt_vocoder* v, const void* packed, const float* mel, int B, int T,
                        float* wav, void* ws, size_t ws_bytes, void* stream);
+/* Ragged batch: utterance b is vocoded at its own lens[b] mel frames (int32, device; frames past it are the
+ * zero padding a batch-1 call of that length sees), so wav[b][0, 256 lens[b]) equals Generator.forward on
+ * mel[b:b+1, :, :lens[b]] alone; wav[b] past it is zero and columns past lens[b] are not computed. Needs the bf16
+ * vconv / pair path on every stage (the defaults) and B <= 512. */
+int mt_vocoder_forward_ragged(const mt_vocoder* v, const void* packed, const float* mel, int B, int T,
+                              const int32_t* lens, float* wav, void* ws, size_t ws_bytes, void* stream);
+/* 1 when mt_vocoder_forward_ragged runs with this handle's precision and path modes, else 0 */
+int mt_vocoder_ragged_supported(const mt_vocoder* v);
 
 /* ---------------------------------------------------------------------------------------
  * Duration -> alignment index path (bit-exact given logw).
@@ -200,6 +211,10 @@ int mt_denorm_crop(const float* z, const float* mean, const float* std, int B, i
 size_t mt_denoise_workspace_bytes(int B, int L);
 int mt_denoise(const float* audio, int B, int L, const float* bias_spec, float strength, float* out,
                void* ws, size_t ws_bytes, void* stream);
+/* Ragged batch: row b denoised as an utterance of lens[b] * lmul samples (int32, device; its own reflect padding
+ * and 1 + samples / 256 frames, as a one-utterance call); out[b] past those samples is zero. */
+int mt_denoise_ragged(const float* audio, int B, int L, const int32_t* lens, int lmul, const float* bias_spec,
+                      float strength, float* out, void* ws, size_t ws_bytes, void* stream);
 /* |STFT| (same framing) of every frame: mag [B][1+L/256][513] (bias spectrum, denoiser.py:57-60) */
 int mt_stft_magnitude(const float* audio, int B, int L, float* mag, void* stream);
 

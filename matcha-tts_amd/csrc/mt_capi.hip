@@ -12,7 +12,7 @@
 namespace mt {
 const char* last_error();
 int denoise(const float* audio, int B, int L, const float* bias_spec, float strength, float* out, void* ws,
-            size_t ws_bytes, hipStream_t st);
+            size_t ws_bytes, hipStream_t st, const int* lens = nullptr, int lmul = 1);
 size_t denoise_workspace_bytes(int B, int L);
 int stft_magnitude(const float* audio, int B, int L, float* mag, hipStream_t st);
 int log_mel(const float* audio, int B, int L, const float* basis, float mean, float stdv, float* mel, hipStream_t st);
@@ -247,6 +247,14 @@ int mt_vocoder_forward(const mt_vocoder* v, const void* packed, const float* mel
   return v->v.forward(packed, mel, B, T, wav, ws, ws_bytes, (hipStream_t)stream);
 }
 
+int mt_vocoder_ragged_supported(const mt_vocoder* v) { return v && v->v.ragged_supported() ? 1 : 0; }
+
+int mt_vocoder_forward_ragged(const mt_vocoder* v, const void* packed, const float* mel, int B, int T,
+                              const int32_t* lens, float* wav, void* ws, size_t ws_bytes, void* stream) {
+  MT_REQUIRE(v && packed && mel && lens && wav && ws, "vocoder_forward_ragged: null argument");
+  return v->v.forward(packed, mel, B, T, wav, ws, ws_bytes, (hipStream_t)stream, lens);
+}
+
 // ---- index path ----
 int mt_durations(const float* logw, const float* x_mask, float length_scale, int B, int Tx, float* w_ceil,
                  float* cum, int64_t* y_lengths, void* stream) {
@@ -272,6 +280,12 @@ int mt_denoise(const float* audio, int B, int L, const float* bias_spec, float s
                size_t ws_bytes, void* stream) {
   MT_REQUIRE(audio && bias_spec && out, "denoise: null argument");
   return mt::denoise(audio, B, L, bias_spec, strength, out, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int mt_denoise_ragged(const float* audio, int B, int L, const int32_t* lens, int lmul, const float* bias_spec,
+                      float strength, float* out, void* ws, size_t ws_bytes, void* stream) {
+  MT_REQUIRE(audio && lens && bias_spec && out, "denoise_ragged: null argument");
+  return mt::denoise(audio, B, L, bias_spec, strength, out, ws, ws_bytes, (hipStream_t)stream, lens, lmul);
 }
 
 size_t mt_maximum_path_workspace_bytes(int B, int Tx, int Ty) { return mt::mas_workspace_bytes(B, Tx, Ty); }

@@ -119,13 +119,18 @@ __device__ __forceinline__ float2* fft1024_r4(float2* src, float2* scr, const fl
   return src;
 }
 
+// ragged batch (lens != null): row b is an utterance of Lb = lens[b] * lmul samples (its own reflect padding and
+// 1 + Lb / 256 frames; the rest of the row is not read), as the reference denoises one utterance per call
 __global__ __launch_bounds__(256) void stft_denoise2_kernel(const float* __restrict__ audio, int L, int nfr,
                                                             const float* __restrict__ bias, float strength,
-                                                            float* __restrict__ frames) {
+                                                            float* __restrict__ frames, const int* lens, int lmul) {
   __shared__ float2 bufA[NFFT], bufB[NFFT], tw[3 * NFFT / 4];
   const int f0 = 2 * blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const bool two = f0 + 1 < nfr;
   const float* x = audio + (size_t)b * L;
+  const int Lb = lens ? min(max(lens[b] * lmul, 0), L) : L;
+  const int nfb = lens ? (Lb > 0 ? 1 + Lb / HOP : 0) : nfr;
+  if (f0 >= nfb) return;
+  const bool two = f0 + 1 < nfb;
   for (int t = tid; t < 3 * NFFT / 4; t += 256) {
     float sn, cs;
     sincospif(2.f * (float)t / (float)NFFT, &sn, &cs);
@@ -140,7 +145,8 @@ __global__ __launch_bounds__(256) void stft_denoise2_kernel(const float* __restr
     for (int u = 0; u < 2; ++u) {
       int i = (f0 + u) * HOP + n - NFFT / 2;  // reflect padding by n_fft/2 on both sides
       if (i < 0) i = -i;
-      if (i >= L) i = 2 * (L - 1) - i;
+      if (i >= Lb) i = 2 * (Lb - 1) - i;
+      i = min(max(i, 0), Lb - 1);  // an utterance shorter than n_fft / 2 (torch's reflect pad raises there)
       v[u] = (u == 0 || two) ? x[i] * w : 0.f;
     }
     bufA[n] = float2{v[0], v[1]};
@@ -183,15 +189,24 @@ __global__ __launch_bounds__(256) void stft_denoise2_kernel(const float* __restr
 }
 
 __global__ void overlap_add_kernel(const float* __restrict__ frames, int nfr, int Lout,
-                                   float* __restrict__ out) {
+                                   float* __restrict__ out, const int* lens, int lmul, int L) {
   const int b = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= Lout) return;
+  int nfb = nfr;
+  if (lens) {  // ragged: this utterance's frames; its output ends at 256 (frames - 1) samples, zeros after
+    const int Lb = min(max(lens[b] * lmul, 0), L);
+    nfb = Lb > 0 ? 1 + Lb / HOP : 0;
+    if (i >= HOP * (nfb - 1)) {
+      out[(size_t)b * Lout + i] = 0.f;
+      return;
+    }
+  }
   const int p = i + NFFT / 2;
   int f0 = (p - NFFT + HOP) / HOP;
   if (f0 < 0) f0 = 0;
   int f1 = p / HOP;
-  if (f1 > nfr - 1) f1 = nfr - 1;
+  if (f1 > nfb - 1) f1 = nfb - 1;
   float s = 0.f, env = 0.f;
   for (int f = f0; f <= f1; ++f) {
     const int n = p - f * HOP;
@@ -209,16 +224,17 @@ size_t denoise_workspace_bytes(int B, int L) {
 }
 
 int denoise(const float* audio, int B, int L, const float* bias_spec, float strength, float* out, void* ws,
-            size_t ws_bytes, hipStream_t st) {
+            size_t ws_bytes, hipStream_t st, const int* lens, int lmul) {
   MT_REQUIRE(B > 0 && L > NFFT / 2, "denoise: need L > %d samples (reflect padding)", NFFT / 2);
   MT_REQUIRE(ws && ws_bytes >= denoise_workspace_bytes(B, L), "denoise: workspace too small");
   const int nfr = 1 + L / HOP;
   const int Lout = HOP * (nfr - 1);
+  MT_REQUIRE(!lens || lmul > 0, "denoise: length multiplier %d", lmul);
   hipLaunchKernelGGL(stft_denoise2_kernel, dim3((nfr + 1) / 2, B), dim3(256), 0, st, audio, L, nfr, bias_spec,
-                     strength, (float*)ws);
+                     strength, (float*)ws, lens, lmul);
   MT_CHECK_HIP(hipGetLastError());
   hipLaunchKernelGGL(overlap_add_kernel, dim3((Lout + 255) / 256, B), dim3(256), 0, st, (const float*)ws, nfr,
-                     Lout, out);
+                     Lout, out, lens, lmul, L);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -240,21 +240,27 @@ struct Vocoder {
   bool stage_vp32(int i) const;  // a 32-channel stage as fused pairs (mt_vpair32, generic weight packing)
   // stage i's ResBlocks as one fused-pair launch per pair: X -> XS (+ lrelu(XS) in RA when act_out)
   int pair_resblock(const char* P, int i, int j, int B, int L, const char* X, char* XS, char* Tb, char* R,
-                    char* RA, char* trash, bool act_out, hipStream_t st) const;
+                    char* RA, char* trash, bool act_out, hipStream_t st, const int* lens = nullptr) const;
   int pair_chain(const char* P, int i, int B, int L, const char* X, char* XS, char* Tb, char* R, char* RA,
-                 char* trash, bool act_out, hipStream_t st) const;
+                 char* trash, bool act_out, hipStream_t st, const int* lens = nullptr) const;
+  // frames per mel frame at the input of upsampler i (the product of the first i upsampling rates)
+  int rate_upto(int i) const;
   size_t frame_elems() const;  // max over stages of (samples per mel frame) x channels
   size_t workspace_bytes(int B, int T) const;
+  // lens (device ints, or null): ragged batch, utterance b vocoded at its own lens[b] mel frames (mt_ragged.h);
+  // its samples past 256 lens[b] are zero
   int forward(const void* packed, const float* mel, int B, int T, float* wav, void* ws, size_t ws_bytes,
-              hipStream_t st) const;
+              hipStream_t st, const int* lens = nullptr) const;
+  bool ragged_supported() const;  // every stage on the bf16 vconv / pair path
   template <class E>
-  int forward_t(const char* P, const float* mel, int B, int T, float* wav, char* ws, hipStream_t st) const;
+  int forward_t(const char* P, const float* mel, int B, int T, float* wav, char* ws, hipStream_t st,
+                const int* lens) const;
   int stage_vconv(const char* P, int i, int B, int L, const char* X, const char* XA, char* XS, char* Tb, char* R,
-                  char* RA, char* trash, bool act_out, hipStream_t st) const;
+                  char* RA, char* trash, bool act_out, hipStream_t st, const int* lens = nullptr) const;
   // upsampler i runs on vconv: its input lrelu(xs) is written by the producer (conv_pre / stage i-1)
   bool ups_vc(int i) const;
   int ups_vconv(const char* P, int i, int B, int L, const char* xa, char* X, char* XA, bool dual, char* trash,
-                hipStream_t st) const;
+                hipStream_t st, const int* lens = nullptr) const;
 };
 
 }  // namespace mt

@@ -78,6 +78,11 @@ struct VConvArgs {
   // to ts[(ts_slot * 256 + workgroup) * 4 + 0..3]; set by launch_vconv, unused otherwise
   unsigned long long* ts;
   int ts_slot;
+  // ragged batch (mt_ragged.h; k >= 2, bf16, B <= RAG_MAXB): utterance b's valid input frames are lens[b] * lmul
+  // (device ints); frames past them read as zero padding and column tiles past them are not computed. null: every
+  // utterance has L frames
+  const int* lens;
+  int lmul;
 };
 
 // LayerNorm (mean, rstd) of a 256-channel frame from its 4 slab partials (mean_i, M2_i), 64 values each,

@@ -27,6 +27,7 @@
 #include <type_traits>
 
 #include "mt_probe.h"
+#include "mt_ragged.h"
 #include "mt_vconv.h"
 
 namespace mt {
@@ -48,16 +49,24 @@ struct VT {
   static_assert(WNC % 16 == 0, "a wave covers whole 16-frame fragments");
   static constexpr int WSLOT = BM * 128;          // BM rows x 64 bf16 channels
   static constexpr int NWW = BM / 64;             // W wave-instructions per wave per step
-  static constexpr int NWSLOT = K1_ ? 3 : 4;      // weight ring (NWSLOT - 1 steps in flight)
   static constexpr int XROWS = K1_ ? TBN : TBN + 64;  // >= BN + (taps - 1) * dil (halo <= 64 rows)
   static constexpr int XBUF = XROWS * 128;
   static constexpr int NXW = XROWS / 64;          // X wave-instructions per wave per chunk
-  // row buffers: chunks staged NXB-1 ahead (the 64-row tiles with 256 frames have one chunk per tile
-  // and stage two tiles ahead; with 384 frames the buffers only fit twice)
-  static constexpr int NXB = K1_ ? 3 : (BM == 64 && TBN <= 256) ? 3 : 2;
+  static constexpr int PARB = NPAR_ * MMAX * 4 + (K1_ ? 0 : RAG_LDS);  // per-channel tables (+ the ragged tile map)
+  static constexpr int LDSMAX = 160 * 1024;
+  // Ring depths: as deep as LDS allows (the short decoder K loops are bound by the DMA latency the ring covers:
+  // NWSLOT - 1 weight steps in flight). K1: weights and rows advance together (every step is a chunk), 3..5 deep.
+  // k >= 2: row buffers hold chunks staged NXB-1 ahead (the 64-row tiles with 256 frames have one chunk per tile
+  // and stage two tiles ahead; with 384 frames the buffers only fit twice); the weight ring 4..6 deep.
+  static constexpr int K1D = (5 * (WSLOT + XBUF) + PARB <= LDSMAX) ? 5 : (4 * (WSLOT + XBUF) + PARB <= LDSMAX) ? 4 : 3;
+  static constexpr int NXB = K1_ ? K1D : (BM == 64 && TBN <= 256) ? 3 : 2;
+  static constexpr int NWSLOT = K1_ ? K1D
+                                    : (6 * WSLOT + NXB * XBUF + PARB <= LDSMAX) ? 6
+                                    : (5 * WSLOT + NXB * XBUF + PARB <= LDSMAX) ? 5 : 4;
   static constexpr int PAR_OFF = NWSLOT * WSLOT + NXB * XBUF;  // per-channel tables: bias, wsum, alpha, ibeta
-  static constexpr int LDS_BYTES = PAR_OFF + NPAR_ * MMAX * 4;
-  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+  static constexpr int RAG_OFF = PAR_OFF + NPAR_ * MMAX * 4;
+  static constexpr int LDS_BYTES = PAR_OFF + PARB;
+  static_assert(LDS_BYTES <= LDSMAX, "LDS budget");
 };
 }  // namespace
 
@@ -124,7 +133,15 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int nch = cin / CHR;
   const int S = nch * taps;
   const int ntn = (a.Lout + BN - 1) / BN, ntm = a.Mpad / BM;
-  const int ntiles = a.B * ntn * ntm;
+  // ragged batch: the live column tiles of each utterance (mt_ragged.h)
+  const bool rag = !K1 && a.lens != nullptr;
+  int* rtc = reinterpret_cast<int*>(smem + TT::RAG_OFF);
+  int* rlv = rtc + RAG_MAXB;
+  if (rag) {
+    rag_build(rtc, rlv, a.lens, a.lmul, L, a.Lout - L, a.Lout, a.B, BN, tid);
+    __syncthreads();
+  }
+  const int ntiles = rag ? rtc[a.B - 1] * ntm : a.B * ntn * ntm;
   const int G = gridDim.x, g = blockIdx.x;
   const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
   const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
@@ -171,8 +188,13 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     const int tile = gl + ti * G;
     const int r = tile / ntm;
     m0 = (tile - r * ntm) * BM;
-    b = r / ntn;
-    n0 = (r - b * ntn) * BN;
+    if (rag) {
+      b = rag_find(rtc, a.B, r);
+      n0 = (r - rag_first(rtc, b)) * BN;
+    } else {
+      b = r / ntn;
+      n0 = (r - b * ntn) * BN;
+    }
   };
 
   const int lrow = lane >> 3, lp = lane & 7;
@@ -193,6 +215,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int c0 = a.c0;
   auto issue_x = [&](int b, int n0, int c, int buf) {
     const int f0 = n0 - a.pad;
+    const int Lx = rag ? rlv[b] : L;  // frames at and past Lx are the utterance's zero padding
     const bool lo = c * CHR < c0;  // chunk from the first or the second source (skip concatenation)
     const int ldx = lo ? c0 : cin - c0;
     const char* xb = lo ? reinterpret_cast<const char*>(a.x) + ((size_t)b * L * c0 + c * CHR) * ES
@@ -204,7 +227,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
-      const bool ok = r < R && f >= 0 && f < L;
+      const bool ok = r < R && f >= 0 && f < Lx;
       const char* src = ok ? xb + (size_t)f * ldx * ES + q * 16 : reinterpret_cast<const char*>(a.zero) + q * 16;
       glds16(src, dst + j * 1024);
     }
@@ -530,7 +553,10 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   // ---- staging cursors and DMA bookkeeping (all wave-uniform) ----
   int issued = 0;                      // global_load_lds (+ epilogue store) instructions this wave issued
   // FIFO of the marks (`issued` right after each staged chunk's rows) not yet waited for: <= NXB-1
-  int nX = 0, mXa = 0, mXb = 0;
+  constexpr int NXM = NXB - 1;
+  int nX = 0, mX[NXM];
+#pragma unroll
+  for (int i = 0; i < NXM; ++i) mX[i] = 0;
   int xti = 0, xc = 0, xub = 0;        // next chunk to stage and its row buffer
   int wti = 0, wc = 0, wt = 0, wq = 0, wsl = 0; // next weight step to stage and its ring slot
   int wb, wn0, wm0, xb_, xn0, xm0;  // decoded tiles of the weight / row cursors
@@ -556,8 +582,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     if (xti < nmine) {
       issue_x(xb_, xn0, xc, xub);
       issued += NXW;
-      if (nX == 0) mXa = issued;
-      else mXb = issued;
+#pragma unroll
+      for (int i = 0; i < NXM; ++i)
+        if (i == nX) mX[i] = issued;  // constant register index, wave-uniform select
       ++nX;
       if (++xc == nch) {
         xc = 0;
@@ -567,8 +594,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     }
   };
   auto pop_x = [&]() -> int {  // mark of the oldest staged chunk not yet waited for
-    const int m = nX > 0 ? mXa : issued;
-    mXa = mXb;
+    const int m = nX > 0 ? mX[0] : issued;
+#pragma unroll
+    for (int i = 0; i + 1 < NXM; ++i) mX[i] = mX[i + 1];
     if (nX > 0) --nX;
     return m;
   };
@@ -622,8 +650,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
 #pragma unroll
   for (int i = 0; i < NXB - 1; ++i) stage_x();
   const int m0w = stage_w();
-  int mWa = stage_w();                       // `issued` after the weights of step qq+1
-  int mWb = NWSLOT > 3 ? stage_w() : 0;      // ... of step qq+2 (ring of 4)
+  int mW[NWSLOT - 2];  // `issued` after the weights of steps qq+1 .. qq+NWSLOT-2
+#pragma unroll
+  for (int i = 0; i < NWSLOT - 2; ++i) mW[i] = stage_w();
   wait_vmcnt(issued - max(m0w, pop_x()));
   raw_barrier();
 #if defined(VCONV_TS)
@@ -642,19 +671,17 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     }
     // publish step qq+1's weights (and rows, on a chunk's first tap); every wave's reads of step qq-1
     // are done (lgkmcnt), so its weight slot and, on a chunk change, the old row buffer may be restaged
-    if (qq + 1 < Q) wait_vmcnt(issued - (rt == 0 ? max(mWa, pop_x()) : mWa));
+    if (qq + 1 < Q) wait_vmcnt(issued - (rt == 0 ? max(mW[0], pop_x()) : mW[0]));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();
     const bool tile_end = t == taps - 1 && c == nch - 1;
     if constexpr ((EF & (VE_RESID | VE_ACCUM | VE_LN | VE_MASK)) != 0)
       if (tile_end) epi_loads(ti);
     if (t == 0) stage_x();  // rows of chunk u+NXB-1 into the buffer chunk u-1 used
-    if constexpr (NWSLOT > 3) {  // weights of step qq + NWSLOT - 1 into the slot step qq-1 used
-      mWa = mWb;
-      mWb = stage_w();
-    } else {
-      mWa = stage_w();
-    }
+    // weights of step qq + NWSLOT - 1 into the slot step qq-1 used
+#pragma unroll
+    for (int i = 0; i + 1 < NWSLOT - 2; ++i) mW[i] = mW[i + 1];
+    mW[NWSLOT - 3] = stage_w();
     // slice 0 of step qq (registers) || reads of slice 1 of step qq; slice 1 || slice 0 of step qq+1
     read_frag(F1, 1, cs, ub, t);
     mma_slice(F0);

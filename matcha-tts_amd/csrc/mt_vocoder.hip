@@ -11,6 +11,7 @@
 #include <type_traits>
 
 #include "mt_model.h"
+#include "mt_ragged.h"
 #include "mt_rbfuse.h"
 #include "mt_vconv.h"
 #include "mt_vpair.h"
@@ -22,18 +23,26 @@ namespace mt {
 // rows staged once in LDS as lrelu'd fp32 (rounded to bf16 first, as the generic kernel stages them),
 // 144-byte rows so each lane's 16-byte reads of rows t..t+6 hit distinct bank slots.
 constexpr int PC_N = 256, PC_ROW = 36;
+// Ragged batch (lens != null): utterance b has Lb = lens[b] * lmul samples; rows past Lb are zero padding and its
+// samples past Lb are written as zeros.
 __global__ __launch_bounds__(256) void post_conv_kernel(const bf16* __restrict__ x, int L,
                                                         const bf16* __restrict__ w, const float* __restrict__ bias,
-                                                        float slope, float* __restrict__ out) {
+                                                        float slope, float* __restrict__ out, const int* lens,
+                                                        int lmul) {
   __shared__ __attribute__((aligned(16))) float xs[(PC_N + 6) * PC_ROW];
   __shared__ __attribute__((aligned(16))) float wsm[7 * 32];
   const int b = blockIdx.y, f0 = blockIdx.x * PC_N, tid = threadIdx.x;
   const bf16* xb = x + (size_t)b * L * 32;
+  const int Lb = lens ? min(max(lens[b] * lmul, 0), L) : L;
+  if (f0 >= Lb) {  // wholly past the utterance
+    if (f0 + tid < L) out[(size_t)b * L + f0 + tid] = 0.f;
+    return;
+  }
   for (int e = tid; e < (PC_N + 6) * 4; e += 256) {
     const int r = e >> 2, q = e & 3;
     const int f = f0 - 3 + r;
     float v[8];
-    if (f >= 0 && f < L) {
+    if (f >= 0 && f < Lb) {
       const u32x4 u = *reinterpret_cast<const u32x4*>(xb + (size_t)f * 32 + q * 8);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -52,6 +61,10 @@ __global__ __launch_bounds__(256) void post_conv_kernel(const bf16* __restrict__
   __syncthreads();
   const int f = f0 + tid;
   if (f >= L) return;
+  if (f >= Lb) {
+    out[(size_t)b * L + f] = 0.f;
+    return;
+  }
   float acc = 0.f;
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
@@ -64,6 +77,23 @@ __global__ __launch_bounds__(256) void post_conv_kernel(const bf16* __restrict__
     }
   }
   out[(size_t)b * L + f] = tanhf(acc + bias[0]);
+}
+
+// rows [lens[b], T) of utterance b of a [B][T][C] bf16 tensor := 0 (a ragged batch's zero padding)
+__global__ void zero_tail_rows_kernel(bf16* __restrict__ x, int T, int C, const int* __restrict__ lens) {
+  const int b = blockIdx.y;
+  const int Lb = min(max(lens[b], 0), T);
+  bf16* xb = x + (size_t)b * T * C;
+  for (size_t e = (size_t)Lb * C + blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < (size_t)T * C;
+       e += (size_t)gridDim.x * blockDim.x)
+    xb[e] = (bf16)0.f;
+}
+
+static int zero_tail_rows(void* x, int B, int T, int C, const int* lens, hipStream_t st) {
+  hipLaunchKernelGGL(zero_tail_rows_kernel, dim3(std::max(1, std::min(64, (T * C + 255) / 256)), B), dim3(256), 0, st,
+                     (bf16*)x, T, C, lens);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
 }
 
 int Vocoder::init(int resblock_, const std::vector<int>& ur, const std::vector<int>& uk, int up_init_,
@@ -263,7 +293,7 @@ bool Vocoder::stage_vp32(int i) const {
 // One launch per pair (mt_vpair128 / mt_vpair / mt_vpair32); the chain state ping-pongs between R and Tb (a pair
 // reads its input's halo, so it cannot write in place); the inputs' activations are applied in LDS.
 int Vocoder::pair_resblock(const char* P, int i, int j, int B, int L, const char* X, char* XS, char* Tb, char* R,
-                           char* RA, char* trash, bool act_out, hipStream_t st) const {
+                           char* RA, char* trash, bool act_out, hipStream_t st, const int* lens) const {
   const int nk = (int)rb_kernels.size();
   const int C = rb1[(size_t)i * nk][0].cout;
   const bool c32 = C == 32;
@@ -288,6 +318,8 @@ int Vocoder::pair_resblock(const char* P, int i, int j, int B, int L, const char
     a.slope = 0.1f;
     a.zero = (const bf16*)(P + zero_off);
     a.trash = (bf16*)trash;
+    a.lens = lens;
+    a.lmul = rate_upto(i + 1);
     int ef = 0;
     if (!last) {
       a.y = (bf16*)((q & 1) ? Tb : R);
@@ -308,12 +340,18 @@ int Vocoder::pair_resblock(const char* P, int i, int j, int B, int L, const char
 }
 
 int Vocoder::pair_chain(const char* P, int i, int B, int L, const char* X, char* XS, char* Tb, char* R, char* RA,
-                        char* trash, bool act_out, hipStream_t st) const {
+                        char* trash, bool act_out, hipStream_t st, const int* lens) const {
   const int nk = (int)rb_kernels.size();
   int rc;
   for (int j = 0; j < nk; ++j)
-    if ((rc = pair_resblock(P, i, j, B, L, X, XS, Tb, R, RA, trash, act_out, st))) return rc;
+    if ((rc = pair_resblock(P, i, j, B, L, X, XS, Tb, R, RA, trash, act_out, st, lens))) return rc;
   return 0;
+}
+
+int Vocoder::rate_upto(int i) const {
+  int r = 1;
+  for (int u = 0; u < i && u < (int)up_rates.size(); ++u) r *= up_rates[(size_t)u];
+  return r;
 }
 
 bool Vocoder::ups_vc(int i) const {
@@ -326,7 +364,7 @@ bool Vocoder::ups_vc(int i) const {
 // exactly the frames in [0, Tout) are kept (hifigan/models.py:184-186; the generic kernel's ConvT
 // mapping, mt_conv.hip ups/opad)
 int Vocoder::ups_vconv(const char* P, int i, int B, int L, const char* xa, char* X, char* XA, bool dual,
-                       char* trash, hipStream_t st) const {
+                       char* trash, hipStream_t st, const int* lens) const {
   const GemmW& g = ups[(size_t)i];
   int Tout = 0, Ncols = 0;
   gemm_geom(g, L, &Tout, &Ncols);
@@ -350,6 +388,8 @@ int Vocoder::ups_vconv(const char* P, int i, int B, int L, const char* xa, char*
     a.zero = (const bf16*)(P + zero_off);
     a.trash = (bf16*)trash;
     a.probe = -1;
+    a.lens = lens;  // the input's valid frames (rate before this upsampler)
+    a.lmul = rate_upto(i);
     a.Lout = Ncols;
     a.ldy = g.M;
     a.yshift = g.opad * g.cout - gi * g.vrows;
@@ -373,14 +413,14 @@ size_t Vocoder::workspace_bytes(int B, int T) const {
 // Rounding points equal the generic per-layer path's: every stored tensor is rounded to bf16 and the
 // activated copies are lrelu of the rounded values.
 int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, const char* XA, char* XS, char* Tb,
-                         char* R, char* RA, char* trash, bool act_out, hipStream_t st) const {
+                         char* R, char* RA, char* trash, bool act_out, hipStream_t st, const int* lens) const {
   const int nk = (int)rb_kernels.size();
   const bf16* zero = (const bf16*)(P + zero_off);
   int rc;
-  if (stage_vp(i)) return pair_chain(P, i, B, L, X, XS, Tb, R, RA, trash, act_out, st);
+  if (stage_vp(i)) return pair_chain(P, i, B, L, X, XS, Tb, R, RA, trash, act_out, st, lens);
   for (int j = 0; j < nk; ++j) {
     if (rb_vp(i, j)) {  // this resblock as fused pairs (from the raw X), the others per layer (from XA)
-      if ((rc = pair_resblock(P, i, j, B, L, X, XS, Tb, R, RA, trash, act_out, st))) return rc;
+      if ((rc = pair_resblock(P, i, j, B, L, X, XS, Tb, R, RA, trash, act_out, st, lens))) return rc;
       continue;
     }
     const std::vector<GemmW>& c1 = rb1[(size_t)i * nk + j];
@@ -406,6 +446,8 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
       a.div = 1.f;
       a.zero = zero;
       a.trash = (bf16*)trash;
+      a.lens = lens;
+      a.lmul = rate_upto(i + 1);
       if ((rc = launch_vconv(VE_ACT, a, st))) return rc;
       VConvArgs b = a;
       b.x = (const bf16*)Tb;
@@ -440,7 +482,7 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
 
 template <class E>
 int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav, char* ws,
-                       hipStream_t st) const {
+                       hipStream_t st, const int* lens) const {
   int rc;
   const size_t big = align256((size_t)B * T * frame_elems() * esize);
   char* XS = ws;
@@ -452,6 +494,8 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
   char* RA = XA + big;
   char* trash = RA + big;  // 4 KiB (vconv stores of frames past L)
   if ((rc = bct_to_btc(dtype, mel, B, n_mels, T, 1.f, xm, n_mels, 0, st))) return rc;
+  // ragged: mel frames past each utterance's length are conv_pre's zero padding
+  if (lens && (rc = zero_tail_rows(xm, B, T, n_mels, lens, st))) return rc;
   {
     ConvArgs a = gemm_args(pre, P, B, T);
     a.x0 = xm;
@@ -478,7 +522,7 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     if constexpr (std::is_same<E, bf16>::value) {
       const bool svc = stage_vc((int)i);
       if (ups_vc((int)i)) {  // polyphase vconv from lrelu(xs) (RA); + XA = lrelu(X) for a vconv stage
-        if ((rc = ups_vconv(P, (int)i, B, L, RA, X, XA, svc && !stage_vp((int)i), trash, st))) return rc;
+        if ((rc = ups_vconv(P, (int)i, B, L, RA, X, XA, svc && !stage_vp((int)i), trash, st, lens))) return rc;
         done_up = true;
       }
       if (svc) {
@@ -490,7 +534,7 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
         }
         L = u.Tout;
         const bool act_out = i + 1 < ups.size() && ups_vc((int)i + 1);
-        if ((rc = stage_vconv(P, (int)i, B, L, X, XA, XS, Tb, R, RA, trash, act_out, st))) return rc;
+        if ((rc = stage_vconv(P, (int)i, B, L, X, XA, XS, Tb, R, RA, trash, act_out, st, lens))) return rc;
         continue;
       }
     }
@@ -499,7 +543,7 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     if constexpr (std::is_same<E, bf16>::value) {
       if (stage_vp32((int)i)) {
         const bool act_out = i + 1 < ups.size() && ups_vc((int)i + 1);
-        if ((rc = pair_chain(P, (int)i, B, L, X, XS, Tb, R, RA, trash, act_out, st))) return rc;
+        if ((rc = pair_chain(P, (int)i, B, L, X, XS, Tb, R, RA, trash, act_out, st, lens))) return rc;
         continue;
       }
     }
@@ -593,7 +637,8 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
   if constexpr (std::is_same<E, bf16>::value) {
     if (post.cin == 32 && post.k == 7 && post.cout == 1) {
       hipLaunchKernelGGL(post_conv_kernel, dim3((L + PC_N - 1) / PC_N, B), dim3(256), 0, st, (const bf16*)XS, L,
-                         (const bf16*)(P + post.w_off), (const float*)(P + post.b_off), 0.01f, wav);
+                         (const bf16*)(P + post.w_off), (const float*)(P + post.b_off), 0.01f, wav, lens,
+                         rate_upto((int)ups.size()));
       MT_CHECK_HIP(hipGetLastError());
       return 0;
     }
@@ -606,13 +651,22 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
   return launch_conv<E, PF_LRELU, EF_TANH | EF_OUTF32>(c, st);
 }
 
+bool Vocoder::ragged_supported() const {
+  if (dtype != BF16 || resblock != 1 || post.cin != 32 || post.k != 7 || post.cout != 1) return false;
+  for (size_t i = 0; i < ups.size(); ++i)
+    if (!ups_vc((int)i) || !(stage_vc((int)i) || stage_vp32((int)i))) return false;
+  return true;
+}
+
 int Vocoder::forward(const void* packed, const float* mel, int B, int T, float* wav, void* ws, size_t ws_bytes,
-                     hipStream_t st) const {
+                     hipStream_t st, const int* lens) const {
   MT_REQUIRE(B > 0 && T > 0, "vocoder: empty input");
   MT_REQUIRE(ws_bytes >= workspace_bytes(B, T), "vocoder: workspace %zu < %zu", ws_bytes,
              workspace_bytes(B, T));
-  if (dtype == BF16) return forward_t<bf16>((const char*)packed, mel, B, T, wav, (char*)ws, st);
-  return forward_t<float>((const char*)packed, mel, B, T, wav, (char*)ws, st);
+  MT_REQUIRE(!lens || (ragged_supported() && B <= RAG_MAXB),
+             "vocoder: per-utterance lengths need the bf16 vconv / pair path on every stage and B <= %d", RAG_MAXB);
+  if (dtype == BF16) return forward_t<bf16>((const char*)packed, mel, B, T, wav, (char*)ws, st, lens);
+  return forward_t<float>((const char*)packed, mel, B, T, wav, (char*)ws, st, nullptr);
 }
 
 }  // namespace mt

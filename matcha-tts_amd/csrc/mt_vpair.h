@@ -2,6 +2,7 @@
 // stages, bf16: the intermediate stays in LDS and the input's activation is applied on chip (mt_vpair128.hip,
 // mt_vpair.hip, mt_vpair32.hip).
 #pragma once
+#include "mt_ragged.h"
 #include "mt_vconv.h"
 
 namespace mt {
@@ -19,6 +20,10 @@ struct VPairArgs {
   float div, slope;     // VE_DIV divisor (nk), lrelu slope (0.1)
   const bf16* zero;     // >= 128 zero bytes
   bf16* trash;          // >= 1 KiB
+  // ragged batch (mt_ragged.h, B <= RAG_MAXB): utterance b has lens[b] * lmul valid frames (zero padding past
+  // them, tiles past them not computed); null: every utterance has L
+  const int* lens;
+  int lmul;
 };
 
 // epilogue flags: 0 | VE_ACCUM | VE_DIV | VE_DUAL combinations (mt_vconv.h values)

@@ -47,7 +47,8 @@ constexpr int TAPW = 64 * 128;       // one tap: 64 output rows x 64 input chann
 constexpr int WSLOT = 2 * TAPW;      // a step = two taps (the last step of an odd-k conv uses one)
 constexpr int NWS = 3;
 constexpr int T_OFF = XBUF, W_OFF = T_OFF + TBUF, PAR_OFF = W_OFF + NWS * WSLOT;
-constexpr int LDS_BYTES = PAR_OFF + 2 * C * 4;
+constexpr int RAG_OFF = PAR_OFF + 2 * C * 4;
+constexpr int LDS_BYTES = RAG_OFF + RAG_LDS;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 }  // namespace
 
@@ -86,7 +87,16 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   const int g4 = lane >> 4, l16 = lane & 15, lrow = lane >> 3, lp = lane & 7;
   const int k = a.taps, d = a.dil, L = a.L;
   const int h1 = d * (k - 1) / 2, h2 = (k - 1) / 2;
-  const int ntn = (L + BN - 1) / BN, ntiles = a.B * ntn;
+  const int ntn = (L + BN - 1) / BN;
+  // ragged batch: the live tiles of each utterance (mt_ragged.h)
+  const bool rag = a.lens != nullptr;
+  int* rtc = reinterpret_cast<int*>(smem + RAG_OFF);
+  int* rlv = rtc + RAG_MAXB;
+  if (rag) {
+    rag_build(rtc, rlv, a.lens, a.lmul, L, 0, L, a.B, BN, tid);
+    __syncthreads();
+  }
+  const int ntiles = rag ? rtc[a.B - 1] : a.B * ntn;
   const int G = gridDim.x, g = blockIdx.x;
   const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
   const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
@@ -103,8 +113,13 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   const int S = nmine * 2 * ns;  // weight steps of this workgroup
   auto tile_of = [&](int ti, int& b, int& n0) {
     const int tile = gl + ti * G;
-    b = tile / ntn;
-    n0 = (tile - b * ntn) * BN;
+    if (rag) {
+      b = rag_find(rtc, a.B, tile);
+      n0 = (tile - rag_first(rtc, b)) * BN;
+    } else {
+      b = tile / ntn;
+      n0 = (tile - b * ntn) * BN;
+    }
   };
   auto stage_w = [&](int s) {  // taps 2m, 2m+1 (clamped to k-1) of conv1 or conv2, m = step within the conv
     const int r2 = s % (2 * ns);
@@ -130,7 +145,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < L;
+      const bool ok = r < R1 && f >= 0 && f < (rag ? rlv[b] : L);
       vp_glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + j * 1024);
     }
     issued += XROWS / 64;
@@ -219,6 +234,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   for (int ti = 0; ti < nmine; ++ti) {
     int b, n0;
     tile_of(ti, b, n0);
+    const int Lt = rag ? rlv[b] : L;  // this utterance's frames (conv2's zero padding starts there)
     // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + HALO2 + h1), then
     // the in-place lrelu of the landed raw rows ----
     vp_wait_vmcnt(issued - xmk);
@@ -269,7 +285,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       for (int fn = 0; fn < FN; ++fn) {
         const int j = wave * WNC + fn * 16 + l16;
         const int f = n0 - HALO2 + j;
-        const bool ok = f >= 0 && f < L;
+        const bool ok = f >= 0 && f < Lt;
         uint32_t o[2][2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -359,7 +375,8 @@ struct K3G {
   static constexpr int XBUF = XROWS * 128, NXB = DB ? 2 : 1;
   static constexpr int TROWS = NF1 + 8;   // conv2 reads rows <= NF1 - 1 + 2
   static constexpr int T_OFF = NXB * XBUF, W_OFF = T_OFF + TROWS * 128, PAR_OFF = W_OFF + 6 * TAPW;
-  static constexpr int LDS = PAR_OFF + 2 * C * 4;
+  static constexpr int RAG_OFF = PAR_OFF + 2 * C * 4;
+  static constexpr int LDS = RAG_OFF + RAG_LDS;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(XROWS % 8 == 0, "rows staged 8 per DMA");
 };
@@ -377,7 +394,16 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   const int g4 = lane >> 4, l16 = lane & 15, lrow = lane >> 3, lp = lane & 7;
   const int d = a.dil, L = a.L;
   const int h1 = d;  // k = 3: h1 = d, h2 = 1 = HALO2
-  const int ntn = (L + BN - 1) / BN, ntiles = a.B * ntn;
+  const int ntn = (L + BN - 1) / BN;
+  // ragged batch: the live tiles of each utterance (mt_ragged.h)
+  const bool rag = a.lens != nullptr;
+  int* rtc = reinterpret_cast<int*>(smem + G3::RAG_OFF);
+  int* rlv = rtc + RAG_MAXB;
+  if (rag) {
+    rag_build(rtc, rlv, a.lens, a.lmul, L, 0, L, a.B, BN, tid);
+    __syncthreads();
+  }
+  const int ntiles = rag ? rtc[a.B - 1] : a.B * ntn;
   const int G = gridDim.x, g = blockIdx.x;
   const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
   const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
@@ -392,8 +418,13 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   int xmk[2] = {0, 0};
   auto tile_of = [&](int ti, int& b, int& n0) {
     const int tile = gl + ti * G;
-    b = tile / ntn;
-    n0 = (tile - b * ntn) * BN;
+    if (rag) {
+      b = rag_find(rtc, a.B, tile);
+      n0 = (tile - rag_first(rtc, b)) * BN;
+    } else {
+      b = tile / ntn;
+      n0 = (tile - b * ntn) * BN;
+    }
   };
   // both convs' 3 taps: DMA j moves rows (j & 7) * 8 .. + 7 of tap j / 8 (conv (j / 8) / 3)
   for (int j = wave; j < 48; j += 8) {
@@ -412,7 +443,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < L;
+      const bool ok = r < R1 && f >= 0 && f < (rag ? rlv[b] : L);
       vp_glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + (DB ? ti & 1 : 0) * K3_XBUF + j * 1024);
       ++issued;
     }
@@ -476,6 +507,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   for (int ti = 0; ti < nmine; ++ti) {
     int b, n0;
     tile_of(ti, b, n0);
+    const int Lt = rag ? rlv[b] : L;  // this utterance's frames (conv2's zero padding starts there)
     char* xs = smem + (DB ? ti & 1 : 0) * K3_XBUF;
     // ---- 1. rows landed (the first wait also covers the weights); old-xs loads, then the next tile's rows
     // into the other buffer (vmcnt retires in order); residual rows; in-place lrelu ----
@@ -522,7 +554,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
       for (int fn = 0; fn < FN; ++fn) {
         const int j = wave * WNC + fn * 16 + l16;
         const int f = n0 - HALO2 + j;
-        const bool ok = f >= 0 && f < L;
+        const bool ok = f >= 0 && f < Lt;
         uint32_t o[2][2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {

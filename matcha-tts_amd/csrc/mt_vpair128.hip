@@ -39,13 +39,14 @@ constexpr int NT = 512, C = 128;
 constexpr int FN = 3;                // 16-frame fragments per wave
 constexpr int WNC = 16 * FN;         // frames per wave (4 waves along frames)
 constexpr int NF1 = 4 * WNC;         // conv1 frames per tile (192)
-constexpr int XROWS = NF1 + 56;      // staged input rows >= NF1 + 2 h1
+constexpr int XROWS = NF1 + 40;      // staged input rows >= NF1 + 2 h1 (k <= 7 at d = 5; room for the ragged map)
 constexpr int XPL = XROWS * 128;     // one 64-channel plane of X
 constexpr int TPL = NF1 * 128;       // one 64-channel plane of T
 constexpr int WSLOT = C * 128;       // one step: 128 output rows x 64 input channels (16 KiB)
 constexpr int NWS = 3;
 constexpr int T_OFF = 0, X_OFF = 2 * TPL, W_OFF = X_OFF + 2 * XPL, PAR_OFF = W_OFF + NWS * WSLOT;
-constexpr int LDS_BYTES = PAR_OFF + 2 * C * 4;
+constexpr int RAG_OFF = PAR_OFF + 2 * C * 4;
+constexpr int LDS_BYTES = RAG_OFF + RAG_LDS;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(XROWS % 8 == 0, "X staged 8 rows per DMA instruction");
 
@@ -89,7 +90,16 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   const int BN = NF1 - 2 * h2;  // output frames per tile
   const int R1 = NF1 + 2 * h1;  // staged rows per plane
   const int nxi = (R1 + 7) / 8; // DMA instructions per plane
-  const int ntn = (L + BN - 1) / BN, ntiles = a.B * ntn;
+  const int ntn = (L + BN - 1) / BN;
+  // ragged batch: the live tiles of each utterance (mt_ragged.h)
+  const bool rag = a.lens != nullptr;
+  int* rtc = reinterpret_cast<int*>(smem + RAG_OFF);
+  int* rlv = rtc + RAG_MAXB;
+  if (rag) {
+    rag_build(rtc, rlv, a.lens, a.lmul, L, 0, L, a.B, BN, tid);
+    __syncthreads();
+  }
+  const int ntiles = rag ? rtc[a.B - 1] : a.B * ntn;
   const int G = gridDim.x, g = blockIdx.x;
   const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
   const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
@@ -106,8 +116,13 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   const int S = nmine * 2 * ns;  // weight steps of this workgroup
   auto tile_of = [&](int ti, int& b, int& n0) {
     const int tile = gl + ti * G;
-    b = tile / ntn;
-    n0 = (tile - b * ntn) * BN;
+    if (rag) {
+      b = rag_find(rtc, a.B, tile);
+      n0 = (tile - rag_first(rtc, b)) * BN;
+    } else {
+      b = tile / ntn;
+      n0 = (tile - b * ntn) * BN;
+    }
   };
   auto stage_w = [&](int s) {  // step m of conv1 or conv2: image block (chunk m / k, tap m % k)
     const int r2 = s % (2 * ns);
@@ -131,7 +146,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
       const int r = 8 * blk + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < L;
+      const bool ok = r < R1 && f >= 0 && f < (rag ? rlv[b] : L);
       glds16(ok ? xb + (size_t)f * C + p * 64 + q * 8 : a.zero + q * 8, smem + X_OFF + p * XPL + blk * 1024);
       ++issued;
     }
@@ -218,6 +233,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   for (int ti = 0; ti < nmine; ++ti) {
     int b, n0;
     tile_of(ti, b, n0);
+    const int Lt = rag ? rlv[b] : L;  // this utterance's frames (conv2's zero padding starts there)
     // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + h2 + h1), then the
     // in-place lrelu of the landed raw rows ----
     wait_vmcnt(issued - xmk);
@@ -265,7 +281,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
       for (int fn = 0; fn < FN; ++fn) {
         const int j = wn * WNC + fn * 16 + l16;
         const int f = n0 - h2 + j;
-        const bool ok = f >= 0 && f < L;
+        const bool ok = f >= 0 && f < Lt;
         uint32_t o[2][2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {

@@ -43,10 +43,11 @@ constexpr int XROWS = NF1 + 128;     // staged input rows >= NF1 + 2 * h1, h1 = 
 constexpr int XBUF = XROWS * RB;
 constexpr int TROWS = NF1 + 16;      // conv2's last (discarded) fragment reads up to row NF1 - 1 + 16
 constexpr int TBUF = TROWS * RB;
-constexpr int KMAX = 13;             // largest kernel size whose weights stay resident
+constexpr int KMAX = 11;             // largest kernel size whose weights stay resident
 constexpr int TAPW = C * RB;         // one tap: 32 output rows x 32 input channels (2 KiB)
 constexpr int T_OFF = XBUF, W_OFF = T_OFF + TBUF, PAR_OFF = W_OFF + 2 * KMAX * TAPW;  // W: [conv][tap]
-constexpr int LDS_BYTES = PAR_OFF + 2 * C * 4;
+constexpr int RAG_OFF = PAR_OFF + 2 * C * 4;
+constexpr int LDS_BYTES = RAG_OFF + RAG_LDS;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(XROWS % 128 == 0 && TAPW == 2 * 1024, "two 1 KiB DMAs per tap");
 
@@ -88,7 +89,16 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   const int g4 = lane >> 4, l16 = lane & 15, lrow = lane >> 2, lp = lane & 3;
   const int k = a.taps, d = a.dil, L = a.L;
   const int h1 = d * (k - 1) / 2, h2 = (k - 1) / 2;
-  const int ntn = (L + BN - 1) / BN, ntiles = a.B * ntn;
+  const int ntn = (L + BN - 1) / BN;
+  // ragged batch: the live tiles of each utterance (mt_ragged.h)
+  const bool rag = a.lens != nullptr;
+  int* rtc = reinterpret_cast<int*>(smem + RAG_OFF);
+  int* rlv = rtc + RAG_MAXB;
+  if (rag) {
+    rag_build(rtc, rlv, a.lens, a.lmul, L, 0, L, a.B, BN, tid);
+    __syncthreads();
+  }
+  const int ntiles = rag ? rtc[a.B - 1] : a.B * ntn;
   const int G = gridDim.x, g = blockIdx.x;
   const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
   const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
@@ -102,8 +112,13 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   int issued = 0, xmk = 0;
   auto tile_of = [&](int ti, int& b, int& n0) __attribute__((always_inline)) {
     const int tile = gl + ti * G;
-    b = tile / ntn;
-    n0 = (tile - b * ntn) * BN;
+    if (rag) {
+      b = rag_find(rtc, a.B, tile);
+      n0 = (tile - rag_first(rtc, b)) * BN;
+    } else {
+      b = tile / ntn;
+      n0 = (tile - b * ntn) * BN;
+    }
   };
   // every tap of both convs from the generic packing [32 rows][k][32]: DMA j moves tap (j / 2) % k of conv
   // j / 2k, rows (j & 1) * 16 .. + 15
@@ -128,7 +143,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       const int r = 16 * j + lrow;
       const int q = lp ^ swz(r);
       const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < L;
+      const bool ok = r < R1 && f >= 0 && f < (rag ? rlv[b] : L);
       glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + j * 1024);
     }
     issued += XROWS / 128;
@@ -197,6 +212,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   for (int ti = 0; ti < nmine; ++ti) {
     int b, n0;
     tile_of(ti, b, n0);
+    const int Lt = rag ? rlv[b] : L;  // this utterance's frames (conv2's zero padding starts there)
     // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + HALO2 + h1), then
     // the in-place lrelu of the landed raw rows ----
     wait_vmcnt(issued - xmk);
@@ -240,7 +256,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     for (int fn = 0; fn < FN; ++fn) {
       const int j = wave * WNC + fn * 16 + l16;
       const int f = n0 - HALO2 + j;
-      const bool ok = f >= 0 && f < L;
+      const bool ok = f >= 0 && f < Lt;
       uint32_t o[2][2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {

@@ -37,8 +37,11 @@ class Denoiser(torch.nn.Module):
         self.register_buffer("bias_spec", mag[:, 0, :][:, :, None].contiguous())  # [1, 513, 1]
 
     @torch.inference_mode()
-    def forward(self, audio, strength=0.0005):
+    def forward(self, audio, strength=0.0005, lengths=None):
+        """``lengths`` (extension, default None = the reference's call): int [B] utterance lengths in units of 256
+        samples (mel frames) for a padded [B, L] batch; row b is then denoised as the one-utterance call on its
+        first 256 * lengths[b] samples (its own reflect padding and frame count) and is zero past them."""
         squeeze = audio.dim() == 1
         a = audio.unsqueeze(0) if squeeze else audio
-        out = rt.denoise(a, self.bias_spec, strength)
+        out = rt.denoise(a, self.bias_spec, strength, lengths=lengths)
         return out.squeeze(0) if squeeze else out

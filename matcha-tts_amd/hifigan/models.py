@@ -135,11 +135,29 @@ class Generator(nn.Module):
             packed = self._pk.put(key, src, self.engine().pack(self.folded_state, src, device))
         return packed
 
-    def forward(self, x):
+    def forward(self, x, lengths=None):
+        """``lengths`` (extension, default None = the reference's call): int [B] mel frames per utterance of a
+        padded batch. Each utterance is then vocoded at its own length, as the reference pipeline calls the
+        vocoder one utterance at a time on the mel `synthesize` cropped to it (main.py:181-198,
+        MOS_audiou_generator.ipynb:265-277): out[b, :, :hop * lengths[b]] equals this forward on
+        x[b:b+1, :, :lengths[b]] alone, and out[b] past it is zero. One batched launch chain on the bf16 path
+        (mt_vocoder_forward_ragged); otherwise one call per utterance."""
         rt.require_gpu(x, what="Generator.forward")
         x = rt.f32c(x)
+        eng = self.engine()
         with torch.no_grad():
-            return self.engine().forward(self.packed(x.device), x)
+            if lengths is None:
+                return eng.forward(self.packed(x.device), x)
+            if eng.ragged_supported():
+                return eng.forward(self.packed(x.device), x, lengths=lengths)
+            B, _, T = x.shape
+            hop = eng.hop
+            out = torch.zeros((B, 1, T * hop), dtype=torch.float32, device=x.device)
+            for b, n in enumerate(int(v) for v in lengths.cpu()):
+                n = max(0, min(n, T))
+                if n:
+                    out[b:b + 1, :, :n * hop] = eng.forward(self.packed(x.device), x[b:b + 1, :, :n].contiguous())
+            return out
 
     def remove_weight_norm(self):
         print("Removing weight norm...")

@@ -66,11 +66,14 @@ SIGNATURES = {
     "mt_vocoder_pack": (c_int, [P, POINTER(c_void_p), P, P]),
     "mt_vocoder_workspace_bytes": (c_size_t, [P, c_int, c_int]),
     "mt_vocoder_forward": (c_int, [P, P, P, c_int, c_int, P, P, c_size_t, P]),
+    "mt_vocoder_forward_ragged": (c_int, [P, P, P, c_int, c_int, P, P, P, c_size_t, P]),
+    "mt_vocoder_ragged_supported": (c_int, [P]),
     "mt_durations": (c_int, [P, P, c_float, c_int, c_int, P, P, P, P]),
     "mt_alignment": (c_int, [P, P, c_int, c_int, c_int, P, c_int, P, P, P, P]),
     "mt_denorm_crop": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P]),
     "mt_denoise_workspace_bytes": (c_size_t, [c_int, c_int]),
     "mt_denoise": (c_int, [P, c_int, c_int, P, c_float, P, P, c_size_t, P]),
+    "mt_denoise_ragged": (c_int, [P, c_int, c_int, P, c_int, P, c_float, P, P, c_size_t, P]),
     "mt_maximum_path_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mt_decoder_step_times_workspace_bytes": (c_size_t, [P, c_int, c_int]),
     "mt_decoder_step_times": (c_int, [P, P, P, P, P, P, P, c_int, c_int, P, P, c_size_t, P]),

@@ -397,13 +397,25 @@ class VocoderEngine:
         self._packed, self._fp = packed, fp
         return packed
 
-    def forward(self, packed, mel, out=None):
+    def ragged_supported(self) -> bool:
+        return bool(lib().mt_vocoder_ragged_supported(self.h))
+
+    def forward(self, packed, mel, out=None, lengths=None):
+        """lengths (int [B], mel frames, or None): a ragged batch, utterance b vocoded at its own lengths[b]
+        frames (mt_vocoder_forward_ragged); its samples past hop * lengths[b] are zero"""
         B, C, T = mel.shape
         out = torch.empty((B, 1, T * self.hop), dtype=torch.float32, device=mel.device) if out is None else out
         L = lib()
         ws = _Workspace.get(L.mt_vocoder_workspace_bytes(self.h, B, T), mel.device)
-        check(L.mt_vocoder_forward(self.h, packed.data_ptr(), ptr(mel), B, T, ptr(out), ws.data_ptr(),
-                                   ws.numel(), stream_handle(mel.device)), "vocoder_forward")
+        if lengths is None:
+            check(L.mt_vocoder_forward(self.h, packed.data_ptr(), ptr(mel), B, T, ptr(out), ws.data_ptr(),
+                                       ws.numel(), stream_handle(mel.device)), "vocoder_forward")
+            return out
+        lens = lengths.to(device=mel.device, dtype=torch.int32).contiguous()
+        if lens.shape != (B,):
+            raise ValueError(f"lengths {tuple(lens.shape)}: expected ({B},)")
+        check(L.mt_vocoder_forward_ragged(self.h, packed.data_ptr(), ptr(mel), B, T, ptr(lens), ptr(out),
+                                          ws.data_ptr(), ws.numel(), stream_handle(mel.device)), "vocoder_forward")
         return out
 
 
@@ -457,7 +469,10 @@ def stft_magnitude(audio: torch.Tensor) -> torch.Tensor:
     return mag
 
 
-def denoise(audio: torch.Tensor, bias_spec: torch.Tensor, strength: float) -> torch.Tensor:
+def denoise(audio: torch.Tensor, bias_spec: torch.Tensor, strength: float, lengths=None,
+            hop: int = 256) -> torch.Tensor:
+    """lengths (int [B] in units of `hop` samples, or None): a ragged batch, row b denoised as an utterance of
+    hop * lengths[b] samples (mt_denoise_ragged); its output past them is zero"""
     require_gpu(audio, what="denoise")
     audio = f32c(audio)
     B, L = audio.shape
@@ -465,8 +480,15 @@ def denoise(audio: torch.Tensor, bias_spec: torch.Tensor, strength: float) -> to
     bias = f32c(bias_spec.reshape(-1).to(audio.device))
     L_ = lib()
     ws = _Workspace.get(L_.mt_denoise_workspace_bytes(B, L), audio.device)
-    check(L_.mt_denoise(ptr(audio), B, L, ptr(bias), float(strength), ptr(out), ws.data_ptr(), ws.numel(),
-                        stream_handle(audio.device)), "denoise")
+    if lengths is None:
+        check(L_.mt_denoise(ptr(audio), B, L, ptr(bias), float(strength), ptr(out), ws.data_ptr(), ws.numel(),
+                            stream_handle(audio.device)), "denoise")
+        return out
+    lens = lengths.to(device=audio.device, dtype=torch.int32).contiguous()
+    if lens.shape != (B,):
+        raise ValueError(f"lengths {tuple(lens.shape)}: expected ({B},)")
+    check(L_.mt_denoise_ragged(ptr(audio), B, L, ptr(lens), int(hop), ptr(bias), float(strength), ptr(out),
+                               ws.data_ptr(), ws.numel(), stream_handle(audio.device)), "denoise")
     return out
 
 

@@ -10,7 +10,9 @@ so only grids with more tiles than CUs exercise the multi-tile walk (cross-tile 
   (b) the bf16 Generator at B=8, T=728 (stage-1 convs with 368 tiles, stages 2-3 >1000 tiles);
   (c) the exact bench step (bf16 text->wav: encoder, 10-step Euler CFM, HiFi-GAN, denoiser) at
       B=32 and at the north-star batch B=256, rows against the oracle run on those rows at the
-      batch's padded length (rows are independent given T_pad and their z slice; SURVEY.md §8e);
+      batch's padded length (rows are independent given T_pad and their z slice), the
+      vocoder and denoiser per utterance on its cropped mel as the reference calls them (the step's ragged
+      vocoder: tests/test_gpu_ragged.py);
   (d) an fp32 10-step CFM solve against the oracle,
 
 and record every mt_vconv launch (variant + grid) so the last test can assert that each variant
@@ -200,17 +202,26 @@ def _bench_rows_vs_oracle(batch, rows, tag, rank=0, world=1, vctk=False, n_ts=10
         zr = O.cfm_solve(O.sub(sd, "decoder.estimator"), mu_y, y_mask, n_ts, z[rows], spks)
         mel_ref = O.denormalize(zr, sd["mel_mean"], sd["mel_std"])[:, :, :t_y]
         gs = {k: v.detach().cpu() for k, v in gsd.items()}
-        wav_ref = O.generator_forward(gs, mel_ref, v1).clamp(-1, 1)
-        den_ref = O.denoise(wav_ref.squeeze(1), O.denoiser_bias_spec(gs, v1), 0.00025)
+        bias = O.denoiser_bias_spec(gs, v1)
+        # the reference's vocoder + denoiser calls are per utterance, on the mel cropped to its y_length
+        # (main.py:198, MOS_audiou_generator.ipynb:276-277); the bench step does that for the batch (ragged)
+        den_ref = []
+        for i in range(len(rows)):
+            n = int(y_ref[i])
+            w = O.generator_forward(gs, mel_ref[i:i + 1, :, :n], v1).clamp(-1, 1)
+            den_ref.append(O.denoise(w.squeeze(1), bias, 0.00025)[0])
     mean, std = float(sd["mel_mean"]), float(sd["mel_std"])
     mel_r = mel.cpu()[rows]
     e_mel = rel_rms((mel_r - mean) / std, (mel_ref - mean) / std)
-    e_wav = rel_rms(wav.cpu()[rows], den_ref)
+    wav_c = wav.cpu()
+    e_wav = rel_rms(torch.cat([wav_c[r, :int(yl[r]) * 256] for r in rows]), torch.cat(den_ref))
     print(f"bench step {'vctk' if vctk else 'lj'} B={batch} n={n_ts} rows {rows}: mel rel-RMS {e_mel:.3e}, "
           f"denoised wav rel-RMS {e_wav:.3e}")
-    for i, r in enumerate(rows):  # every row inside its useful length, and silence-free
+    for i, r in enumerate(rows):  # every row inside its useful length (silence-free), and zero past it
         n = int(yl[r]) * 256
-        assert rel_rms(wav.cpu()[r, :n], den_ref[i, :n]) < 1e-2
+        assert den_ref[i].shape[0] == n
+        assert rel_rms(wav_c[r, :n], den_ref[i]) < 1e-2
+        assert torch.count_nonzero(wav_c[r, n:]) == 0
     assert e_mel < 1e-2 and e_wav < 1e-2, (e_mel, e_wav)
     return t_pad
 
