@@ -910,13 +910,19 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
   a.ldy = a.M;
   a.ylim = a.L * a.M;
   a.ystride = (long long)a.L * a.M;
-  const int BM = a.M % 128 == 0 ? 128 : 64;
-  const long cu = cu_count(), ntm = a.Mpad / BM;
-  // frames per tile by rounds of tiles over the CUs x frames (an fp32 tile is MFMA-bound: no fixed-cost weight)
-  auto rounds = [&](long f) { return ((long)a.B * ((a.L + f - 1) / f) * ntm + cu - 1) / cu * f; };
-  int bn = 128;
-  if (BM == 128 && rounds(256) < rounds(bn)) bn = 256;
-  const long ntiles = (long)a.B * ((a.L + bn - 1) / bn) * ntm;
+  // tile (rows x frames) by rounds of tiles over the CUs x tile size (an fp32 tile is MFMA-bound: no fixed-cost
+  // weight): 128 x 128 / 128 x 256 / 64 x 128, ties to the larger tile (the text encoder's FFN conv1, 768 rows at
+  // B = 32: 384 tiles of 128 x 128 = 2 rounds of 256 CUs, 768 tiles of 64 x 128 = 3 rounds of half the work)
+  const long cu = cu_count();
+  auto rounds = [&](long bm, long f) {
+    return ((long)a.B * ((a.L + f - 1) / f) * (a.Mpad / bm) + cu - 1) / cu * bm * f;
+  };
+  int BM = a.M % 128 == 0 ? 128 : 64, bn = 128;
+  if (BM == 128) {
+    if (rounds(128, 256) < rounds(128, 128)) bn = 256;
+    if (rounds(64, 128) < rounds(128, bn)) BM = 64, bn = 128;
+  }
+  const long ntiles = (long)a.B * ((a.L + bn - 1) / bn) * (a.Mpad / BM);
   const int G = (int)std::min<long>(ntiles, cu);
   {
     const int rec[VCLOG_FIELDS] = {ef | (1 << 20), BM, bn, (int)k1, (int)ntiles, G, a.taps, a.M, a.cin, a.B, a.L};

@@ -140,7 +140,12 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} is missing: build it with `make -C matcha-tts_amd` "
                 "(or __graft_entry__.build()); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
+        # timing experiments against an OLDER build of the library (tools/*: MT_LIB) may lack newer entry points
+        older = os.environ.get("MT_LIB") is not None and os.path.abspath(LIB_PATH) == os.path.abspath(
+            os.environ["MT_LIB"])
         for name, (res, args) in SIGNATURES.items():
+            if older and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -10,6 +10,9 @@ sys.path.insert(0, HERE)
 
 import torch  # noqa: E402
 
+if os.environ.get("MT_LIB"):  # timing experiments: another build of the library
+    import matcha_hip._lib as _L  # noqa: E402
+    _L.LIB_PATH = os.environ["MT_LIB"]
 import bench  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
