@@ -83,6 +83,7 @@ struct VConvArgs {
   // utterance has L frames
   const int* lens;
   int lmul;
+  int xcd_tiles;  // set by launch_vconv: 1 = XCD-major tile ownership (mt_vconv.hip), 0 = round-robin walk
 };
 
 // LayerNorm (mean, rstd) of a 256-channel frame from its 4 slab partials (mean_i, M2_i), 64 values each,

@@ -2,9 +2,11 @@
 //
 // GEMM view (same as mt_conv.h): rows m = output channels, columns n = output frames of one
 // utterance, K = taps x C_in. One workgroup = 8 waves (2 in M x 4 in N, 64x64 per wave,
-// v_mfma_f32_16x16x32_bf16) owns a 128 x 256 output tile at a time and walks the tiles
-// gl, gl + G, gl + 2G, ... (G = one workgroup per CU; gl groups consecutive tiles on workgroups that
-// share an XCD, so the tiles that read the same input rows / weights meet in one L2).
+// v_mfma_f32_16x16x32_bf16) owns a 128 x 256 output tile at a time and walks its tiles: on grids of up to
+// three rounds the XCD that runs it owns a contiguous, frame-major range of the tiles (so a launch reads what
+// the previous one wrote from its own L2), else gl, gl + G, gl + 2G, ... (G = one workgroup per CU; gl groups
+// consecutive tiles on workgroups that share an XCD, so the tiles that read the same input rows / weights meet
+// in one L2).
 //
 // K loop of a tile: for each 64-channel chunk c, for each tap t: one "step" =
 //   A = W[c][t] (128 rows x 128 B, one 16 KiB slot of a 4-slot ring)
@@ -143,8 +145,19 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   }
   const int ntiles = rag ? rtc[a.B - 1] * ntm : a.B * ntn * ntm;
   const int G = gridDim.x, g = blockIdx.x;
-  const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
-  const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
+  // XCD-major tile ownership (MT_XCD_TILES, A/B knob; default on): workgroup g runs on XCD g % 8 (round-robin
+  // dispatch; speed only, never correctness) and the 8 XCDs own CONTIGUOUS tile ranges in proportion to their
+  // workgroup counts, walked round-robin by their workgroups. Tiles are frame-major, so every launch maps a frame
+  // range to the same XCD: a conv reads what the previous launch wrote from that XCD's L2 (the decoder's
+  // activations fit its 4 MiB). Off: the round-robin walk gl, gl + G, ... with consecutive gl on one XCD.
+  const int xcd = g & 7, lw = g >> 3;
+  const int gx = (G - xcd + 7) >> 3;                   // workgroups on this XCD
+  const int sx = xcd * (G >> 3) + min(xcd, G & 7);     // workgroups on the XCDs before it
+  const int xt0 = (int)((long)ntiles * sx / G), xt1 = (int)((long)ntiles * (sx + gx) / G);
+  const bool xmaj = a.xcd_tiles != 0;
+  const int gl = xmaj ? xt0 + lw : (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
+  const int gstep = xmaj ? gx : G;
+  const int nmine = xmaj ? (gl < xt1 ? (xt1 - gl + gx - 1) / gx : 0) : (gl < ntiles ? (ntiles - gl + G - 1) / G : 0);
   const int Q = nmine * S;
   if (Q == 0) return;
 #if defined(VCONV_TS)
@@ -185,7 +198,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   }
 
   auto tile_of = [&](int ti, int& b, int& n0, int& m0) {
-    const int tile = gl + ti * G;
+    const int tile = gl + ti * gstep;
     const int r = tile / ntm;
     m0 = (tile - r * ntm) * BM;
     if (rag) {
@@ -822,6 +835,15 @@ bool vconv_supported_f32(int cin, int cout, int k, int stride) {
   return stride == 1 && cin % 32 == 0 && cout % 64 == 0 && cout <= MMAX && (k == 1 || BN + (k - 1) <= 320);
 }
 
+// MT_XCD_TILES=0 (A/B knob, read once): the round-robin tile walk instead of XCD-major ownership
+static int xcd_tiles_knob() {
+  static const int v = [] {
+    const char* e = getenv("MT_XCD_TILES");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return v;
+}
+
 static int cu_count() {
   static int n = 0;
   if (n == 0) {
@@ -900,6 +922,7 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(!(ef & VE_MASK) || a0.emask, "vconv f32: mask");
   VConvArgs a = a0;
   a.c0 = a.cin;
+  a.xcd_tiles = xcd_tiles_knob();
   const bool k1 = a.taps == 1;
   if (k1) {
     MT_REQUIRE(a0.pad == 0, "vconv f32: 1x1 conv with padding");
@@ -979,6 +1002,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
                                   a0.gn_T == a0.L && a0.gn_T >= vconv_gnres_min_frames() && a0.M % 64 == 0),
              "vconv: residual GroupNorm (1x1, resid, partials, gamma / beta, mask, T >= %d)", vconv_gnres_min_frames());
   VConvArgs a = a0;
+  a.xcd_tiles = xcd_tiles_knob();
   if (a.c0 == 0) a.c0 = a.cin;  // one source
   MT_REQUIRE(a.c0 == a.cin || (a.x1 && a.c0 % 64 == 0 && a.c0 > 0 && a.c0 < a.cin), "vconv: channel split %d/%d",
              a.c0, a.cin);
@@ -1042,6 +1066,9 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   const int tf = (!k1 && !placed) ? vconv_tile_frames(a.B, a.L, a.Mpad, ef) : BN;  // 256, 192 or 128
   if (tf != BN) ntiles = (long)a.B * ((a.L + tf - 1) / tf) * (a.Mpad / BM);
   const int G = (int)std::min<long>(ntiles, cu_count());
+  // XCD-major ownership pays where a launch's activations fit the XCDs' L2 (the decoder at B = 32: CFM solve
+  // 8.71 -> 8.61 ms); on larger grids (B = 256: 40.2 vs 40.5 ms) the round-robin walk's weight reuse wins
+  a.xcd_tiles = a.xcd_tiles && ntiles <= 3L * G;
   MT_REQUIRE(!(ef & VE_GNSTATS) || a0.gn_parts == 0 || a0.gn_parts == ((a.L + tf - 1) / tf) * (8 / (BM / 64)),
              "vconv: caller expects %d GroupNorm partial slots, the launch writes a different count", a0.gn_parts);
   {
