@@ -324,9 +324,11 @@ size_t attention_part_bytes(int B, int T, int heads) {
 constexpr int UNI_C = 256, UNI_PART = UNI_C + 4;  // UNI_PSMAX (mt_misc.h): part slices per utterance
 
 __global__ __launch_bounds__(256) void attn_uni_part_kernel(const bf16* __restrict__ x, const float* __restrict__ mask,
-                                                            int T, float* __restrict__ part) {
+                                                            int T, float* __restrict__ part, int xr) {
   __shared__ float red[8][UNI_C + 1];
-  const int S = gridDim.x, s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int S = gridDim.x, tid = threadIdx.x;
+  const int ci = xcd_chunk(blockIdx.x + S * blockIdx.y, S * gridDim.y, xr);  // (slice, utterance), XCD-aligned
+  const int s = ci % S, b = ci / S;
   const int fr = tid >> 5, cl = tid & 31, c = cl * 8;
   const int f0 = (int)((long)s * T / S), f1 = (int)((long)(s + 1) * T / S);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, n = 0.f;
@@ -376,21 +378,42 @@ __global__ __launch_bounds__(256) void attn_uni_part_kernel(const bf16* __restri
   }
 }
 
-// the utterance's attention output vector o_b (grid B): merge of the SP masked-sum slices, then the two GEMVs
+// the utterance's attention output vector o_b (grid B): merge of the SP masked-sum slices, then the two GEMVs.
+// Every load is issued up front (the partials, this lane's V-row and out-projection weights: none depends on
+// another), so the kernel pays one memory round trip instead of three; the arithmetic and its order are unchanged.
 __global__ __launch_bounds__(256) void attn_uni_vec_kernel(int SP, const float* __restrict__ part,
                                                            const bf16* __restrict__ wqkv, int mq, const float* __restrict__ bqkv,
                                                            const bf16* __restrict__ wout, const float* __restrict__ bout,
                                                            float* __restrict__ ovec) {
   __shared__ float zb[UNI_C], vb[128];
   const int b = blockIdx.x, tid = threadIdx.x;
-  {  // merge the utterance's SP part slices in order (all loads in flight at once)
-    float zz[UNI_PSMAX], nn[UNI_PSMAX];
+  // GEMVs: 4 lanes per output row, each a quarter of K, combined by two lane shuffles
+  const int q4 = tid & 3, rq = tid >> 2;  // 64 row slots per pass
+  float zz[UNI_PSMAX], nn[UNI_PSMAX];
 #pragma unroll
-    for (int k = 0; k < UNI_PSMAX; ++k) {
-      const size_t o = ((size_t)b * SP + min(k, SP - 1)) * UNI_PART;
-      zz[k] = part[o + tid];
-      nn[k] = part[o + UNI_C];
-    }
+  for (int k = 0; k < UNI_PSMAX; ++k) {
+    const size_t o = ((size_t)b * SP + min(k, SP - 1)) * UNI_PART;
+    zz[k] = part[o + tid];
+    nn[k] = part[o + UNI_C];
+  }
+  // V rows 256 .. 383 of the LN-folded QKV image [4 chunks][mq rows][64]; lane quarter q4 = chunk q4
+  u32x4 wv[2][8];
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const bf16* wr = wqkv + ((size_t)q4 * mq + 256 + rq + 64 * pass) * 64;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wv[pass][i] = *reinterpret_cast<const u32x4*>(wr + 8 * i);
+  }
+  // out-projection [2 chunks][256 rows][64]: quarter q4 = chunk q4 / 2, half (q4 & 1) of its 64 elements
+  const int ck = q4 >> 1, k0 = (q4 & 1) * 32;
+  u32x4 wo[4][4];
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const bf16* wr = wout + ((size_t)ck * UNI_C + rq + 64 * pass) * 64 + k0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wo[pass][i] = *reinterpret_cast<const u32x4*>(wr + 8 * i);
+  }
+  {  // merge the utterance's SP part slices in order
     float z = 0.f, n = 0.f;
 #pragma unroll
     for (int k = 0; k < UNI_PSMAX; ++k)
@@ -401,9 +424,6 @@ __global__ __launch_bounds__(256) void attn_uni_vec_kernel(int SP, const float* 
     zb[tid] = z / n;
   }
   __syncthreads();
-  // GEMVs: 4 lanes per output row, each a quarter of K with all its 16-byte weight loads independent (issued
-  // together), combined by two lane shuffles
-  const int q4 = tid & 3, rq = tid >> 2;  // 64 row slots per pass
   auto dot8 = [](u32x4 w, const float* z) {
     float acc = 0.f;
 #pragma unroll
@@ -411,47 +431,36 @@ __global__ __launch_bounds__(256) void attn_uni_vec_kernel(int SP, const float* 
       acc += __uint_as_float(w[e] << 16) * z[2 * e] + __uint_as_float(w[e] & 0xffff0000u) * z[2 * e + 1];
     return acc;
   };
-  {  // V rows 256 .. 383 of the LN-folded QKV image [4 chunks][mq rows][64]; lane quarter q4 = chunk q4
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      const int r = rq + 64 * pass;
-      const bf16* wr = wqkv + ((size_t)q4 * mq + 256 + r) * 64;
-      u32x4 w[8];
+  for (int pass = 0; pass < 2; ++pass) {
+    const int r = rq + 64 * pass;
+    float v = 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) w[i] = *reinterpret_cast<const u32x4*>(wr + 8 * i);
-      float v = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v += dot8(w[i], zb + q4 * 64 + 8 * i);
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      if (q4 == 0) vb[r] = (float)(bf16)(v + bqkv[256 + r]);
-    }
+    for (int i = 0; i < 8; ++i) v += dot8(wv[pass][i], zb + q4 * 64 + 8 * i);
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    if (q4 == 0) vb[r] = (float)(bf16)(v + bqkv[256 + r]);
   }
   __syncthreads();
-  {  // out-projection [2 chunks][256 rows][64]: quarter q4 = chunk q4 / 2, half (q4 & 1) of its 64 elements
 #pragma unroll
-    for (int pass = 0; pass < 4; ++pass) {
-      const int r = rq + 64 * pass;
-      const int ck = q4 >> 1, k0 = (q4 & 1) * 32;
-      const bf16* wr = wout + ((size_t)ck * UNI_C + r) * 64 + k0;
-      u32x4 w[4];
+  for (int pass = 0; pass < 4; ++pass) {
+    const int r = rq + 64 * pass;
+    float o = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) w[i] = *reinterpret_cast<const u32x4*>(wr + 8 * i);
-      float o = 0.f;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o += dot8(w[i], vb + ck * 64 + k0 + 8 * i);
-      o += __shfl_xor(o, 1, 64);
-      o += __shfl_xor(o, 2, 64);
-      if (q4 == 0) ovec[(size_t)b * UNI_C + r] = o + bout[r];
-    }
+    for (int i = 0; i < 4; ++i) o += dot8(wo[pass][i], vb + ck * 64 + k0 + 8 * i);
+    o += __shfl_xor(o, 1, 64);
+    o += __shfl_xor(o, 2, 64);
+    if (q4 == 0) ovec[(size_t)b * UNI_C + r] = o + bout[r];
   }
 }
 
 // x += o_b on every frame of the slice, + the next LayerNorm's per-slab (mean, M2) (grid slices x B)
 __global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ x, int T, const float* __restrict__ ovec,
-                                                             float* __restrict__ row_out) {
+                                                             float* __restrict__ row_out, int xr) {
   __shared__ float ob[UNI_C];
-  const int S = gridDim.x, s = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int S = gridDim.x, tid = threadIdx.x;
+  const int ci = xcd_chunk(blockIdx.x + S * blockIdx.y, S * gridDim.y, xr);  // (slice, utterance), XCD-aligned
+  const int s = ci % S, b = ci / S;
   ob[tid] = ovec[(size_t)b * UNI_C + tid];
   __syncthreads();
   const int fr = tid >> 5, cl = tid & 31, c = cl * 8;
@@ -504,10 +513,12 @@ int launch_uniform_attention(void* x, const float* mask, int B, int T, const voi
              "uniform attention: arguments (C = 256, 2 heads x 64)");
   const int SP = uniform_part_slices(T);
   float* ovec = part + (size_t)B * UNI_PSMAX * UNI_PART;  // [B][256] after the slice sums (uniform_attention_floats)
-  hipLaunchKernelGGL(attn_uni_part_kernel, dim3(SP, B), dim3(256), 0, st, (const bf16*)x, mask, T, part);
+  const int xr = xcd_remap_for((size_t)B * T * UNI_C * sizeof(bf16));
+  hipLaunchKernelGGL(attn_uni_part_kernel, dim3(SP, B), dim3(256), 0, st, (const bf16*)x, mask, T, part, xr);
   hipLaunchKernelGGL(attn_uni_vec_kernel, dim3(B), dim3(256), 0, st, SP, (const float*)part, (const bf16*)wqkv, mq,
                      bqkv, (const bf16*)wout, bout, ovec);
-  hipLaunchKernelGGL(attn_uni_apply_kernel, dim3(SP, B), dim3(256), 0, st, (bf16*)x, T, (const float*)ovec, row_out);
+  hipLaunchKernelGGL(attn_uni_apply_kernel, dim3(SP, B), dim3(256), 0, st, (bf16*)x, T, (const float*)ovec, row_out,
+                     xr);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -142,6 +142,17 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+
+// XCD-aligned block order (speed only, never correctness): block i of an n-block grid runs on XCD i % 8 (the
+// dispatcher's round-robin); returns the chunk index block i should process so that each XCD takes a CONTIGUOUS
+// range of chunks, in proportion to its block count — the same frame-range-to-XCD map mt_vconv's XCD-major tile
+// walk uses, so a kernel reads what its neighbour launch wrote from its own XCD's L2. remap = 0: identity.
+__device__ __forceinline__ int xcd_chunk(int i, int n, int remap) {
+  if (!remap) return i;
+  const int x = i & 7, j = i >> 3;
+  return x * (n >> 3) + min(x, n & 7) + j;
+}
+
 }  // namespace mt
 
 // ---------------------------------------------------------------------------

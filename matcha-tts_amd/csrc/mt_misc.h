@@ -78,4 +78,10 @@ size_t uniform_attention_floats(int B);  // workspace of launch_uniform_attentio
 int launch_uniform_attention(void* x, const float* mask, int B, int T, const void* wqkv, int mq, const float* bqkv,
                              const void* wout, const float* bout, float* part, float* row_out, hipStream_t st);
 
+// the XCD-aligned block order of the decoder's streaming kernels (mt_common.h xcd_chunk; MT_XCD_TILES=0 turns it
+// and mt_vconv's XCD-major tile walk off)
+int xcd_remap_enabled();
+// ... for a launch streaming `bytes` of activations: only while they fit the XCDs' L2 (the decoder at B = 32: CFM
+// solve 8.70 -> 8.47 ms with mt_vconv's XCD-major walk; at B = 256 the round-robin order is faster)
+inline int xcd_remap_for(size_t bytes) { return xcd_remap_enabled() && bytes <= (24u << 20) ? 1 : 0; }
 }  // namespace mt

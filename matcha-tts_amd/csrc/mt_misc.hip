@@ -535,9 +535,12 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ 
                                                        const double* __restrict__ part, int nparts,
                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
                                                        float eps, const float* __restrict__ tb, int tb_ld,
-                                                       const float* __restrict__ mask, bf16* __restrict__ h) {
+                                                       const float* __restrict__ mask, bf16* __restrict__ h, int xr) {
   __shared__ float ga[256], gs[256], gm[8], gr[8];
-  const int b = blockIdx.y, tid = threadIdx.x;
+  const int tid = threadIdx.x;
+  // (frame block, utterance), XCD-aligned (mt_common.h xcd_chunk)
+  const int ci = xcd_chunk(blockIdx.x + gridDim.x * blockIdx.y, gridDim.x * gridDim.y, xr);
+  const int b = ci / gridDim.x, bx = ci % gridDim.x;
   const int G = C >> 5;
   const int cpr = C >> 3;  // 16-byte groups per row
   const int rows_per = 256 / cpr;
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ 
   constexpr int NR = GN_FR / 8;  // rows per thread at C = 256 (fewer used at smaller C)
   u32x4 v[NR];
   float mk[NR];
-  const int t0 = blockIdx.x * GN_FR + tid / cpr;
+  const int t0 = bx * GN_FR + tid / cpr;
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int t = min(t0 + j * rows_per, T - 1);
@@ -591,7 +594,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const bf16* __restrict__ 
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int t = t0 + j * rows_per;
-    if (t >= T || t >= (int)(blockIdx.x + 1) * GN_FR) break;
+    if (t >= T || t >= (bx + 1) * GN_FR) break;
     const size_t row = (size_t)b * T + t;
     u32x4 o;
 #pragma unroll
@@ -611,7 +614,7 @@ int gn_apply(const void* y, int B, int T, int C, const double* part, int nparts,
              const float* beta, float eps, const float* tb, int tb_ld, const float* mask, void* h, hipStream_t st) {
   MT_REQUIRE(C % 32 == 0 && C <= 256 && C >= 64 && 256 % (C / 8) == 0 && nparts > 0, "gn_apply: C %d", C);
   hipLaunchKernelGGL(gn_apply_kernel, dim3((T + GN_FR - 1) / GN_FR, B), dim3(256), 0, st, (const bf16*)y, T, C, part, nparts,
-                     gamma, beta, eps, tb, tb_ld, mask, (bf16*)h);
+                     gamma, beta, eps, tb, tb_ld, mask, (bf16*)h, xcd_remap_for((size_t)B * T * C * sizeof(bf16)));
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }

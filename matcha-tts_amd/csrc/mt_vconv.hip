@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "mt_misc.h"
 #include "mt_probe.h"
 #include "mt_ragged.h"
 #include "mt_vconv.h"
@@ -843,6 +844,8 @@ static int xcd_tiles_knob() {
   }();
   return v;
 }
+
+int xcd_remap_enabled() { return xcd_tiles_knob(); }
 
 static int cu_count() {
   static int n = 0;
