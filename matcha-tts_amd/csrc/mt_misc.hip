@@ -399,29 +399,56 @@ int rowdot(const float* x, int ldx, const float* W, const float* bias, float* y,
 // duration -> alignment index path (model.py:1273-1289, 42-76). Bit-exact: every value is
 // an integer-valued fp32 (< 2^24), so sums and prefix sums are exact in any order.
 // ------------------------------------------------------------------------------------
-__global__ void durations_kernel(const float* __restrict__ logw, const float* __restrict__ xmask,
-                                 float ls, int Tx, float* __restrict__ w_ceil,
-                                 float* __restrict__ cum, long long* __restrict__ ylen) {
-  const int b = blockIdx.x;
-  for (int x = threadIdx.x; x < Tx; x += blockDim.x) {
-    const size_t i = (size_t)b * Tx + x;
-    const float w = (expf(logw[i]) * xmask[i]) * ls;
-    w_ceil[i] = ceilf(w);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float c = 0.f;
-    for (int x = 0; x < Tx; ++x) {
-      c += w_ceil[(size_t)b * Tx + x];
-      cum[(size_t)b * Tx + x] = c;
+__global__ __launch_bounds__(256) void durations_kernel(const float* __restrict__ logw, const float* __restrict__ xmask,
+                                                        float ls, int Tx, float* __restrict__ w_ceil,
+                                                        float* __restrict__ cum, long long* __restrict__ ylen) {
+  // thread t owns the DUR_PER consecutive tokens [t * per, (t + 1) * per): ceil(exp(logw) * mask * ls), then an
+  // inclusive block scan of the per-thread sums (wave shuffles + one LDS pass). Every value is an integer-valued
+  // fp32 below 2^24, so this order gives the serial cumsum's bits exactly.
+  constexpr int DUR_PER = 32;  // Tx <= 8192
+  __shared__ float wsum[4];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int per = (Tx + 255) / 256, x0 = tid * per;
+  float w[DUR_PER];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < DUR_PER; ++k) {
+    const int x = x0 + k;
+    w[k] = 0.f;
+    if (k < per && x < Tx) {
+      const size_t i = (size_t)b * Tx + x;
+      w[k] = ceilf((expf(logw[i]) * xmask[i]) * ls);
+      w_ceil[i] = w[k];
+      s += w[k];
     }
+  }
+  float inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  float run = inc - s;
+  for (int u = 0; u < wv; ++u) run += wsum[u];
+#pragma unroll
+  for (int k = 0; k < DUR_PER; ++k) {
+    const int x = x0 + k;
+    if (k < per && x < Tx) {
+      run += w[k];
+      cum[(size_t)b * Tx + x] = run;
+    }
+  }
+  if (tid == 255) {
+    const float c = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     ylen[b] = (long long)(c < 1.f ? 1.f : c);
   }
 }
 
 int durations(const float* logw, const float* xmask, float ls, int B, int Tx, float* w_ceil, float* cum,
               long long* ylen, hipStream_t st) {
-  MT_REQUIRE(B > 0 && Tx > 0, "durations: empty input");
+  MT_REQUIRE(B > 0 && Tx > 0 && Tx <= 8192, "durations: B %d, Tx %d (<= 8192)", B, Tx);
   hipLaunchKernelGGL(durations_kernel, dim3(B), dim3(256), 0, st, logw, xmask, ls, Tx, w_ceil, cum, ylen);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
@@ -432,7 +459,7 @@ int durations(const float* logw, const float* xmask, float ls, int B, int Tx, fl
 __global__ void alignment_kernel(const float* __restrict__ cum, const long long* __restrict__ ylen, int Tx,
                                  int T, const float* __restrict__ mu, int C, float* __restrict__ attn,
                                  float* __restrict__ mu_y, float* __restrict__ y_mask) {
-  const int b = blockIdx.y;
+  const int b = blockIdx.y, z = blockIdx.z, Z = gridDim.z;  // z: this block's share of the token rows / channels
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= T) return;
   const float* cb = cum + (size_t)b * Tx;
@@ -448,11 +475,11 @@ __global__ void alignment_kernel(const float* __restrict__ cum, const long long*
   }
   if (attn) {
     float* ab = attn + (size_t)b * Tx * T + j;
-    for (int x = 0; x < Tx; ++x) ab[(size_t)x * T] = (x == tok) ? 1.f : 0.f;
+    for (int x = z * Tx / Z; x < (z + 1) * Tx / Z; ++x) ab[(size_t)x * T] = (x == tok) ? 1.f : 0.f;
   }
-  if (y_mask) y_mask[(size_t)b * T + j] = (long long)j < ylen[b] ? 1.f : 0.f;
+  if (y_mask && z == 0) y_mask[(size_t)b * T + j] = (long long)j < ylen[b] ? 1.f : 0.f;
   if (mu_y) {
-    for (int c = 0; c < C; ++c)
+    for (int c = z * C / Z; c < (z + 1) * C / Z; ++c)
       mu_y[((size_t)b * C + c) * T + j] = tok >= 0 ? mu[((size_t)b * C + c) * Tx + tok] : 0.f;
   }
 }
@@ -460,7 +487,8 @@ __global__ void alignment_kernel(const float* __restrict__ cum, const long long*
 int alignment(const float* cum, const long long* ylen, int B, int Tx, int T, const float* mu, int C, float* attn,
               float* mu_y, float* y_mask, hipStream_t st) {
   MT_REQUIRE(B > 0 && Tx > 0 && T > 0, "alignment: empty input");
-  dim3 grid((T + 255) / 256, B);
+  // the writes (the one-hot attn [B][Tx][T] dominates: 23 MB at B = 32) split over 8 blocks per frame range
+  dim3 grid((T + 255) / 256, B, std::max(1, std::min(8, std::min(Tx, std::max(C, 1)))));
   hipLaunchKernelGGL(alignment_kernel, grid, dim3(256), 0, st, cum, ylen, Tx, T, mu, C, attn, mu_y, y_mask);
   MT_CHECK_HIP(hipGetLastError());
   return 0;

@@ -39,6 +39,34 @@ def test_durations_alignment_bit_exact():
         assert torch.equal(y_mask.cpu()[:, 0], ref_mask)
 
 
+@pytest.mark.parametrize("B,Tx", [(3, 251), (2, 1000), (1, 8192)])
+def test_durations_scan_and_alignment_long_text(B, Tx):
+    """The block-parallel ceil / cumsum (every partial sum an integer below 2^24, so exact in any order) and the
+    alignment with its writes split over the token rows: equal to torch's serial cumsum and to the oracle's
+    generate_path / mu_y gather (model.py:1273-1289), ragged masks included."""
+    from matcha_hip import runtime as rt
+    from oracle import matcha_oracle as O
+    g = torch.Generator().manual_seed(Tx)
+    logw = torch.randn(B, 1, Tx, generator=g) * 0.7 + 0.6
+    lens = torch.randint(Tx // 2, Tx + 1, (B,), generator=g)
+    lens[0] = Tx
+    x_mask = (torch.arange(Tx)[None] < lens[:, None]).float()[:, None]
+    w_ceil, cum, yl = rt.durations(logw.to(DEV), x_mask.to(DEV), 1.0)
+    w_ref = torch.ceil(torch.exp(logw) * x_mask)
+    assert torch.equal(w_ceil.cpu(), w_ref)
+    assert torch.equal(cum.cpu(), torch.cumsum(w_ref[:, 0], dim=1))
+    assert torch.equal(yl.cpu(), torch.clamp_min(w_ref.sum(dim=(1, 2)), 1).long())
+    if Tx > 1000:
+        return
+    tp = int(yl.max())
+    mu = torch.randn(B, 80, Tx, generator=g)
+    attn, mu_y, y_mask = rt.alignment(cum, yl, tp, mu.to(DEV))
+    y_m = O.sequence_mask(yl.cpu(), tp).unsqueeze(1).float()
+    a_ref = O.generate_path(w_ref.squeeze(1), (x_mask.unsqueeze(-1) * y_m.unsqueeze(2)).squeeze(1))
+    assert torch.equal(attn.cpu()[:, 0], a_ref)
+    assert torch.equal(mu_y.cpu(), torch.matmul(a_ref.transpose(1, 2), mu.transpose(1, 2)).transpose(1, 2))
+
+
 def test_durations_edge_cases():
     """All-masked utterance (y_length clamps to 1, empty path) and a 1-token utterance."""
     from matcha_hip import runtime as rt
