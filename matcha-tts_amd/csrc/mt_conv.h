@@ -80,6 +80,10 @@ struct ConvArgs {
   float dt;
   int half_step;             // midpoint first half: inc = (pred*dt)*0.5
   int update_master;
+  // ragged batch (the fp32 vocoder's per-utterance lengths, mt_ragged.h): utterance b's input has lens[b] * lmul
+  // valid frames (zero padding past them); tiles past its output columns exit, outputs past them are not written
+  const int* lens;
+  int lmul;
 };
 
 // Host launcher. Picks a tile configuration from (M, N), validates the geometry and

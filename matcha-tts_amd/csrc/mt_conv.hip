@@ -75,6 +75,10 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
   const int ntiles = (a.Ncols + BN - 1) / BN;
   const int b = blockIdx.x / ntiles, nt = blockIdx.x - b * ntiles;
   const int n0 = nt * BN, m0 = blockIdx.y * BM;
+  // ragged batch: this utterance's valid input frames / output frames (whole block uniform)
+  const int Lin = a.lens ? min(max(a.lens[b] * a.lmul, 0), a.Tin) : a.Tin;
+  const int Lout = a.lens ? min(a.Tout, a.stride > 1 ? Lin / a.stride : Lin * a.ups) : a.Tout;
+  if (a.lens && n0 >= Lin + (a.Ncols - a.Tin)) return;  // a tile wholly past the utterance
 
   float* ga = reinterpret_cast<float*>(smem + 2 * TL::BUF_BYTES);  // [256]
   float* gsh = ga + 256;                                           // [256]
@@ -173,7 +177,7 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
       const int r = v / VPR, sl = v % VPR;
       int f = fbase + r;
       int ch = cbase + sl * VN;
-      const bool ok = (v < RB * VPR) && f >= 0 && f < a.Tin && ch < a.cin;
+      const bool ok = (v < RB * VPR) && f >= 0 && f < Lin && ch < a.cin;
       f = ok ? f : 0;
       ch = ok ? ch : 0;
       const size_t row = (size_t)b * a.Tin + f;
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
       const int f = fbase + r;
       const int ch = cbase + sl * VN;
       Vec16<E> val = xr[i];
-      if (f < 0 || f >= a.Tin || ch >= a.cin) {
+      if (f < 0 || f >= Lin || ch >= a.cin) {
         val = zero16<E>();
       } else if constexpr (PF != 0) {
         const size_t row = (size_t)b * a.Tin + f;
@@ -321,7 +325,7 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
       const int n = n0 + wn * WN + fn * 16 + (lane & 15);
       if (n >= a.Ncols) continue;
       const int fr = n * a.ups + ph - a.opad;
-      if (fr < 0 || fr >= a.Tout) continue;
+      if (fr < 0 || fr >= Lout) continue;
       const size_t orow = (size_t)b * a.Tout + fr;
       float em = 1.f;
       if constexpr ((EF & (EF_MASK | EF_GNADD | EF_FMASK)) != 0) em = a.emask[orow];

@@ -79,19 +79,21 @@ __global__ __launch_bounds__(256) void post_conv_kernel(const bf16* __restrict__
   out[(size_t)b * L + f] = tanhf(acc + bias[0]);
 }
 
-// rows [lens[b], T) of utterance b of a [B][T][C] bf16 tensor := 0 (a ragged batch's zero padding)
-__global__ void zero_tail_rows_kernel(bf16* __restrict__ x, int T, int C, const int* __restrict__ lens) {
+// rows [lens[b], T) of utterance b of a [B][T][C] tensor := 0 (a ragged batch's zero padding)
+template <class E>
+__global__ void zero_tail_rows_kernel(E* __restrict__ x, int T, int C, const int* __restrict__ lens) {
   const int b = blockIdx.y;
   const int Lb = min(max(lens[b], 0), T);
-  bf16* xb = x + (size_t)b * T * C;
+  E* xb = x + (size_t)b * T * C;
   for (size_t e = (size_t)Lb * C + blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < (size_t)T * C;
        e += (size_t)gridDim.x * blockDim.x)
-    xb[e] = (bf16)0.f;
+    xb[e] = (E)0.f;
 }
 
-static int zero_tail_rows(void* x, int B, int T, int C, const int* lens, hipStream_t st) {
-  hipLaunchKernelGGL(zero_tail_rows_kernel, dim3(std::max(1, std::min(64, (T * C + 255) / 256)), B), dim3(256), 0, st,
-                     (bf16*)x, T, C, lens);
+static int zero_tail_rows(int dtype, void* x, int B, int T, int C, const int* lens, hipStream_t st) {
+  const dim3 grid(std::max(1, std::min(64, (T * C + 255) / 256)), B);
+  if (dtype == BF16) hipLaunchKernelGGL(zero_tail_rows_kernel<bf16>, grid, dim3(256), 0, st, (bf16*)x, T, C, lens);
+  else hipLaunchKernelGGL(zero_tail_rows_kernel<float>, grid, dim3(256), 0, st, (float*)x, T, C, lens);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -495,11 +497,20 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
   char* trash = RA + big;  // 4 KiB (vconv stores of frames past L)
   if ((rc = bct_to_btc(dtype, mel, B, n_mels, T, 1.f, xm, n_mels, 0, st))) return rc;
   // ragged: mel frames past each utterance's length are conv_pre's zero padding
-  if (lens && (rc = zero_tail_rows(xm, B, T, n_mels, lens, st))) return rc;
+  if (lens && (rc = zero_tail_rows(dtype, xm, B, T, n_mels, lens, st))) return rc;
+  // generic (fp32) path: the waveform past each utterance is zero (its conv_post tiles there exit unwritten)
+  if (lens && !std::is_same<E, bf16>::value)
+    MT_CHECK_HIP(hipMemsetAsync(wav, 0, (size_t)B * T * rate_upto((int)ups.size()) * sizeof(float), st));
+  // the generic kernel's ragged lengths (ConvArgs::lens) at the input rate of each conv
+  auto rag = [&](ConvArgs& c, int rate) {
+    c.lens = lens;
+    c.lmul = rate;
+  };
   {
     ConvArgs a = gemm_args(pre, P, B, T);
     a.x0 = xm;
     a.y = XS;
+    rag(a, 1);
     bool dual = false;
     if constexpr (std::is_same<E, bf16>::value) dual = ups_vc(0);
     if (dual) {  // + lrelu(xs) in RA, the first upsampler's vconv input
@@ -517,6 +528,7 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     u.x0 = XS;
     u.y = X;
     u.slope = 0.1f;
+    rag(u, rate_upto((int)i));
     const int C = ups[i].cout;
     bool done_up = false;
     if constexpr (std::is_same<E, bf16>::value) {
@@ -608,6 +620,7 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
           a.x0 = xin;
           a.y = Tb;
           a.slope = 0.1f;
+          rag(a, rate_upto((int)i + 1));
           if ((rc = launch_conv<E, PF_LRELU, 0>(a, st))) return rc;
           src = Tb;
         }
@@ -616,6 +629,7 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
         b.x0 = src;
         b.y = dst;
         b.slope = 0.1f;
+        rag(b, rate_upto((int)i + 1));
         b.resid = xin;
         b.ldr = g.cout;
         b.div = (float)nk;
@@ -646,13 +660,15 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
   ConvArgs c = gemm_args(post, P, B, L);
   c.x0 = XS;
   c.y = wav;
+  rag(c, rate_upto((int)ups.size()));
   c.ldy = 1;
   c.slope = 0.01f;
   return launch_conv<E, PF_LRELU, EF_TANH | EF_OUTF32>(c, st);
 }
 
 bool Vocoder::ragged_supported() const {
-  if (dtype != BF16 || resblock != 1 || post.cin != 32 || post.k != 7 || post.cout != 1) return false;
+  if (dtype != BF16) return true;  // the generic per-layer kernel everywhere (ConvArgs::lens)
+  if (resblock != 1 || post.cin != 32 || post.k != 7 || post.cout != 1) return false;
   for (size_t i = 0; i < ups.size(); ++i)
     if (!ups_vc((int)i) || !(stage_vc((int)i) || stage_vp32((int)i))) return false;
   return true;
@@ -666,7 +682,7 @@ int Vocoder::forward(const void* packed, const float* mel, int B, int T, float* 
   MT_REQUIRE(!lens || (ragged_supported() && B <= RAG_MAXB),
              "vocoder: per-utterance lengths need the bf16 vconv / pair path on every stage and B <= %d", RAG_MAXB);
   if (dtype == BF16) return forward_t<bf16>((const char*)packed, mel, B, T, wav, (char*)ws, st, lens);
-  return forward_t<float>((const char*)packed, mel, B, T, wav, (char*)ws, st, nullptr);
+  return forward_t<float>((const char*)packed, mel, B, T, wav, (char*)ws, st, lens);
 }
 
 }  // namespace mt

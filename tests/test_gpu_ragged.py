@@ -7,7 +7,7 @@ The reference vocodes and denoises one utterance per call, on the mel `synthesiz
     per utterance, the same MFMA accumulation order), and is zero past its length;
   - every row against the fp32 oracle's one-utterance call (rel-RMS 1e-2, the SURVEY §8c bf16 bar);
   - lengths 1 and 0 and a batch where every row is full (= the padded call);
-  - the fp32 engine (no ragged kernel path) runs the per-utterance calls itself.
+  - the fp32 engine on the generic per-layer kernel (within fp32 accumulation order of its one-utterance calls).
 """
 import pytest
 import torch
@@ -72,16 +72,20 @@ def test_vocoder_ragged_full_rows_equal_padded_call():
     assert torch.equal(full, rag)
 
 
-def test_vocoder_ragged_fp32_engine_loops_per_utterance():
+def test_vocoder_ragged_fp32_generic_kernel():
+    """fp32 (parity mode): the generic per-layer kernel runs the ragged batch (ConvArgs::lens). Its tile shape may
+    differ between the batch and a one-utterance call, so rows agree with the one-utterance calls to fp32
+    accumulation order (1e-5, the fp32 waveform tolerance), and are zero past their lengths."""
     g = _gen("fp32")
-    assert not g.engine().ragged_supported()
+    assert g.engine().ragged_supported()
     B, T = 3, 96
     lens = torch.tensor([96, 40, 17])
     mel = _mel(B, T, seed=5).to(DEV)
     wav = g(mel, lengths=lens.to(DEV))
     for b in range(B):
         n = int(lens[b])
-        assert torch.equal(wav[b:b + 1, :, :n * 256], g(mel[b:b + 1, :, :n].contiguous()))
+        one = g(mel[b:b + 1, :, :n].contiguous())
+        assert (wav[b:b + 1, :, :n * 256] - one).abs().max() < 1e-5, b
         assert torch.count_nonzero(wav[b, :, n * 256:]) == 0
 
 
