@@ -214,8 +214,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int lrow = lane >> 3, lp = lane & 7;
   // staging of one step's weights / one chunk's rows; (b, n0, m0) of the cursor's tile are kept
   // decoded by the caller (no integer division per step)
-  // DMA issue: the first `nld` waves (8, or 4 with MT_VCONV_LOADERS=4: the other waves then never stall on a full
-  // memory queue and keep issuing MFMAs) share every staging instruction; only they count and wait on vmcnt
+  // DMA issue: the first `nld` waves (4 by default, 8 with MT_VCONV_LOADERS=8) share every staging instruction and
+  // alone keep the staging cursors and count / wait on vmcnt; the other wave on each SIMD issues MFMAs meanwhile
   const int nld = a.loaders == 4 ? 4 : 8;
   const bool ldr = wave < nld;
   const int wper = NWW * 8 / nld, xper = NXW * 8 / nld;  // instructions per loader wave: one step, one chunk
@@ -584,6 +584,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   tile_of(0, wb, wn0, wm0);
   tile_of(0, xb_, xn0, xm0);
   auto stage_w = [&]() -> int {
+    if (!ldr) return issued;  // non-loader waves keep no staging cursors (nothing to wait on either)
     if (wq < Q) {
       if (ldr) {
         issue_w(wm0, wc, wt, wsl);
@@ -602,6 +603,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     return issued;
   };
   auto stage_x = [&]() {
+    if (!ldr) return;
     if (xti < nmine) {
       if (ldr) {
         issue_x(xb_, xn0, xc, xub);
@@ -864,11 +866,13 @@ static int xcd_tiles_knob() {
 
 int xcd_remap_enabled() { return xcd_tiles_knob(); }
 
-// MT_VCONV_LOADERS=4 (A/B knob, read once): only waves 0-3 issue the staging DMAs (default: all 8)
+// MT_VCONV_LOADERS=8 (A/B knob, read once): every wave issues staging DMAs; default 4: only waves 0-3 issue them and
+// keep the staging cursors, so the other wave on each SIMD runs its MFMAs through that scalar work (vocoder
+// -0.3..-1.2 %, CFM solve -0.8 % at B = 32, vocoder -0.9 % at B = 256; tools/r3ee.sh)
 static int loaders_knob() {
   static const int v = [] {
     const char* e = getenv("MT_VCONV_LOADERS");
-    return e && e[0] == '4' ? 4 : 8;
+    return e && e[0] == '8' ? 8 : 4;
   }();
   return v;
 }
