@@ -24,6 +24,7 @@
 // boundaries, so the next tile's first weights and rows land while this tile's epilogue stores.
 // Zero padding (frames outside [0, L)) is read from a zero page instead of branching.
 #include <algorithm>
+#include <vector>
 #include <climits>
 #include <cstdlib>
 #include <type_traits>
@@ -38,6 +39,7 @@ namespace mt {
 namespace {
 constexpr int BN = 256, NT = 512;                // BN: frames per tile (128 for small 1x1 grids)
 constexpr int MMAX = 1024;                        // largest C_out (per-channel epilogue tables in LDS)
+constexpr int PF_MAX = 32;                        // most 1 KiB pieces of the next launch's weights per workgroup
 constexpr int BMP = 64;                           // packed weight rows are padded to a multiple of this
 // Tile geometry by output rows per workgroup: BM = 128 (waves 2 in M x 4 in N, 64x64 per wave) for
 // C_out % 128 == 0, BM = 64 (1 x 8 waves, 64x32 per wave) for the 64-channel stage.
@@ -580,6 +582,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   for (int i = 0; i < NXM; ++i) mX[i] = 0;
   int xti = 0, xc = 0, xub = 0;        // next chunk to stage and its row buffer
   int wti = 0, wc = 0, wt = 0, wq = 0, wsl = 0; // next weight step to stage and its ring slot
+  bool pfd = false;                                // the next launch's weights prefetched (VConvArgs::pf)
   int wb, wn0, wm0, xb_, xn0, xm0;  // decoded tiles of the weight / row cursors
   tile_of(0, wb, wn0, wm0);
   tile_of(0, xb_, xn0, xm0);
@@ -599,6 +602,20 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
         }
       }
       ++wq;
+    } else if (a.pf && !pfd) {
+      // every step of this workgroup is staged: warm the XCD's L2 with a share of the NEXT launch's weight image
+      // (VConvArgs::pf; the XCD's workgroups split it, workgroup g running on XCD g % 8) by DMAs into the weight
+      // slot no later step uses; they join the counted stream after every needed DMA, so no wait includes them
+      // unless it has to
+      pfd = true;
+      const int G = (int)gridDim.x, xg = (int)blockIdx.x & 7;
+      const int per_xcd = (G - xg + 7) >> 3, np = (a.pf_bytes + 1023) >> 10;
+      const int share = min((np + per_xcd - 1) / per_xcd, PF_MAX), p0 = ((int)blockIdx.x >> 3) * share;
+      for (int j = wave; j < share && p0 + j < np; j += nld) {
+        const int byte = min((p0 + j) * 1024 + lane * 16, a.pf_bytes - 16);
+        glds16(a.pf + byte, smem + wsl * WSLOT);
+        ++issued;
+      }
     }
     return issued;
   };
@@ -739,6 +756,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       }
     }
   }
+  // the prefetch DMAs write (dead) LDS: they land before the workgroup's LDS can be handed to another one
+  if (pfd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if defined(VCONV_EXP)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -955,6 +974,8 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(!(ef & VE_MASK) || a0.emask, "vconv f32: mask");
   VConvArgs a = a0;
   a.c0 = a.cin;
+  a.pf = nullptr;
+  a.pf_bytes = 0;
   a.xcd_tiles = xcd_tiles_knob();
   const bool k1 = a.taps == 1;
   if (k1) {
@@ -1014,6 +1035,48 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
 }
 
 
+namespace {
+struct PfPlan {
+  int mode = 0;
+  std::vector<std::pair<const bf16*, int>> seq;  // weight image and its bytes, per bf16 launch in order
+  size_t pos = 0;
+};
+thread_local PfPlan g_pf;
+}  // namespace
+
+void vconv_pf_begin(int mode) {
+  g_pf.mode = mode;
+  g_pf.pos = 0;
+  if (mode == 1) g_pf.seq.clear();
+}
+
+int vconv_pf_enabled() {
+  static const int on = [] {
+    const char* e = getenv("MT_VCONV_PF");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on;
+}
+
+// this launch's place in the plan: record its image, or take the next launch's as the prefetch
+static void pf_assign(VConvArgs& a) {
+  a.pf = nullptr;
+  a.pf_bytes = 0;
+  const long wbytes = (long)(a.cin / 64) * a.taps * a.Mpad * 64 * 2;
+  if (g_pf.mode == 1) {
+    g_pf.seq.emplace_back(a.w, (int)std::min<long>(wbytes, 1l << 30));
+  } else if (g_pf.mode == 2) {
+    if (g_pf.pos < g_pf.seq.size() && g_pf.seq[g_pf.pos].first == a.w) {
+      if (++g_pf.pos < g_pf.seq.size()) {
+        a.pf = reinterpret_cast<const char*>(g_pf.seq[g_pf.pos].first);
+        a.pf_bytes = g_pf.seq[g_pf.pos].second;
+      }
+    } else {
+      g_pf.mode = 0;  // not the recorded chain
+    }
+  }
+}
+
 int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(a0.x && a0.w && a0.bias && a0.y && a0.zero && a0.trash, "vconv: null pointer");
   if (a0.f32) return launch_vconv_f32(ef, a0, st);
@@ -1037,6 +1100,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   VConvArgs a = a0;
   a.xcd_tiles = xcd_tiles_knob();
   a.loaders = loaders_knob();
+  pf_assign(a);
   if (a.c0 == 0) a.c0 = a.cin;  // one source
   MT_REQUIRE(a.c0 == a.cin || (a.x1 && a.c0 % 64 == 0 && a.c0 > 0 && a.c0 < a.cin), "vconv: channel split %d/%d",
              a.c0, a.cin);
@@ -1103,6 +1167,12 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   // XCD-major ownership pays where a launch's activations fit the XCDs' L2 (the decoder at B = 32: CFM solve
   // 8.71 -> 8.61 ms); on larger grids (B = 256: 40.2 vs 40.5 ms) the round-robin walk's weight reuse wins
   a.xcd_tiles = a.xcd_tiles && ntiles <= 3L * G;
+  // the prefetch pays on multi-round grids (B = 256 decoder: 42.6 -> 42.3 ms); on one-round grids (B = 32) every
+  // workgroup's staging ends in its prologue, where the prefetch competes with the first tile's DMAs (+0.6 %)
+  if (ntiles <= G) {
+    a.pf = nullptr;
+    a.pf_bytes = 0;
+  }
   MT_REQUIRE(!(ef & VE_GNSTATS) || a0.gn_parts == 0 || a0.gn_parts == ((a.L + tf - 1) / tf) * (8 / (BM / 64)),
              "vconv: caller expects %d GroupNorm partial slots, the launch writes a different count", a0.gn_parts);
   {
