@@ -317,8 +317,9 @@ size_t attention_part_bytes(int B, int T, int heads) {
 // block needs neither Q, K, V of every frame nor the per-frame out-projection: one masked mean of xhat per
 // utterance and two 256-wide GEMVs. BasicTransformerBlock's x + attn1(...) (model.py:733-737) becomes x_j += o.
 // part: grid (S, B), slice s of utterance b -> part[b][s][0..255] = sum over masked frames of xhat, [256] = count
-// apply: grid (S, B), merges the S partials (slice order), the GEMVs (every block, redundantly: 2 x 32 K MACs),
-//   then x_j = bf16(x_j + o) for the slice's frames + the (mean, M2) per 64-channel slab of the stored row
+// vec: grid B, merges the utterance's S partials (slice order) and runs the two GEMVs -> o_b (one launch per
+//   utterance: the round-2 apply that redid them in every slice's workgroup was 1.56 vs 1.25 ms per step)
+// apply: grid (S, B), x_j = bf16(x_j + o) for the slice's frames + the (mean, M2) per 64-channel slab of the stored row
 //   (the LayerNorm partials LN3 reads, VE_ROWSTATS format). Rounding as the GEMM path: V averaged in fp32,
 //   o rounded to bf16 (the attention output was stored bf16), x + (W_o o + b_o) in fp32, stored bf16.
 constexpr int UNI_C = 256, UNI_PART = UNI_C + 4;  // UNI_PSMAX (mt_misc.h): part slices per utterance
