@@ -89,6 +89,7 @@ struct VConvArgs {
   // launch's workgroups pull into their XCDs' L2 once their own staging is done (null: none)
   const char* pf;
   int pf_bytes;
+  int pf_late;  // 1: only from the workgroup's second-to-last step on (one-round grids)
 };
 
 // L2 warm-up plan of a launch chain (the decoder's captured evaluation chain): mode 1 records the weight image of

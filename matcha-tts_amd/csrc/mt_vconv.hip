@@ -583,11 +583,13 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   int xti = 0, xc = 0, xub = 0;        // next chunk to stage and its row buffer
   int wti = 0, wc = 0, wt = 0, wq = 0, wsl = 0; // next weight step to stage and its ring slot
   bool pfd = false;                                // the next launch's weights prefetched (VConvArgs::pf)
+  int swc = 0;                                     // stage_w calls so far
   int wb, wn0, wm0, xb_, xn0, xm0;  // decoded tiles of the weight / row cursors
   tile_of(0, wb, wn0, wm0);
   tile_of(0, xb_, xn0, xm0);
   auto stage_w = [&]() -> int {
     if (!ldr) return issued;  // non-loader waves keep no staging cursors (nothing to wait on either)
+    ++swc;                    // calls: NWSLOT - 1 in the prologue, then one per step
     if (wq < Q) {
       if (ldr) {
         issue_w(wm0, wc, wt, wsl);
@@ -602,7 +604,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
         }
       }
       ++wq;
-    } else if (a.pf && !pfd) {
+    } else if (a.pf && !pfd && (!a.pf_late || swc >= NWSLOT + Q - 2)) {
       // every step of this workgroup is staged: warm the XCD's L2 with a share of the NEXT launch's weight image
       // (VConvArgs::pf; the XCD's workgroups split it, workgroup g running on XCD g % 8) by DMAs into the weight
       // slot no later step uses; they join the counted stream after every needed DMA, so no wait includes them
@@ -1058,6 +1060,15 @@ int vconv_pf_enabled() {
   return on;
 }
 
+// one-round grids: -1 no prefetch, 1 prefetch from the second-to-last step (MT_VCONV_PF_LATE, A/B knob)
+static int pf_late_knob() {
+  static const int v = [] {
+    const char* e = getenv("MT_VCONV_PF_LATE");
+    return e && e[0] == '1' ? 1 : -1;
+  }();
+  return v;
+}
+
 // this launch's place in the plan: record its image, or take the next launch's as the prefetch
 static void pf_assign(VConvArgs& a) {
   a.pf = nullptr;
@@ -1169,7 +1180,8 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   a.xcd_tiles = a.xcd_tiles && ntiles <= 3L * G;
   // the prefetch pays on multi-round grids (B = 256 decoder: 42.6 -> 42.3 ms); on one-round grids (B = 32) every
   // workgroup's staging ends in its prologue, where the prefetch competes with the first tile's DMAs (+0.6 %)
-  if (ntiles <= G) {
+  a.pf_late = ntiles <= G ? pf_late_knob() : 0;
+  if (ntiles <= G && a.pf_late < 0) {
     a.pf = nullptr;
     a.pf_bytes = 0;
   }
