@@ -90,6 +90,7 @@ struct VConvArgs {
   const char* pf;
   int pf_bytes;
   int pf_late;  // 1: only from the workgroup's second-to-last step on (one-round grids)
+  int pro_mode;  // set by launch_vconv: 0 the loaders issue the prologue DMAs, 1 all waves chunk 0 + step 0, 2 all of it
 };
 
 // L2 warm-up plan of a launch chain (the decoder's captured evaluation chain): mode 1 records the weight image of

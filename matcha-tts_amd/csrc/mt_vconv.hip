@@ -221,13 +221,16 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int nld = a.loaders == 4 ? 4 : 8;
   const bool ldr = wave < nld;
   const int wper = NWW * 8 / nld, xper = NXW * 8 / nld;  // instructions per loader wave: one step, one chunk
+  // the split of the stage being issued: the prologue may deal its stages over all 8 waves (VConvArgs::pro_mode)
+  int cnl = nld, cpw = wper, cpx = xper;
+  bool pro = a.pro_mode > 0;
   auto issue_w = [&](int m0, int c, int t, int slot) {
     const char* base = reinterpret_cast<const char*>(a.w) + ((size_t)(c * taps + t) * a.Mpad + m0) * 128;
     char* dst = smem + slot * WSLOT;
 #pragma unroll
     for (int i = 0; i < 2 * NWW; ++i) {
-      if (i >= wper) break;
-      const int j = wave * wper + i;
+      if (i >= cpw) break;
+      const int j = wave * cpw + i;
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       glds16(base + r * 128 + q * 16, dst + j * 1024);
@@ -245,8 +248,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     char* dst = smem + NWSLOT * WSLOT + buf * XBUF;
 #pragma unroll
     for (int i = 0; i < 2 * NXW; ++i) {
-      if (i >= xper) break;
-      const int j = wave + nld * i;
+      if (i >= cpx) break;
+      const int j = wave + cnl * i;
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
@@ -588,12 +591,12 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   tile_of(0, wb, wn0, wm0);
   tile_of(0, xb_, xn0, xm0);
   auto stage_w = [&]() -> int {
-    if (!ldr) return issued;  // non-loader waves keep no staging cursors (nothing to wait on either)
+    if (!ldr && !pro) return issued;  // non-loader waves keep no staging cursors (nothing to wait on either)
     ++swc;                    // calls: NWSLOT - 1 in the prologue, then one per step
     if (wq < Q) {
-      if (ldr) {
+      if (ldr || pro) {
         issue_w(wm0, wc, wt, wsl);
-        issued += wper;
+        issued += cpw;
       }
       if (++wsl == NWSLOT) wsl = 0;
       if (++wt == taps) {
@@ -604,7 +607,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
         }
       }
       ++wq;
-    } else if (a.pf && !pfd && (!a.pf_late || swc >= NWSLOT + Q - 2)) {
+    } else if (ldr && a.pf && !pfd && (!a.pf_late || swc >= NWSLOT + Q - 2)) {
       // every step of this workgroup is staged: warm the XCD's L2 with a share of the NEXT launch's weight image
       // (VConvArgs::pf; the XCD's workgroups split it, workgroup g running on XCD g % 8) by DMAs into the weight
       // slot no later step uses; they join the counted stream after every needed DMA, so no wait includes them
@@ -622,11 +625,11 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     return issued;
   };
   auto stage_x = [&]() {
-    if (!ldr) return;
+    if (!ldr && !pro) return;
     if (xti < nmine) {
-      if (ldr) {
+      if (ldr || pro) {
         issue_x(xb_, xn0, xc, xub);
-        issued += xper;
+        issued += cpx;
       }
 #pragma unroll
       for (int i = 0; i < NXM; ++i)
@@ -693,15 +696,30 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       ++issued;
     }
   }
+  // pro_mode 1: all 8 waves issue the rows of chunk 0 and the weights of step 0, the loaders the rest;
+  // 2: all 8 waves issue the whole prologue; 0: the loaders issue it. Waves that are not loaders wait for
+  // everything they issued before the first barrier.
+  if (pro) cnl = 8, cpw = NWW, cpx = NXW;
+  int m0w;
+  if (a.pro_mode == 1) {
+    stage_x();
+    m0w = stage_w();
+    pro = false, cnl = nld, cpw = wper, cpx = xper;
 #pragma unroll
-  for (int i = 0; i < NXB - 1; ++i) stage_x();
-  const int m0w = stage_w();
+    for (int i = 1; i < NXB - 1; ++i) stage_x();
+  } else {
+#pragma unroll
+    for (int i = 0; i < NXB - 1; ++i) stage_x();
+    m0w = stage_w();
+  }
   int mW[NWSLOT - 2];  // `issued` after the weights of steps qq+1 .. qq+NWSLOT-2
 #pragma unroll
   for (int i = 0; i < NWSLOT - 2; ++i) mW[i] = stage_w();
+  pro = false, cnl = nld, cpw = wper, cpx = xper;
   {
     const int mx = pop_x();
     if (ldr) wait_vmcnt(issued - max(m0w, mx));
+    else if (a.pro_mode > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   raw_barrier();
 #if defined(VCONV_TS)
@@ -1061,6 +1079,17 @@ int vconv_pf_enabled() {
 }
 
 // one-round grids: -1 no prefetch, 1 prefetch from the second-to-last step (MT_VCONV_PF_LATE, A/B knob)
+// prologue DMA issue split (VConvArgs::pro_mode; MT_VCONV_PRO = 0 / 1 / 2, default 1): all 8 waves dealing chunk 0
+// and step 0 took the B = 32 CFM solve 9.273 -> 9.228 ms (2 A/B pairs, vocoder within noise); the whole prologue
+// over 8 waves (2) was slower (9.32 ms: the non-loaders then wait for the ring's deepest stages)
+static int pro_knob() {
+  static const int v = [] {
+    const char* e = getenv("MT_VCONV_PRO");
+    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
+  }();
+  return v;
+}
+
 static int pf_late_knob() {
   static const int v = [] {
     const char* e = getenv("MT_VCONV_PF_LATE");
@@ -1111,6 +1140,7 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   VConvArgs a = a0;
   a.xcd_tiles = xcd_tiles_knob();
   a.loaders = loaders_knob();
+  a.pro_mode = a.loaders == 4 ? pro_knob() : 0;
   pf_assign(a);
   if (a.c0 == 0) a.c0 = a.cin;  // one source
   MT_REQUIRE(a.c0 == a.cin || (a.x1 && a.c0 % 64 == 0 && a.c0 > 0 && a.c0 < a.cin), "vconv: channel split %d/%d",
