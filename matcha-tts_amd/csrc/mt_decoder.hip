@@ -886,24 +886,8 @@ int Decoder::chain_graph(const char* P, const Work& w, const TimeSched& ts, int 
     }
   }
   if (!gc.cap) MT_CHECK_HIP(hipStreamCreateWithFlags(&gc.cap, hipStreamNonBlocking));
-  const bool pf = vconv_pf_enabled();
-  if (pf) {
-    // a first capture records the chain's mt_vconv weight images in launch order (nothing runs); the kept capture
-    // gives every launch the next one's image to pull into L2 behind its own work (VConvArgs::pf)
-    vconv_pf_begin(1);
-    MT_CHECK_HIP(hipStreamBeginCapture(gc.cap, hipStreamCaptureModeThreadLocal));
-    const int rc0 = solve_chain(P, w, ts, S, B, T, n_steps, solver, gc.cap);
-    hipGraph_t g0 = nullptr;
-    const hipError_t e0 = hipStreamEndCapture(gc.cap, &g0);
-    if (g0) (void)hipGraphDestroy(g0);
-    vconv_pf_begin(0);
-    if (rc0) return rc0;
-    MT_CHECK_HIP(e0);
-  }
   MT_CHECK_HIP(hipStreamBeginCapture(gc.cap, hipStreamCaptureModeThreadLocal));
-  vconv_pf_begin(pf ? 2 : 0);
   const int rc = solve_chain(P, w, ts, S, B, T, n_steps, solver, gc.cap);
-  vconv_pf_begin(0);
   hipGraph_t g = nullptr;
   const hipError_t e = hipStreamEndCapture(gc.cap, &g);
   if (rc || e != hipSuccess || !g) {

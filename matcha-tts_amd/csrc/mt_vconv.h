@@ -85,19 +85,7 @@ struct VConvArgs {
   int lmul;
   int xcd_tiles;  // set by launch_vconv: 1 = XCD-major tile ownership (mt_vconv.hip), 0 = round-robin walk
   int loaders;    // set by launch_vconv: waves that issue the staging DMAs (8, or 4)
-  // set by launch_vconv under a prefetch plan (vconv_pf_begin): the next vconv launch's weight image, which this
-  // launch's workgroups pull into their XCDs' L2 once their own staging is done (null: none)
-  const char* pf;
-  int pf_bytes;
-  int pf_late;  // 1: only from the workgroup's second-to-last step on (one-round grids)
-  int pro_mode;  // set by launch_vconv: 0 the loaders issue the prologue DMAs, 1 all waves chunk 0 + step 0, 2 all of it
 };
-
-// L2 warm-up plan of a launch chain (the decoder's captured evaluation chain): mode 1 records the weight image of
-// every bf16 launch_vconv in order, mode 2 gives launch i the image of launch i + 1 as VConvArgs::pf (a launch whose
-// weights differ from the recorded sequence ends the plan); 0 ends either. MT_VCONV_PF=0 disables it.
-void vconv_pf_begin(int mode);
-int vconv_pf_enabled();
 
 // LayerNorm (mean, rstd) of a 256-channel frame from its 4 slab partials (mean_i, M2_i), 64 values each,
 // packed (m0, q0, m1, q1), (m2, q2, m3, q3): Chan's merge, var = M2 / 256

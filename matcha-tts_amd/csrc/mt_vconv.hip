@@ -24,7 +24,6 @@
 // boundaries, so the next tile's first weights and rows land while this tile's epilogue stores.
 // Zero padding (frames outside [0, L)) is read from a zero page instead of branching.
 #include <algorithm>
-#include <vector>
 #include <climits>
 #include <cstdlib>
 #include <type_traits>
@@ -39,7 +38,6 @@ namespace mt {
 namespace {
 constexpr int BN = 256, NT = 512;                // BN: frames per tile (128 for small 1x1 grids)
 constexpr int MMAX = 1024;                        // largest C_out (per-channel epilogue tables in LDS)
-constexpr int PF_MAX = 32;                        // most 1 KiB pieces of the next launch's weights per workgroup
 constexpr int BMP = 64;                           // packed weight rows are padded to a multiple of this
 // Tile geometry by output rows per workgroup: BM = 128 (waves 2 in M x 4 in N, 64x64 per wave) for
 // C_out % 128 == 0, BM = 64 (1 x 8 waves, 64x32 per wave) for the 64-channel stage.
@@ -221,16 +219,13 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int nld = a.loaders == 4 ? 4 : 8;
   const bool ldr = wave < nld;
   const int wper = NWW * 8 / nld, xper = NXW * 8 / nld;  // instructions per loader wave: one step, one chunk
-  // the split of the stage being issued: the prologue may deal its stages over all 8 waves (VConvArgs::pro_mode)
-  int cnl = nld, cpw = wper, cpx = xper;
-  bool pro = a.pro_mode > 0;
   auto issue_w = [&](int m0, int c, int t, int slot) {
     const char* base = reinterpret_cast<const char*>(a.w) + ((size_t)(c * taps + t) * a.Mpad + m0) * 128;
     char* dst = smem + slot * WSLOT;
 #pragma unroll
     for (int i = 0; i < 2 * NWW; ++i) {
-      if (i >= cpw) break;
-      const int j = wave * cpw + i;
+      if (i >= wper) break;
+      const int j = wave * wper + i;
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       glds16(base + r * 128 + q * 16, dst + j * 1024);
@@ -248,8 +243,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     char* dst = smem + NWSLOT * WSLOT + buf * XBUF;
 #pragma unroll
     for (int i = 0; i < 2 * NXW; ++i) {
-      if (i >= cpx) break;
-      const int j = wave + cnl * i;
+      if (i >= xper) break;
+      const int j = wave + nld * i;
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
@@ -585,18 +580,15 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   for (int i = 0; i < NXM; ++i) mX[i] = 0;
   int xti = 0, xc = 0, xub = 0;        // next chunk to stage and its row buffer
   int wti = 0, wc = 0, wt = 0, wq = 0, wsl = 0; // next weight step to stage and its ring slot
-  bool pfd = false;                                // the next launch's weights prefetched (VConvArgs::pf)
-  int swc = 0;                                     // stage_w calls so far
   int wb, wn0, wm0, xb_, xn0, xm0;  // decoded tiles of the weight / row cursors
   tile_of(0, wb, wn0, wm0);
   tile_of(0, xb_, xn0, xm0);
   auto stage_w = [&]() -> int {
-    if (!ldr && !pro) return issued;  // non-loader waves keep no staging cursors (nothing to wait on either)
-    ++swc;                    // calls: NWSLOT - 1 in the prologue, then one per step
+    if (!ldr) return issued;  // non-loader waves keep no staging cursors (nothing to wait on either)
     if (wq < Q) {
-      if (ldr || pro) {
+      if (ldr) {
         issue_w(wm0, wc, wt, wsl);
-        issued += cpw;
+        issued += wper;
       }
       if (++wsl == NWSLOT) wsl = 0;
       if (++wt == taps) {
@@ -607,29 +599,15 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
         }
       }
       ++wq;
-    } else if (ldr && a.pf && !pfd && (!a.pf_late || swc >= NWSLOT + Q - 2)) {
-      // every step of this workgroup is staged: warm the XCD's L2 with a share of the NEXT launch's weight image
-      // (VConvArgs::pf; the XCD's workgroups split it, workgroup g running on XCD g % 8) by DMAs into the weight
-      // slot no later step uses; they join the counted stream after every needed DMA, so no wait includes them
-      // unless it has to
-      pfd = true;
-      const int G = (int)gridDim.x, xg = (int)blockIdx.x & 7;
-      const int per_xcd = (G - xg + 7) >> 3, np = (a.pf_bytes + 1023) >> 10;
-      const int share = min((np + per_xcd - 1) / per_xcd, PF_MAX), p0 = ((int)blockIdx.x >> 3) * share;
-      for (int j = wave; j < share && p0 + j < np; j += nld) {
-        const int byte = min((p0 + j) * 1024 + lane * 16, a.pf_bytes - 16);
-        glds16(a.pf + byte, smem + wsl * WSLOT);
-        ++issued;
-      }
     }
     return issued;
   };
   auto stage_x = [&]() {
-    if (!ldr && !pro) return;
+    if (!ldr) return;
     if (xti < nmine) {
-      if (ldr || pro) {
+      if (ldr) {
         issue_x(xb_, xn0, xc, xub);
-        issued += cpx;
+        issued += xper;
       }
 #pragma unroll
       for (int i = 0; i < NXM; ++i)
@@ -696,30 +674,15 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       ++issued;
     }
   }
-  // pro_mode 1: all 8 waves issue the rows of chunk 0 and the weights of step 0, the loaders the rest;
-  // 2: all 8 waves issue the whole prologue; 0: the loaders issue it. Waves that are not loaders wait for
-  // everything they issued before the first barrier.
-  if (pro) cnl = 8, cpw = NWW, cpx = NXW;
-  int m0w;
-  if (a.pro_mode == 1) {
-    stage_x();
-    m0w = stage_w();
-    pro = false, cnl = nld, cpw = wper, cpx = xper;
 #pragma unroll
-    for (int i = 1; i < NXB - 1; ++i) stage_x();
-  } else {
-#pragma unroll
-    for (int i = 0; i < NXB - 1; ++i) stage_x();
-    m0w = stage_w();
-  }
+  for (int i = 0; i < NXB - 1; ++i) stage_x();
+  const int m0w = stage_w();
   int mW[NWSLOT - 2];  // `issued` after the weights of steps qq+1 .. qq+NWSLOT-2
 #pragma unroll
   for (int i = 0; i < NWSLOT - 2; ++i) mW[i] = stage_w();
-  pro = false, cnl = nld, cpw = wper, cpx = xper;
   {
     const int mx = pop_x();
     if (ldr) wait_vmcnt(issued - max(m0w, mx));
-    else if (a.pro_mode > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   raw_barrier();
 #if defined(VCONV_TS)
@@ -776,8 +739,6 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       }
     }
   }
-  // the prefetch DMAs write (dead) LDS: they land before the workgroup's LDS can be handed to another one
-  if (pfd) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #if defined(VCONV_EXP)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -994,8 +955,6 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(!(ef & VE_MASK) || a0.emask, "vconv f32: mask");
   VConvArgs a = a0;
   a.c0 = a.cin;
-  a.pf = nullptr;
-  a.pf_bytes = 0;
   a.xcd_tiles = xcd_tiles_knob();
   const bool k1 = a.taps == 1;
   if (k1) {
@@ -1055,68 +1014,6 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
 }
 
 
-namespace {
-struct PfPlan {
-  int mode = 0;
-  std::vector<std::pair<const bf16*, int>> seq;  // weight image and its bytes, per bf16 launch in order
-  size_t pos = 0;
-};
-thread_local PfPlan g_pf;
-}  // namespace
-
-void vconv_pf_begin(int mode) {
-  g_pf.mode = mode;
-  g_pf.pos = 0;
-  if (mode == 1) g_pf.seq.clear();
-}
-
-int vconv_pf_enabled() {
-  static const int on = [] {
-    const char* e = getenv("MT_VCONV_PF");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return on;
-}
-
-// one-round grids: -1 no prefetch, 1 prefetch from the second-to-last step (MT_VCONV_PF_LATE, A/B knob)
-// prologue DMA issue split (VConvArgs::pro_mode; MT_VCONV_PRO = 0 / 1 / 2, default 1): all 8 waves dealing chunk 0
-// and step 0 took the B = 32 CFM solve 9.273 -> 9.228 ms (2 A/B pairs, vocoder within noise); the whole prologue
-// over 8 waves (2) was slower (9.32 ms: the non-loaders then wait for the ring's deepest stages)
-static int pro_knob() {
-  static const int v = [] {
-    const char* e = getenv("MT_VCONV_PRO");
-    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
-  }();
-  return v;
-}
-
-static int pf_late_knob() {
-  static const int v = [] {
-    const char* e = getenv("MT_VCONV_PF_LATE");
-    return e && e[0] == '1' ? 1 : -1;
-  }();
-  return v;
-}
-
-// this launch's place in the plan: record its image, or take the next launch's as the prefetch
-static void pf_assign(VConvArgs& a) {
-  a.pf = nullptr;
-  a.pf_bytes = 0;
-  const long wbytes = (long)(a.cin / 64) * a.taps * a.Mpad * 64 * 2;
-  if (g_pf.mode == 1) {
-    g_pf.seq.emplace_back(a.w, (int)std::min<long>(wbytes, 1l << 30));
-  } else if (g_pf.mode == 2) {
-    if (g_pf.pos < g_pf.seq.size() && g_pf.seq[g_pf.pos].first == a.w) {
-      if (++g_pf.pos < g_pf.seq.size()) {
-        a.pf = reinterpret_cast<const char*>(g_pf.seq[g_pf.pos].first);
-        a.pf_bytes = g_pf.seq[g_pf.pos].second;
-      }
-    } else {
-      g_pf.mode = 0;  // not the recorded chain
-    }
-  }
-}
-
 int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(a0.x && a0.w && a0.bias && a0.y && a0.zero && a0.trash, "vconv: null pointer");
   if (a0.f32) return launch_vconv_f32(ef, a0, st);
@@ -1140,8 +1037,6 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   VConvArgs a = a0;
   a.xcd_tiles = xcd_tiles_knob();
   a.loaders = loaders_knob();
-  a.pro_mode = a.loaders == 4 ? pro_knob() : 0;
-  pf_assign(a);
   if (a.c0 == 0) a.c0 = a.cin;  // one source
   MT_REQUIRE(a.c0 == a.cin || (a.x1 && a.c0 % 64 == 0 && a.c0 > 0 && a.c0 < a.cin), "vconv: channel split %d/%d",
              a.c0, a.cin);
@@ -1208,13 +1103,6 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   // XCD-major ownership pays where a launch's activations fit the XCDs' L2 (the decoder at B = 32: CFM solve
   // 8.71 -> 8.61 ms); on larger grids (B = 256: 40.2 vs 40.5 ms) the round-robin walk's weight reuse wins
   a.xcd_tiles = a.xcd_tiles && ntiles <= 3L * G;
-  // the prefetch pays on multi-round grids (B = 256 decoder: 42.6 -> 42.3 ms); on one-round grids (B = 32) every
-  // workgroup's staging ends in its prologue, where the prefetch competes with the first tile's DMAs (+0.6 %)
-  a.pf_late = ntiles <= G ? pf_late_knob() : 0;
-  if (ntiles <= G && a.pf_late < 0) {
-    a.pf = nullptr;
-    a.pf_bytes = 0;
-  }
   MT_REQUIRE(!(ef & VE_GNSTATS) || a0.gn_parts == 0 || a0.gn_parts == ((a.L + tf - 1) / tf) * (8 / (BM / 64)),
              "vconv: caller expects %d GroupNorm partial slots, the launch writes a different count", a0.gn_parts);
   {
