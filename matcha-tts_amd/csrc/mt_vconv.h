@@ -84,7 +84,6 @@ struct VConvArgs {
   const int* lens;
   int lmul;
   int xcd_tiles;  // set by launch_vconv: 1 = XCD-major tile ownership (mt_vconv.hip), 0 = round-robin walk
-  int loaders;    // set by launch_vconv: waves that issue the staging DMAs (8, or 4)
 };
 
 // LayerNorm (mean, rstd) of a 256-channel frame from its 4 slab partials (mean_i, M2_i), 64 values each,

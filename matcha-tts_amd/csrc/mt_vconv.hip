@@ -214,18 +214,12 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   const int lrow = lane >> 3, lp = lane & 7;
   // staging of one step's weights / one chunk's rows; (b, n0, m0) of the cursor's tile are kept
   // decoded by the caller (no integer division per step)
-  // DMA issue: the first `nld` waves (4 by default, 8 with MT_VCONV_LOADERS=8) share every staging instruction and
-  // alone keep the staging cursors and count / wait on vmcnt; the other wave on each SIMD issues MFMAs meanwhile
-  const int nld = a.loaders == 4 ? 4 : 8;
-  const bool ldr = wave < nld;
-  const int wper = NWW * 8 / nld, xper = NXW * 8 / nld;  // instructions per loader wave: one step, one chunk
   auto issue_w = [&](int m0, int c, int t, int slot) {
     const char* base = reinterpret_cast<const char*>(a.w) + ((size_t)(c * taps + t) * a.Mpad + m0) * 128;
     char* dst = smem + slot * WSLOT;
 #pragma unroll
-    for (int i = 0; i < 2 * NWW; ++i) {
-      if (i >= wper) break;
-      const int j = wave * wper + i;
+    for (int i = 0; i < NWW; ++i) {
+      const int j = wave * NWW + i;
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       glds16(base + r * 128 + q * 16, dst + j * 1024);
@@ -242,9 +236,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
                         : reinterpret_cast<const char*>(a.x1) + ((size_t)b * L * (cin - c0) + (c * CHR - c0)) * ES;
     char* dst = smem + NWSLOT * WSLOT + buf * XBUF;
 #pragma unroll
-    for (int i = 0; i < 2 * NXW; ++i) {
-      if (i >= xper) break;
-      const int j = wave + nld * i;
+    for (int i = 0; i < NXW; ++i) {
+      const int j = wave + 8 * i;
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
@@ -584,12 +577,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   tile_of(0, wb, wn0, wm0);
   tile_of(0, xb_, xn0, xm0);
   auto stage_w = [&]() -> int {
-    if (!ldr) return issued;  // non-loader waves keep no staging cursors (nothing to wait on either)
     if (wq < Q) {
-      if (ldr) {
-        issue_w(wm0, wc, wt, wsl);
-        issued += wper;
-      }
+      issue_w(wm0, wc, wt, wsl);
+      issued += NWW;
       if (++wsl == NWSLOT) wsl = 0;
       if (++wt == taps) {
         wt = 0;
@@ -603,12 +593,9 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     return issued;
   };
   auto stage_x = [&]() {
-    if (!ldr) return;
     if (xti < nmine) {
-      if (ldr) {
-        issue_x(xb_, xn0, xc, xub);
-        issued += xper;
-      }
+      issue_x(xb_, xn0, xc, xub);
+      issued += NXW;
 #pragma unroll
       for (int i = 0; i < NXM; ++i)
         if (i == nX) mX[i] = issued;  // constant register index, wave-uniform select
@@ -665,7 +652,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     // 1 KiB per wave-instruction (lane-linear), instructions dealt round-robin over the waves; lanes past the
     // table's end read the zero page. Loads retire in order, so the first counted wait covers them.
     const int per = (a.M * 4 + 1023) >> 10;
-    for (int j = wave; ldr && j < ntab * per; j += nld) {
+    for (int j = wave; j < ntab * per; j += 8) {
       const int ti = j / per, part = j - ti * per;
       const int byte = part * 1024 + lane * 16;
       const char* src = byte < a.M * 4 ? reinterpret_cast<const char*>(tabs[ti]) + byte
@@ -680,10 +667,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   int mW[NWSLOT - 2];  // `issued` after the weights of steps qq+1 .. qq+NWSLOT-2
 #pragma unroll
   for (int i = 0; i < NWSLOT - 2; ++i) mW[i] = stage_w();
-  {
-    const int mx = pop_x();
-    if (ldr) wait_vmcnt(issued - max(m0w, mx));
-  }
+  wait_vmcnt(issued - max(m0w, pop_x()));
   raw_barrier();
 #if defined(VCONV_TS)
   ts_v[1] = __builtin_amdgcn_s_memrealtime();
@@ -701,10 +685,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     }
     // publish step qq+1's weights (and rows, on a chunk's first tap); every wave's reads of step qq-1
     // are done (lgkmcnt), so its weight slot and, on a chunk change, the old row buffer may be restaged
-    if (qq + 1 < Q) {
-      const int mx = rt == 0 ? pop_x() : 0;
-      if (ldr) wait_vmcnt(issued - (rt == 0 ? max(mW[0], mx) : mW[0]));
-    }
+    if (qq + 1 < Q) wait_vmcnt(issued - (rt == 0 ? max(mW[0], pop_x()) : mW[0]));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     raw_barrier();
     const bool tile_end = t == taps - 1 && c == nch - 1;
@@ -866,17 +847,6 @@ static int xcd_tiles_knob() {
 
 int xcd_remap_enabled() { return xcd_tiles_knob(); }
 
-// MT_VCONV_LOADERS=8 (A/B knob, read once): every wave issues staging DMAs; default 4: only waves 0-3 issue them and
-// keep the staging cursors, so the other wave on each SIMD runs its MFMAs through that scalar work (vocoder
-// -0.3..-1.2 %, CFM solve -0.8 % at B = 32, vocoder -0.9 % at B = 256; tools/r3ee.sh)
-static int loaders_knob() {
-  static const int v = [] {
-    const char* e = getenv("MT_VCONV_LOADERS");
-    return e && e[0] == '8' ? 8 : 4;
-  }();
-  return v;
-}
-
 static int cu_count() {
   static int n = 0;
   if (n == 0) {
@@ -1036,7 +1006,6 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
              "vconv: residual GroupNorm (1x1, resid, partials, gamma / beta, mask, T >= %d)", vconv_gnres_min_frames());
   VConvArgs a = a0;
   a.xcd_tiles = xcd_tiles_knob();
-  a.loaders = loaders_knob();
   if (a.c0 == 0) a.c0 = a.cin;  // one source
   MT_REQUIRE(a.c0 == a.cin || (a.x1 && a.c0 % 64 == 0 && a.c0 > 0 && a.c0 < a.cin), "vconv: channel split %d/%d",
              a.c0, a.cin);
