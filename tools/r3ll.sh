@@ -1,4 +1,4 @@
-# build A/B: the r03d library (before the prefetch / prologue-split code, fewer SGPR spills) vs the current one
+# build A/B: libmatcha_hip_old.so (whichever older build was copied there) vs the current library
 set -o pipefail
 mkdir -p gpurun_out/r3ll
 OLD=$PWD/matcha-tts_amd/libmatcha_hip_old.so
