@@ -41,7 +41,7 @@ import torch  # noqa: E402
 SR, HOP = 22050, 256
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
@@ -59,7 +59,50 @@ def parse():
     p.add_argument("--model", default="lj", choices=["lj", "vctk"],
                    help="lj: single speaker (configs[1..2]); vctk: 109 speakers with the speaker-embedding "
                         "condition (configs[3]: B=128 over 8 GPUs = 16/GPU, 20 ODE steps)")
-    return p.parse_args()
+    # CPU rehearsal of the multi-rank launch (tests/test_bench_dist.py): gloo ranks, shards and the MAX / SUM
+    # reduction with a host-side stand-in for the step; no GPU is touched
+    p.add_argument("--cpu-selftest", action="store_true", help=argparse.SUPPRESS)
+    return p.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """``--gpus N`` with no WORLD_SIZE in the environment: start N rank processes of this script, one per GPU, the
+    way ``torch.distributed.run --nnodes 1 --nproc-per-node N --master-addr 127.0.0.1`` does (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR / MASTER_PORT in each child's environment), and return the job's exit code (the first
+    failing rank's; the other ranks are then stopped). The reference takes its device count from the CLI the same
+    way (``devices=args.gpus``, train_standalone.py:763, 866-867). This parent never touches the GPU: it starts the
+    children as fresh processes and only waits for them."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this driver
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # one rank failed: the job has failed, stop the ranks we started
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def build_models(device, precision, seed, n_spks=1):
@@ -399,11 +442,43 @@ def fp32_record(device, seed, batch, n_ts, denoise, steps=3):
             "ceiling_note": "fp32 MFMA 157.3 TF / 735 MFLOP per frame -> 214k frames/s (SURVEY.md §8d)"}
 
 
-def main():
-    a = parse()
+def cpu_selftest(a, world, rank):
+    """--cpu-selftest: one rank of the launch contract on the CPU (gloo): the shard, a barrier-bracketed timed
+    region around a host stand-in for the step, the MAX / SUM reduction and rank 0's JSON line"""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    x, xl = shard_inputs(rank, world, a.batch, a.seed)
+    frames = int(xl.sum()) * 3  # the forced duration head: 3 frames per token
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        torch.mm(torch.ones(64, 64), torch.ones(64, 64))
+    if world > 1:
+        dist.barrier()
+    el, tot = reduce_over_ranks(time.perf_counter() - t0, frames, dist if world > 1 else None, torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"metric": "cpu-selftest", "value": tot * a.steps / el, "n_gpus": world, "steps": a.steps,
+                          "warmup": a.warmup, "frames_per_step": tot, "scaling": "weak"}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus, argv))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
+    if a.cpu_selftest:
+        return cpu_selftest(a, world, rank)
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -76,9 +76,12 @@ int mt_encoder_set_mfma_attention(mt_encoder* e, int enable);
 /* fp32: 1 (default) runs the prenet / attention-projection / FFN / duration-predictor convs on mt_vconv's fp32 mode
  * (LDS-DMA staging, exact-fp32 MFMA); 0 = the generic implicit-GEMM kernel (A/B, tests). Same arithmetic. */
 int mt_encoder_set_vconv(mt_encoder* e, int enable);
+/* oov (nullable, device int32): set to 0, then to 1 when any id of x (padding included) lies outside [0, n_vocab):
+ * nn.Embedding's IndexError (model.py:522); the caller raises at its next host sync. The embedding reads a clamped
+ * row for such an id, so the launch itself stays in bounds. */
 int mt_encoder_forward(const mt_encoder* e, const void* packed, const int64_t* x, const int64_t* x_lengths,
-                       const float* spks, int B, int Tx, float* mu, float* logw, float* x_mask, void* ws,
-                       size_t ws_bytes, void* stream);
+                       const float* spks, int B, int Tx, float* mu, float* logw, float* x_mask, int32_t* oov,
+                       void* ws, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * U-Net estimator + CFM solver. Hyper-parameters are those of main.py:67-76
@@ -322,6 +325,10 @@ int mtt_adam(float* p, const float* g, float* m, float* v, size_t n, const float
 /* clip factor for a flat gradient holding the SUM over `world` ranks: norm = sqrt(*sumsq) * inv_world (the norm of
  * the DDP-averaged gradient), out = min(1, max_norm / (norm + 1e-6)) * inv_world (torch.nn.utils.clip_grad_norm_) */
 int mtt_clip_factor(const float* sumsq, float max_norm, float inv_world, float* out, float* norm_out, void* stream);
+/* torch.cuda.amp.GradScaler.unscale_ ("16-mixed", train_standalone.py:868): g *= inv_scale in place, and
+ * *found = the number of non-finite elements of the unscaled gradient (the per-element found-inf check of
+ * torch._amp_foreach_non_finite_check_and_unscale_); scratch >= 1024 floats */
+int mtt_unscale(float* g, size_t n, float inv_scale, float* found, float* scratch, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Op-level entry points (per-kernel parity tests)

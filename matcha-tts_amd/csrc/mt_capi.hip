@@ -92,10 +92,10 @@ int mt_encoder_set_vconv(mt_encoder* e, int enable) {
   return 0;
 }
 int mt_encoder_forward(const mt_encoder* e, const void* packed, const int64_t* x, const int64_t* x_lengths,
-                       const float* spks, int B, int Tx, float* mu, float* logw, float* x_mask, void* ws,
-                       size_t ws_bytes, void* stream) {
+                       const float* spks, int B, int Tx, float* mu, float* logw, float* x_mask, int32_t* oov,
+                       void* ws, size_t ws_bytes, void* stream) {
   MT_REQUIRE(e && packed, "encoder_forward: null argument");
-  return e->e.forward(packed, (const long long*)x, (const long long*)x_lengths, spks, B, Tx, mu, logw, x_mask, ws,
+  return e->e.forward(packed, (const long long*)x, (const long long*)x_lengths, spks, B, Tx, mu, logw, x_mask, oov, ws,
                       ws_bytes, (hipStream_t)stream);
 }
 
@@ -508,6 +508,9 @@ int mtt_adam(float* p, const float* g, float* m, float* v, size_t n, const float
 }
 int mtt_clip_factor(const float* sumsq, float max_norm, float inv_world, float* out, float* norm_out, void* stream) {
   return mt::clip_factor(sumsq, max_norm, inv_world, out, norm_out, (hipStream_t)stream);
+}
+int mtt_unscale(float* g, size_t n, float inv_scale, float* found, float* scratch, void* stream) {
+  return mt::unscale_found_inf(g, n, inv_scale, found, scratch, (hipStream_t)stream);
 }
 
 int mt_vconv_log_start(int capacity) { return mt::vclog_start(capacity); }

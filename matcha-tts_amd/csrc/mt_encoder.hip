@@ -23,11 +23,16 @@ namespace mt {
 template <class E>
 __global__ void embed_kernel(const long long* __restrict__ ids, const long long* __restrict__ xlen, int Tx,
                              const float* __restrict__ emb, int nvocab, int C, float scale, E* __restrict__ out,
-                             float* __restrict__ xmask) {
+                             float* __restrict__ xmask, int* __restrict__ oov) {
   const int row = blockIdx.x;  // b * Tx + t
   const int b = row / Tx, t = row - b * Tx;
   long long id = ids[row];
-  id = id < 0 ? 0 : (id >= nvocab ? nvocab - 1 : id);
+  // nn.Embedding rejects an id outside [0, n_vocab) anywhere in x, padding included (model.py:522): flag it for the
+  // host (the caller raises IndexError at its next sync), and read a valid row so no access leaves the table
+  if (id < 0 || id >= nvocab) {
+    if (oov && threadIdx.x == 0) oov[0] = 1;
+    id = id < 0 ? 0 : nvocab - 1;
+  }
   const float* e = emb + (size_t)id * C;
   // stored masked: every consumer reads x * x_mask (the prenet's first conv, model.py:203; its residual x_org is
   // masked again by the prenet's final `* x_mask`, model.py:208), so no conv needs a mask prologue
@@ -667,7 +672,7 @@ constexpr int kNotVc = 0x7fff0001;  // v32(): the layer is not on mt_vconv's fp3
 
 template <class E>
 int Encoder::forward_t(const char* P, const long long* ids, const long long* xlen, const float* spks, int B, int Tx,
-                       float* mu, float* logw, float* xmask, char* ws, hipStream_t st) const {
+                       float* mu, float* logw, float* xmask, int* oov, char* ws, hipStream_t st) const {
   int rc;
   const size_t n = (size_t)B * Tx;
   const int wmax = std::max(std::max(W, 3 * W), std::max(F, DF));
@@ -704,9 +709,10 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
     a.probe = -1;
     return launch_vconv(ef, a, st);
   };
-  // embedding * sqrt(C) and x_mask
+  // embedding * sqrt(C) and x_mask (+ the out-of-vocabulary flag)
+  if (oov) MT_CHECK_HIP(hipMemsetAsync(oov, 0, sizeof(int), st));
   hipLaunchKernelGGL((embed_kernel<E>), dim3((unsigned)n), dim3(256), 0, st, ids, xlen, Tx, (const float*)(P + emb_off),
-                     n_vocab, C, sqrtf((float)C), (E*)Q, xmask);
+                     n_vocab, C, sqrtf((float)C), (E*)Q, xmask, oov);
   MT_CHECK_HIP(hipGetLastError());
   // prenet (ConvReluNorm, model.py:196-208): h = relu(LN(conv(h*m))) x3, x = (x + proj(h)) * m
   const char* cur = Q;
@@ -888,13 +894,13 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
 }
 
 int Encoder::forward(const void* packed, const long long* ids, const long long* xlen, const float* spks, int B, int Tx,
-                     float* mu, float* logw, float* xmask, void* ws, size_t ws_bytes, hipStream_t st) const {
+                     float* mu, float* logw, float* xmask, int* oov, void* ws, size_t ws_bytes, hipStream_t st) const {
   MT_REQUIRE(B > 0 && Tx > 0 && ids && xlen && mu && logw && xmask, "encoder: empty input");
   MT_REQUIRE(W == C || spks, "encoder: multi-speaker model needs spks [B][%d]", spk_dim);
   MT_REQUIRE(ws_bytes >= workspace_bytes(B, Tx), "encoder: workspace %zu < %zu", ws_bytes, workspace_bytes(B, Tx));
   if (dtype == BF16)
-    return forward_t<bf16>((const char*)packed, ids, xlen, spks, B, Tx, mu, logw, xmask, (char*)ws, st);
-  return forward_t<float>((const char*)packed, ids, xlen, spks, B, Tx, mu, logw, xmask, (char*)ws, st);
+    return forward_t<bf16>((const char*)packed, ids, xlen, spks, B, Tx, mu, logw, xmask, oov, (char*)ws, st);
+  return forward_t<float>((const char*)packed, ids, xlen, spks, B, Tx, mu, logw, xmask, oov, (char*)ws, st);
 }
 
 }  // namespace mt

@@ -402,53 +402,57 @@ int rowdot(const float* x, int ldx, const float* W, const float* bias, float* y,
 __global__ __launch_bounds__(256) void durations_kernel(const float* __restrict__ logw, const float* __restrict__ xmask,
                                                         float ls, int Tx, float* __restrict__ w_ceil,
                                                         float* __restrict__ cum, long long* __restrict__ ylen) {
-  // thread t owns the DUR_PER consecutive tokens [t * per, (t + 1) * per): ceil(exp(logw) * mask * ls), then an
-  // inclusive block scan of the per-thread sums (wave shuffles + one LDS pass). Every value is an integer-valued
-  // fp32 below 2^24, so this order gives the serial cumsum's bits exactly.
-  constexpr int DUR_PER = 32;  // Tx <= 8192
+  // chunks of 256 * DUR_PER tokens; in a chunk thread t owns the `per` consecutive tokens [t * per, (t + 1) * per):
+  // ceil(exp(logw) * mask * ls), then an inclusive block scan of the per-thread sums (wave shuffles + one LDS pass)
+  // on top of the previous chunks' total. Every value is an integer-valued fp32 below 2^24, so this order gives the
+  // serial cumsum's bits exactly.
+  constexpr int DUR_PER = 32;
   __shared__ float wsum[4];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int per = (Tx + 255) / 256, x0 = tid * per;
-  float w[DUR_PER];
-  float s = 0.f;
+  float base = 0.f;
+  for (int c0 = 0; c0 < Tx; c0 += 256 * DUR_PER) {
+    const int n = min(Tx - c0, 256 * DUR_PER);
+    const int per = (n + 255) / 256, x0 = c0 + tid * per;
+    float w[DUR_PER];
+    float s = 0.f;
 #pragma unroll
-  for (int k = 0; k < DUR_PER; ++k) {
-    const int x = x0 + k;
-    w[k] = 0.f;
-    if (k < per && x < Tx) {
-      const size_t i = (size_t)b * Tx + x;
-      w[k] = ceilf((expf(logw[i]) * xmask[i]) * ls);
-      w_ceil[i] = w[k];
-      s += w[k];
+    for (int k = 0; k < DUR_PER; ++k) {
+      const int x = x0 + k;
+      w[k] = 0.f;
+      if (k < per && x < c0 + n) {
+        const size_t i = (size_t)b * Tx + x;
+        w[k] = ceilf((expf(logw[i]) * xmask[i]) * ls);
+        w_ceil[i] = w[k];
+        s += w[k];
+      }
     }
-  }
-  float inc = s;
+    float inc = s;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float v = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += v;
-  }
-  if (lane == 63) wsum[wv] = inc;
-  __syncthreads();
-  float run = inc - s;
-  for (int u = 0; u < wv; ++u) run += wsum[u];
-#pragma unroll
-  for (int k = 0; k < DUR_PER; ++k) {
-    const int x = x0 + k;
-    if (k < per && x < Tx) {
-      run += w[k];
-      cum[(size_t)b * Tx + x] = run;
+    for (int o = 1; o < 64; o <<= 1) {
+      const float v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
     }
+    __syncthreads();  // the previous chunk's wsum reads are done
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    float run = base + (inc - s);
+    for (int u = 0; u < wv; ++u) run += wsum[u];
+#pragma unroll
+    for (int k = 0; k < DUR_PER; ++k) {
+      const int x = x0 + k;
+      if (k < per && x < c0 + n) {
+        run += w[k];
+        cum[(size_t)b * Tx + x] = run;
+      }
+    }
+    base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
   }
-  if (tid == 255) {
-    const float c = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    ylen[b] = (long long)(c < 1.f ? 1.f : c);
-  }
+  if (tid == 255) ylen[b] = (long long)(base < 1.f ? 1.f : base);
 }
 
 int durations(const float* logw, const float* xmask, float ls, int B, int Tx, float* w_ceil, float* cum,
               long long* ylen, hipStream_t st) {
-  MT_REQUIRE(B > 0 && Tx > 0 && Tx <= 8192, "durations: B %d, Tx %d (<= 8192)", B, Tx);
+  MT_REQUIRE(B > 0 && Tx > 0, "durations: B %d, Tx %d", B, Tx);
   hipLaunchKernelGGL(durations_kernel, dim3(B), dim3(256), 0, st, logw, xmask, ls, Tx, w_ceil, cum, ylen);
   MT_CHECK_HIP(hipGetLastError());
   return 0;

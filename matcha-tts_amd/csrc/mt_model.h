@@ -203,10 +203,10 @@ struct Encoder {
   int pack(const float* const* p, void* packed, hipStream_t st) const;
   size_t workspace_bytes(int B, int Tx) const;
   int forward(const void* packed, const long long* ids, const long long* xlen, const float* spks, int B, int Tx,
-              float* mu, float* logw, float* xmask, void* ws, size_t ws_bytes, hipStream_t st) const;
+              float* mu, float* logw, float* xmask, int* oov, void* ws, size_t ws_bytes, hipStream_t st) const;
   template <class E>
   int forward_t(const char* P, const long long* ids, const long long* xlen, const float* spks, int B, int Tx,
-                float* mu, float* logw, float* xmask, char* ws, hipStream_t st) const;
+                float* mu, float* logw, float* xmask, int* oov, char* ws, hipStream_t st) const;
 };
 
 // -------------------------------------------------------------------------------------

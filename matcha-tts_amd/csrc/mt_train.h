@@ -94,5 +94,6 @@ int embed_bwd(const long long* ids, size_t ntok, const float* dout, int V, int C
 int adam_step(float* p, const float* g, float* m, float* v, size_t n, const float* gscale, float lr, float b1,
               float b2, float eps, int step, hipStream_t st);
 int clip_factor(const float* sumsq, float max_norm, float inv_world, float* out, float* norm_out, hipStream_t st);
+int unscale_found_inf(float* g, size_t n, float inv_scale, float* found, float* scratch, hipStream_t st);
 
 }  // namespace mt

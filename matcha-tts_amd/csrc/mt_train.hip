@@ -564,6 +564,36 @@ int sum_all(const float* a, const float* b, size_t n, float* out, float* scratch
   return 0;
 }
 
+// GradScaler.unscale_ (torch._amp_foreach_non_finite_check_and_unscale_): g *= inv_scale in place with a
+// per-element found-inf check on the unscaled value; partial[block] = the block's count of non-finite elements
+__global__ __launch_bounds__(256) void unscale_kernel(float* __restrict__ g, size_t n, float inv_scale,
+                                                      float* __restrict__ partial) {
+  __shared__ float red[256];
+  float bad = 0.f;
+  for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const float v = g[i] * inv_scale;
+    g[i] = v;
+    bad += isfinite(v) ? 0.f : 1.f;
+  }
+  red[threadIdx.x] = bad;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+int unscale_found_inf(float* g, size_t n, float inv_scale, float* found, float* scratch, hipStream_t st) {
+  MT_REQUIRE(g && found && scratch && n > 0, "unscale: args");
+  const int nb = (int)std::min<size_t>(1024, (n + 255) / 256);
+  hipLaunchKernelGGL(unscale_kernel, dim3(nb), dim3(256), 0, st, g, n, inv_scale, scratch);
+  hipLaunchKernelGGL(sum_kernel, dim3(1), dim3(256), 0, st, (const float*)scratch, (const float*)nullptr, (size_t)nb,
+                     found);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 // ---------------------------------------------------------------------------------------------- dropout
 // out = a * keep / (1 - p), keep = hash(seed, i) >= p (counter-based, so a step's masks are a function of its
 // seed: reproducible, and the backward re-derives the same mask instead of storing it)

@@ -11,7 +11,9 @@
 //
 // One persistent 512-thread workgroup per CU walks the tiles. Waves: 2 along rows (64 output channels each)
 // x 4 along frames (48 frames = 3 fragments each). Per tile:
-//   1. the RAW input rows (192 conv1 frames + the conv1 halo 2 h1 <= 56 rows) of both 64-channel planes land
+//   1. the RAW input rows (192 conv1 frames + the conv1 halo 2 h1 <= 40 rows: k <= 7 at d = 5, k = 11 at d <= 3;
+//      a k = 11, d = 5 pair is not supported here and runs per layer on mt_vconv — the default vocoder fuses only
+//      the k = 3 resblock on this kernel) of both 64-channel planes land
 //      in LDS by global_load_lds_dwordx4 (issued during the previous tile's second conv); each lane reads its
 //      residual rows out of them, then one in-place VALU pass turns them into lrelu(rows);
 //   2. conv1: 128 rows x 192 frames over (chunk, tap) steps; epilogue lrelu(round(acc + b1)), zero outside
@@ -23,7 +25,7 @@
 // K = 32 slices each: the per-output MFMA accumulation order of mt_vconv's K loop, and its rounding points
 // (every stored tensor rounded to bf16 once, activated outputs lrelu'd in fp32 first), so the results are the
 // same bits as the per-layer mt_vconv path.
-// LDS (162,816 B): T planes (2 x 192 rows) | X planes (2 x 248 rows) | weight ring | biases. Rows are 128 B
+// LDS: T planes (2 x 192 rows) | X planes (2 x XROWS = 232 rows) | weight ring | biases | the ragged tile map. Rows are 128 B
 // with the 16-byte unit XOR-swizzled by (row & 6) (mt_vconv's conflict-free layout). conv2's discarded last
 // fragments read up to 2 h2 rows past a T plane: into the next plane / the X planes, never outside LDS.
 #include <algorithm>

@@ -35,7 +35,7 @@ SIGNATURES = {
     "mt_encoder_workspace_bytes": (c_size_t, [P, c_int, c_int]),
     "mt_encoder_set_mfma_attention": (c_int, [P, c_int]),
     "mt_encoder_set_vconv": (c_int, [P, c_int]),
-    "mt_encoder_forward": (c_int, [P, P, P, P, P, c_int, c_int, P, P, P, P, c_size_t, P]),
+    "mt_encoder_forward": (c_int, [P, P, P, P, P, c_int, c_int, P, P, P, P, P, c_size_t, P]),
     "mt_decoder_create": (c_int, [c_int, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
     "mt_decoder_destroy": (None, [P]),
     "mt_decoder_num_params": (c_int, [P]),
@@ -121,6 +121,7 @@ SIGNATURES = {
     "mtt_embed_bwd": (c_int, [P, c_size_t, P, c_int, c_int, c_float, P, P]),
     "mtt_adam": (c_int, [P, P, P, P, c_size_t, P, c_float, c_float, c_float, c_float, c_int, P]),
     "mtt_clip_factor": (c_int, [P, c_float, c_float, P, P, P]),
+    "mtt_unscale": (c_int, [P, c_size_t, c_float, P, P, P]),
     "mt_vconv_log_start": (c_int, [c_int]),
     "mt_vconv_log_stop": (c_int, [P, c_int]),
 }

@@ -197,7 +197,8 @@ class EncoderEngine:
         return packed
 
     def forward(self, packed, x: torch.Tensor, x_lengths: torch.Tensor, spks: Optional[torch.Tensor] = None):
-        """x int64 [B,Tx], x_lengths int64 [B] -> mu [B,80,Tx], logw [B,1,Tx], x_mask [B,1,Tx] (fp32)."""
+        """x int64 [B,Tx], x_lengths int64 [B] -> mu [B,80,Tx], logw [B,1,Tx], x_mask [B,1,Tx] (fp32), oov int32 [1]
+        (1 when an id of x lies outside [0, n_vocab): see ``check_ids``)."""
         x = x.to(torch.int64).contiguous()
         xl = x_lengths.to(torch.int64).contiguous()
         B, Tx = x.shape
@@ -206,10 +207,20 @@ class EncoderEngine:
         logw = torch.empty(B, 1, Tx, dtype=torch.float32, device=dev)
         x_mask = torch.empty(B, 1, Tx, dtype=torch.float32, device=dev)
         L = lib()
+        oov = torch.empty(1, dtype=torch.int32, device=dev)
         ws = _Workspace.get(L.mt_encoder_workspace_bytes(self.h, B, Tx), dev)
         check(L.mt_encoder_forward(self.h, packed.data_ptr(), ptr(x), ptr(xl), ptr(spks), B, Tx, ptr(mu), ptr(logw),
-                                   ptr(x_mask), ws.data_ptr(), ws.numel(), stream_handle(dev)), "encoder_forward")
-        return mu, logw, x_mask
+                                   ptr(x_mask), ptr(oov), ws.data_ptr(), ws.numel(), stream_handle(dev)),
+              "encoder_forward")
+        return mu, logw, x_mask, oov
+
+
+def check_ids(oov: torch.Tensor) -> None:
+    """nn.Embedding's error for an out-of-vocabulary token id (model.py:471, 522: ``self.emb(x)`` raises
+    IndexError on the CPU; on a GPU torch reports it at the next sync). Reads the encoder's device flag, i.e. one
+    host sync: ``MatchaTTS.synthesize`` calls it right after the reference's own sync on max(y_lengths)."""
+    if int(oov.item()) != 0:
+        raise IndexError("index out of range in self (a token id of x lies outside [0, n_vocab))")
 
 
 class DecoderEngine:

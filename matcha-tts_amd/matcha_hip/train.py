@@ -1016,15 +1016,20 @@ class MatchaTrainer:
 
     def optimizer_step(self):
         """gradient_clip_val 5.0 (norm of the world-averaged gradient) then torch.optim.Adam (lr, defaults).
-        "16-mixed": the gradient holds loss-scale x the true one; the unscale is folded into the clip factor, and an
-        inf / NaN anywhere (the all-reduced buffer is the same on every rank) skips the update and halves the scale
-        (GradScaler.unscale_ / step / update; its found-inf check syncs with the host, as here)."""
+        "16-mixed" runs Lightning's MixedPrecision sequence: GradScaler.unscale_ (the summed, loss-scaled buffer times
+        1 / (world * scale) in place, with torch's per-element found-inf check on the unscaled values), the clip on
+        the unscaled gradient, then GradScaler.step / update: a non-finite element skips the update and halves the
+        scale, ``growth_interval`` finite steps in a row double it. The found-inf flag is read on the host, as
+        GradScaler.step does (``found_inf.item()``); the all-reduced buffer is the same on every rank."""
         g = self.grads.flat
-        scale, sumsq = empty(2, like=g), total(g, g)
-        S = self.scaler["scale"] if self.scaler else 1.0
+        scale = empty(2, like=g)
         if self.scaler is not None:
             sc = self.scaler
-            if not math.isfinite(sumsq.item()):
+            found = empty(1, like=g)
+            check(lib().mtt_unscale(g.data_ptr(), g.numel(), 1.0 / (self.world * sc["scale"]), found.data_ptr(),
+                                    _Scratch.get(1024, g).data_ptr(), _s(g)), "unscale")
+            sumsq = total(g, g)
+            if found.item() != 0.0:
                 sc["scale"] *= sc["backoff_factor"]
                 sc["_growth_tracker"] = 0
                 self.last["grad_norm"] = sumsq.sqrt()
@@ -1034,9 +1039,13 @@ class MatchaTrainer:
             if sc["_growth_tracker"] == sc["growth_interval"]:
                 sc["scale"] *= sc["growth_factor"]
                 sc["_growth_tracker"] = 0
+            inv = 1.0  # already unscaled and averaged
+        else:
+            sumsq = total(g, g)
+            inv = 1.0 / self.world  # the buffer holds the sum over ranks; the average folds into the clip factor
         self.step_count += 1
-        check(lib().mtt_clip_factor(sumsq.data_ptr(), float(self.clip), 1.0 / (self.world * S), scale.data_ptr(),
-                                    scale[1:].data_ptr(), _s(g)), "clip_factor")
+        check(lib().mtt_clip_factor(sumsq.data_ptr(), float(self.clip), inv, scale.data_ptr(), scale[1:].data_ptr(),
+                                    _s(g)), "clip_factor")
         check(lib().mtt_adam(self.params.flat.data_ptr(), g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), g.numel(),
                              scale.data_ptr(), float(self.lr), 0.9, 0.999, 1e-8, self.step_count, _s(g)), "adam")
         self.last["grad_norm"] = scale[1:]

@@ -223,7 +223,14 @@ class TextEncoder(nn.Module):
         return self._engines[self.precision]
 
     def forward(self, x, x_lengths, spks=None):
-        """model.py:503-535 on the GPU -> (mu [B,80,Tx], logw [B,1,Tx], x_mask [B,1,Tx]) fp32."""
+        """model.py:503-535 on the GPU -> (mu [B,80,Tx], logw [B,1,Tx], x_mask [B,1,Tx]) fp32. An id outside
+        [0, n_vocab) raises IndexError, as ``self.emb(x)`` does (model.py:522)."""
+        mu, logw, x_mask, oov = self.forward_unchecked(x, x_lengths, spks)
+        rt.check_ids(oov)
+        return mu, logw, x_mask
+
+    def forward_unchecked(self, x, x_lengths, spks=None):
+        """forward without the host sync of the id check: also returns the device flag for ``rt.check_ids``"""
         rt.require_gpu(x, x_lengths, spks, what="TextEncoder.forward")
         if self.n_spks > 1 and spks is None:
             raise ValueError("multi-speaker TextEncoder needs spks [B, spk_emb_dim]")
@@ -510,7 +517,7 @@ class MatchaTTS(nn.Module):
     def synthesize(self, x, x_lengths, n_timesteps, temperature=1.0, spks=None, length_scale=1.0):
         """model.py:1264-1300 -> (mel [B,80,y_max], y_lengths int64 [B], attn [B,1,Tx,T_pad])."""
         rt.require_gpu(x, x_lengths, spks, what="MatchaTTS.synthesize")
-        mu, logw, x_mask = self.encoder(x, x_lengths, spks)
+        mu, logw, x_mask, oov = self.encoder.forward_unchecked(x, x_lengths, spks)
         w_ceil, cum, y_lengths = rt.durations(logw, x_mask, length_scale)
         # validate the estimator's packed weights now, while the GPU runs the encoder, instead of after the
         # host sync below (nothing between here and the solve can change them)
@@ -519,6 +526,7 @@ class MatchaTTS(nn.Module):
         est._pk.trust_next((est.precision, str(x.device)))
         try:
             y_max = int(y_lengths.max())                 # the reference's host sync (model.py:1278-1281)
+            rt.check_ids(oov)                            # nn.Embedding's IndexError (model.py:522), after it
             t_pad = fix_len_compatibility(y_max)
             attn, mu_y, y_mask = rt.alignment(cum, y_lengths, t_pad, mu)
             z = self.decoder(mu_y, y_mask, n_timesteps, temperature, spks, cond=None, max_valid=y_max)

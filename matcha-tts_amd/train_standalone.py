@@ -105,6 +105,8 @@ class _FusedAdam:
         # the engine's dropout-stream position rides in the param group (torch's Adam keeps only hyper-parameters
         # there; an extra key is carried through load_state_dict unchanged)
         groups = [dict(self.param_groups[0], params=list(range(len(self._index()))), dropout_calls=int(st["calls"]))]
+        if st.get("scaler") is not None:  # "16-mixed": GradScaler.state_dict() (Lightning checkpoints it too)
+            groups[0]["loss_scaler"] = dict(st["scaler"])
         return {"state": state, "param_groups": groups}
 
     def load_state_dict(self, sd):
@@ -131,7 +133,8 @@ class _FusedAdam:
             step = int(float(st["step"]))
         tr.load_optimizer_state({"exp_avg": m, "exp_avg_sq": v, "step": step,
                                  "lr": self.param_groups[0]["lr"],
-                                 "calls": sd["param_groups"][0].get("dropout_calls")})
+                                 "calls": sd["param_groups"][0].get("dropout_calls"),
+                                 "scaler": sd["param_groups"][0].get("loss_scaler")})
 
 
 class MatchaLightningModule(torch.nn.Module):
@@ -174,7 +177,10 @@ class MatchaLightningModule(torch.nn.Module):
         return dist.get_world_size(self.process_group) if dist.is_available() and dist.is_initialized() else 1
 
     def _model_fp(self):
-        return [(t.data_ptr(), t._version) for t in self.model.state_dict(keep_vars=True).values()]
+        """(address, version) of the tensors the engine holds (the buffers mel_mean / mel_std are not among them:
+        _broadcast_buffers rewrites those every DDP step and must not trigger a parameter reload)"""
+        return [(t.data_ptr(), t._version) for k, t in self.model.state_dict(keep_vars=True).items()
+                if k.startswith(("encoder.", "decoder.estimator."))]
 
     def trainer(self) -> MatchaTrainer:
         """the GPU training engine, built from the model's current weights on first use; a later change of the

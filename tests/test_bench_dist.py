@@ -54,3 +54,35 @@ def test_bench_sharding_and_reduction_gloo_world2():
         assert np.array_equal(x, gx[rank * 4:(rank + 1) * 4, : x.shape[1]])
     # shards are disjoint slices: together they are the global set
     assert np.array_equal(np.concatenate([r[2] for r in res]), gl)
+
+
+def _run_bench(args, env_extra=None, timeout=180):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_bench_gpus_flag_launches_its_own_ranks():
+    """``python bench.py --gpus 2`` with no launcher in the environment starts 2 rank processes itself (RANK /
+    WORLD_SIZE / MASTER_* set per child, torch.distributed.run style), and rank 0 prints ONE line with n_gpus 2 and
+    the SUM of both shards' frames (CPU rehearsal: gloo ranks, host stand-in for the step)."""
+    import json
+
+    from matcha_hip import synthetic
+    r = _run_bench(["--gpus", "2", "--steps", "3", "--warmup", "0", "--batch", "4", "--cpu-selftest"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    _, gl = synthetic.synthetic_text(8, seed=1234)
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["frames_per_step"] == int(gl.sum()) * 3
+
+
+def test_bench_rejects_world_mismatch():
+    """--gpus must match the world a launcher started: WORLD_SIZE=1 with --gpus 2 exits non-zero instead of
+    measuring one GPU and labelling it two"""
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--cpu-selftest"], {"WORLD_SIZE": "1", "RANK": "0",
+                                                                         "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr

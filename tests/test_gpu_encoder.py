@@ -142,3 +142,27 @@ def test_text_encoder_fp32_vconv_matches_generic_kernel(name, n_spks, lengths):
     e_mu, e_logw = (mu1 - mu0).abs().max().item(), (logw1 - logw0).abs().max().item()
     print(f"{name}: fp32 vconv vs generic: mu max|d| {e_mu:.2e}, logw max|d| {e_logw:.2e}")
     assert e_mu < 2e-5 and e_logw < 2e-5, (e_mu, e_logw)
+
+
+@pytest.mark.parametrize("bad,where", [(178, "live"), (-1, "live"), (500, "padding")])
+def test_out_of_vocabulary_id_raises(bad, where):
+    """nn.Embedding's error semantics (model.py:471, 522: ``self.emb(x)`` raises IndexError for an id outside
+    [0, n_vocab), including one in the padded tail of x): TextEncoder.forward and MatchaTTS.synthesize raise
+    IndexError instead of synthesizing from a clamped row; the largest valid id (n_vocab - 1) runs, and the same
+    model still synthesizes afterwards."""
+    m, _ = _model(1, "fp32", 13)
+    x, xl = _inputs([20, 11], 3)
+    x[0, 5] = 177  # n_vocab - 1 is valid
+    mu, _, _ = m.encoder(x.to(DEV), xl.to(DEV))
+    assert torch.isfinite(mu).all()
+    xb = x.clone()
+    if where == "live":
+        xb[1, 4] = bad
+    else:
+        xb[1, 15] = bad  # past x_lengths[1] = 11
+    with pytest.raises(IndexError):
+        m.encoder(xb.to(DEV), xl.to(DEV))
+    with pytest.raises(IndexError):
+        m.synthesize(xb.to(DEV), xl.to(DEV), n_timesteps=2, temperature=0.667)
+    mel, yl, _ = m.synthesize(x.to(DEV), xl.to(DEV), n_timesteps=2, temperature=0.667)
+    assert torch.isfinite(mel).all() and int(yl.min()) >= 1

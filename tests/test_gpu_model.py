@@ -39,10 +39,11 @@ def test_durations_alignment_bit_exact():
         assert torch.equal(y_mask.cpu()[:, 0], ref_mask)
 
 
-@pytest.mark.parametrize("B,Tx", [(3, 251), (2, 1000), (1, 8192)])
+@pytest.mark.parametrize("B,Tx", [(3, 251), (2, 1000), (1, 8192), (2, 20001)])
 def test_durations_scan_and_alignment_long_text(B, Tx):
     """The block-parallel ceil / cumsum (every partial sum an integer below 2^24, so exact in any order) and the
-    alignment with its writes split over the token rows: equal to torch's serial cumsum and to the oracle's
+    alignment with its writes split over the token rows (Tx past 8192: the scan runs in 8192-token chunks carrying
+    the running sum): equal to torch's serial cumsum and to the oracle's
     generate_path / mu_y gather (model.py:1273-1289), ragged masks included."""
     from matcha_hip import runtime as rt
     from oracle import matcha_oracle as O

@@ -450,38 +450,45 @@ def test_lightning_module_drop_in():
     assert mod(batch["x"], batch["x_lengths"], batch["y"], batch["y_lengths"])[3].shape == (3, x.shape[1], y.shape[2])
 
 
-def _lightning(sd):
+def _lightning(sd, precision="32"):
     from types import SimpleNamespace
 
     import train_standalone as TS
     from conftest import DEC, DP, ENC
     mod = TS.MatchaLightningModule(178, 1, 64, SimpleNamespace(**ENC), SimpleNamespace(**DEC),
                                    {"solver": "euler", "sigma_min": 1e-4}, SimpleNamespace(**DP),
-                                   {"mel_mean": 0.0, "mel_std": 1.0})
+                                   {"mel_mean": 0.0, "mel_std": 1.0}, precision=precision)
     mod.model.load_state_dict(sd)
     return mod.to(DEV)
 
 
-def test_lightning_module_resume_and_reload():
+@pytest.mark.parametrize("precision", ["32", "16-mixed"])
+def test_lightning_module_resume_and_reload(precision):
     """Checkpoint / resume (train_standalone.py:850-857, 882): module.state_dict() + optimizer.state_dict() saved after
     a step and loaded into a FRESH module and optimizer continue bit-identically (the Adam moments, the step count
     and thus the dropout stream come back); a state dict loaded into a live module's .model is what its next step
     trains (the engine's flat parameters are refreshed from it)."""
     sd, x, xl, y, yl, _, _ = _setup(seed=25)
     batch = {"x": x.to(DEV), "x_lengths": xl.to(DEV), "y": y.to(DEV), "y_lengths": yl.to(DEV)}
-    a = _lightning(sd)
+    a = _lightning(sd, precision)
     opt_a = a.configure_optimizers()
+    if precision == "16-mixed":
+        # a scale the first steps keep (a skipped step would leave no Adam state to carry), growth after 2 steps
+        a.trainer().scaler.update(scale=1024.0, growth_interval=2)
     torch.manual_seed(1)
     a.training_step(batch, 0)
     opt_a.step()
     msd = {k: v.detach().clone() for k, v in a.state_dict().items()}
     osd = opt_a.state_dict()
     assert len(osd["state"]) == len(list(a.parameters())) and float(osd["state"][0]["step"]) == 1.0
+    if precision == "16-mixed":  # GradScaler's state rides in the optimizer state (ADVICE r3: it was dropped)
+        assert osd["param_groups"][0]["loss_scaler"] == {"scale": 1024.0, "growth_factor": 2.0, "backoff_factor": 0.5,
+                                                         "growth_interval": 2, "_growth_tracker": 1}
     torch.manual_seed(2)
     la = a.training_step(batch, 1).item()
     opt_a.step()
     wa = {k: v.detach().clone() for k, v in a.model.state_dict().items()}
-    b = _lightning(sd)
+    b = _lightning(sd, precision)
     b.load_state_dict(msd)
     opt_b = b.configure_optimizers()
     opt_b.load_state_dict(osd)
@@ -489,9 +496,124 @@ def test_lightning_module_resume_and_reload():
     lb = b.training_step(batch, 1).item()
     opt_b.step()
     assert la == lb
+    if precision == "16-mixed":  # both grew the scale at the second finite step
+        assert a.trainer().scaler == b.trainer().scaler and b.trainer().scaler["scale"] == 2048.0
     for k, v in b.model.state_dict().items():
         assert torch.equal(v, wa[k]), k
     # reload into a live module: the next step starts from the loaded weights
     a.model.load_state_dict(sd)
     tp = a.trainer().parameters()
     assert all(torch.equal(tp[k].cpu(), sd[k].float()) for k in tp)
+
+
+# ----------------------------------------------------------------------------------------- mixed precision
+def _autocast_step(sd, x, xl, y, yl, t, z, attn, dt):
+    """The reference's own mixed-precision arithmetic: autograd through the oracle on the GPU under
+    torch.autocast(dt) on the given alignment; fp16 with GradScaler's rule (loss x 2^16, halved until the gradient
+    is finite). -> (losses, unscaled fp32 gradients, the scale that was used)"""
+    import oracle.matcha_oracle as O
+    S = 65536.0 if dt == torch.float16 else 1.0
+    while True:
+        params = {k: v.clone().float().to(DEV).requires_grad_(True) for k, v in sd.items()
+                  if k.startswith(("encoder.", "decoder.estimator."))}
+        with torch.autocast("cuda", dtype=dt):
+            dur, prior, cfm, _, _ = O.training_losses(params, *(v.to(DEV) for v in (x, xl, y, yl, t, z)), HP,
+                                                      mas=lambda lp, m: attn.to(DEV))
+        grads = torch.autograd.grad((dur + prior + cfm) * S, list(params.values()), allow_unused=True)
+        g = {k: (gr.float() / S if gr is not None else torch.zeros_like(p)).cpu() for (k, p), gr in
+             zip(params.items(), grads)}
+        if all(torch.isfinite(v).all() for v in g.values()) or S < 1.0:
+            return [float(v) for v in (dur, prior, cfm)], g, S
+        S /= 2.0
+
+
+@pytest.mark.parametrize("precision,dt", [("16-mixed", torch.float16), ("bf16-mixed", torch.bfloat16)])
+def test_training_step_mixed_precision_vs_autocast(precision, dt):
+    """The whole step in the reference's training precision (train_standalone.py:764, 868: "16-mixed"; and
+    "bf16-mixed") at configs[4]'s size (B = 64, T_y = 868), against the fp32 autograd oracle: the alignment is the
+    fp32 run's (the log-prior / MAS path stays exact fp32), and the losses and the flat gradient are no further from
+    the fp32 oracle than the reference's own mixed arithmetic (the oracle under torch.autocast on the GPU, same
+    alignment, fp16 with GradScaler's backoff) is, with a 25 % margin (or within a floor of 2e-4 on a loss)."""
+    from matcha_hip.train import MatchaTrainer
+    import oracle.matcha_oracle as O
+    sd, x, xl, y, yl, t, z = _configs4_batch(seed=43)
+    args = (x.to(DEV), xl.to(DEV), y.to(DEV), yl.to(DEV))
+    ref = MatchaTrainer(sd, HP, DEV, dropout=False)
+    attn = ref.forward_backward(*args, t=t.to(DEV), z=z.to(DEV))["attn"].cpu()
+    del ref
+    tr = MatchaTrainer(sd, HP, DEV, dropout=False, precision=precision)
+    out = tr.forward_backward(*args, t=t.to(DEV), z=z.to(DEV))
+    S = tr.scaler["scale"] if tr.scaler else 1.0
+    assert torch.equal(out["attn"].cpu(), attn)
+    names = list(tr.grads.names)
+    mine = tr.grads.flat.detach().double().cpu() / S
+    assert torch.isfinite(mine).all()
+    (dur, prior, cfm, _, _), gref = _oracle_grads(sd, x, xl, y, yl, t, z, mas=lambda lp, m: attn)
+    flat_ref = torch.cat([gref[n].reshape(-1) for n in names]).double()
+    ac_losses, ac_g, ac_S = _autocast_step(sd, x, xl, y, yl, t, z, attn, dt)
+    flat_ac = torch.cat([ac_g[n].reshape(-1) for n in names]).double()
+    e_mine, e_ac = _rel(mine, flat_ref), _rel(flat_ac, flat_ref)
+    l_ref = [float(v) for v in (dur, prior, cfm)]
+    l_mine = [float(out[k]) for k in ("dur_loss", "prior_loss", "cfm_loss")]
+    print(f"{precision}: flat {e_mine:.3e} vs autocast {e_ac:.3e} (scale {ac_S}); losses "
+          f"{[abs(a - b) / abs(b) for a, b in zip(l_mine, l_ref)]} vs {[abs(a - b) / abs(b) for a, b in zip(ac_losses, l_ref)]}")
+    assert e_mine <= 1.25 * e_ac, (e_mine, e_ac)
+    for a_, c_, r_ in zip(l_mine, ac_losses, l_ref):
+        assert abs(a_ - r_) <= max(1.25 * abs(c_ - r_), 2e-4 * abs(r_)), (a_, c_, r_)
+
+
+def test_loss_scaler_skip_backoff_and_growth():
+    """GradScaler semantics of "16-mixed" (torch.cuda.amp defaults, Lightning's MixedPrecision plugin): a non-finite
+    element anywhere in the gradient (inf or NaN) skips the update — parameters, Adam moments and step count
+    untouched — and halves the scale; growth_interval finite steps in a row double it; and each taken step equals
+    clip_grad_norm_(5.0) + Adam applied by torch to the unscaled gradient."""
+    from matcha_hip.train import MatchaTrainer
+    sd, x, xl, y, yl, t, z = _setup(seed=26)
+    args = (x.to(DEV), xl.to(DEV), y.to(DEV), yl.to(DEV))
+    kw = dict(t=t.to(DEV), z=z.to(DEV))
+    tr = MatchaTrainer(sd, HP, DEV, dropout=False, precision="16-mixed")
+    tr.scaler.update(scale=1024.0, growth_interval=3)
+    for i, bad in enumerate((float("inf"), float("nan"), -float("inf"))):
+        tr.forward_backward(*args, **kw)
+        p0, m0 = tr.params.flat.clone(), tr.m.clone()
+        tr.grads.flat[1000 + 7 * i] = bad
+        assert tr.optimizer_step()["skipped"]
+        assert tr.scaler["scale"] == 1024.0 / 2 ** (i + 1) and tr.scaler["_growth_tracker"] == 0
+        assert tr.step_count == 0 and torch.equal(tr.params.flat, p0) and torch.equal(tr.m, m0)
+    tr.scaler["scale"] = 1024.0
+    for i in range(3):
+        tr.forward_backward(*args, **kw)
+        S = tr.scaler["scale"]
+        g = {k: v.detach().cpu() / S for k, v in tr.gradients().items()}
+        p0 = {k: v.detach().cpu().clone() for k, v in tr.parameters().items()}
+        m_ref = [tr.m.cpu().clone(), tr.v.cpu().clone()]
+        assert not tr.optimizer_step()["skipped"]
+        # torch on the same (unscaled) gradient from the same state: the first step only (fresh Adam moments)
+        if i == 0:
+            ref = {k: p0[k].clone().requires_grad_(True) for k in tr.grads.names}
+            for k, p in ref.items():
+                p.grad = g[k].clone()
+            norm = torch.nn.utils.clip_grad_norm_(list(ref.values()), 5.0)
+            torch.optim.Adam(list(ref.values()), lr=1e-4).step()
+            assert abs(tr.last["grad_norm"].item() - norm.item()) <= 1e-5 * norm.item()
+            assert max(float((tr.parameters()[k].cpu() - ref[k].detach()).abs().max()) for k in ref) < 5e-7
+            assert float(m_ref[0].abs().max()) == 0.0
+    assert tr.step_count == 3 and tr.scaler["scale"] == 2048.0 and tr.scaler["_growth_tracker"] == 0
+
+
+def test_loss_scaler_found_inf_is_per_element():
+    """torch's found-inf is per element of the unscaled gradient (torch._amp_foreach_non_finite_check_and_unscale_),
+    not a test of the sum of squares: a finite gradient so large that its squared norm overflows fp32 is NOT
+    skipped (round-3 verdict) — the clip factor goes to 0, as in clip_grad_norm_, and Adam takes a zero step."""
+    from matcha_hip.train import MatchaTrainer
+    sd, x, xl, y, yl, t, z = _setup(seed=27)
+    tr = MatchaTrainer(sd, HP, DEV, dropout=False, precision="16-mixed")
+    tr.scaler.update(scale=1024.0)
+    tr.forward_backward(x.to(DEV), xl.to(DEV), y.to(DEV), yl.to(DEV), t=t.to(DEV), z=z.to(DEV))
+    tr.grads.flat[5] = 3.0e38  # finite after the unscale; its square overflows
+    tr.grads.flat[6] = -3.0e38
+    p0 = tr.params.flat.clone()
+    out = tr.optimizer_step()
+    assert not out["skipped"] and tr.step_count == 1 and tr.scaler["_growth_tracker"] == 1
+    assert not math.isfinite(out["grad_norm"].item())
+    assert torch.equal(tr.params.flat, p0)  # clip factor 0 -> zero gradient -> Adam's first step moves nothing

@@ -1,7 +1,7 @@
 #!/bin/bash
 # SGPR spills (v_writelane) and SGPR / VGPR counts per kernel of one source file, from the device assembly.
 # mt_vconv sits at the 100-SGPR limit: run this before and after any change that adds wave-uniform state, and A/B
-# the two BUILDS (tools/r3ll.sh with MT_LIB) rather than a knob inside one build (experiments that lost).
+# the two BUILDS (tools/ab_build.sh + tools/ab_run.sh) rather than a knob inside one build (experiments that lost).
 # Usage: bash tools/sgpr_spills.sh matcha-tts_amd/csrc/mt_vconv.hip [extra hipcc flags]
 set -o pipefail
 SRC=${1:?source file}; shift

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time the bench step's vocoder alone (bf16 Generator with the step's per-utterance lengths, i.e. the ragged
 launch chain) on the mel the bench's synthesize produces. A/B knobs act through the environment (MT_LIB,
-MT_VCONV_EARLY, MT_XCD_TILES). Usage: python tools/voc_time.py [B] [reps]"""
+MT_XCD_TILES). Usage: python tools/voc_time.py [B] [reps]"""
 import os
 import sys
 
