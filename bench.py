@@ -220,7 +220,7 @@ def roofline_by_kernel(detail, frame_scale=1.0):
     pairs, priced as their two convs): mean launch ms, algorithmic rate on both sides and the fraction of the
     side the kernel's own intensity bounds it by."""
     out = {}
-    for kind in ("vconv", "vpair128", "vpair", "vpair32", "rbfuse"):
+    for kind in ("rbconv", "vconv", "vpair128", "vpair", "vpair32", "rbfuse"):
         ls = [d for d in detail if d["kind"] == kind]
         if not ls:
             continue
@@ -236,7 +236,7 @@ def roofline_by_kernel(detail, frame_scale=1.0):
     return out
 
 
-def roofline(probe, default_workload=True, frame_scale=1.0):
+def roofline(probe, default_workload=True, frame_scale=1.0, pmc_name="pmc_vconv.json"):
     """Dominant kernel family of the step: the LDS-DMA persistent implicit-GEMM convs that run every ResBlock
     conv of HiFi-GAN (51 launches per step): per layer on mt_vconv, stage 1 and stage 2's k = 7 / 11 resblocks
     (30 convs; C = 256/128 on B x 8/64 * T_y frames); as fused conv pairs, stage 2's k = 3 resblock on
@@ -265,8 +265,8 @@ def roofline(probe, default_workload=True, frame_scale=1.0):
     gbs = nbytes / (ms * 1e-3) / 1e9
     peak_f, peak_b = PEAK_FLOPS / 1e12, PEAK_BW / 1e9
     ridge = PEAK_FLOPS / PEAK_BW
-    traffic, pmc_file = None, _latest_profile("pmc_vconv.json")
-    if pmc_file and default_workload:  # the PMC passes ran the default bench workload only
+    traffic, pmc_file = None, _latest_profile(pmc_name)
+    if pmc_file and default_workload:  # the PMC passes ran this workload (pmc_name: the default or the B=256 one)
         try:
             traffic = json.load(open(pmc_file)).get("hbm_bytes_per_launch")
         except Exception:
@@ -279,7 +279,8 @@ def roofline(probe, default_workload=True, frame_scale=1.0):
             "frac": round(achieved / peak, 4), "traffic": traffic,
             "traffic_ratio": round(traffic / nbytes, 3) if traffic else None,
             "traffic_source": os.path.relpath(pmc_file, HERE) if traffic else None,
-            "kernel": "vconv_kernel<bf16> LDS-DMA implicit-GEMM conv, HiFi-GAN stage 1-4 ResBlock convs (stage 2 k=3 and stages 3-4 as fused pairs)",
+            "kernel": "LDS-DMA implicit-GEMM convs, HiFi-GAN stage 1-4 ResBlock convs: rbconv_kernel (stages 1-2 per layer, "
+                      "compile-time K loop), vpair128 (stage 2 k=3 pairs), vpair / vpair32 (stages 3-4 pairs)",
             "launches": n, "launch_ms": round(ms, 4), "flops_per_launch": flops,
             "algo_bytes_per_launch": nbytes, "intensity_flop_per_byte": round(intensity, 1),
             "tflops": round(tflops, 2), "mfma_frac": round(tflops / peak_f, 4),
@@ -355,22 +356,34 @@ def cpu_baseline(m_sd, g_sd, x, xl, n_ts, n_utt=3):
 def north_star(m, g, den, batch, seed, n_ts, denoise, steps=10, warmup=2):
     """BASELINE north_star target point: B=256 utterances on ONE MI355X, 10-step text->wav, timed in this
     same run (its own warm-up; barrier-free single GPU)."""
+    from matcha_hip import runtime as rt
     x_cpu, xl_cpu = shard_inputs(0, 1, batch, seed)
     x, xl = x_cpu.to(m.mel_mean.device), xl_cpu.to(m.mel_mean.device)
     for _ in range(warmup):
         step(m, g, den, x, xl, n_ts, denoise)
     _, yl, _ = step(m, g, den, x, xl, n_ts, denoise)
     yls = [int(v) for v in yl.cpu()]
+    # the roofline family's launches of the LAST timed step are probed, as on the headline line
+    rt.probe_start(rt.PROBE_VCONV, 64)
+    rt.probe_pause(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
+        if i == steps - 1:
+            rt.probe_pause(False)
         step(m, g, den, x, xl, n_ts, denoise)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / steps
+    detail = rt.probe_detail()
+    probe = rt.probe_stop()
     t_pad = 4 * math.ceil(max(yls) / 4)
+    fs = sum(yls) / (len(yls) * max(yls))
+    roof = roofline(probe, default_workload=True, frame_scale=fs, pmc_name="pmc_vconv_b256.json")
+    roof["by_kernel"] = roofline_by_kernel(detail, frame_scale=fs)
     return {"batch": batch, "steps": steps, "warmup": warmup, "ms_per_step": round(el * 1e3, 3),
             "value": round(sum(yls) / el, 2), "unit": "mel-frames/s", "seq_len": t_pad,
-            "rtf": round(el / (sum(yls) * HOP / SR), 6), "path_roofline": path_roofline(el, yls, t_pad, n_ts)}
+            "rtf": round(el / (sum(yls) * HOP / SR), 6), "roofline": roof,
+            "path_roofline": path_roofline(el, yls, t_pad, n_ts)}
 
 
 def timed_batch(m, g, den, x, xl, n_ts, denoise, steps, warmup):

@@ -346,12 +346,17 @@ int mt_op_conv1d_tile(int variant, int dtype, const void* x, int B, int Tin, int
                       float slope, void* y, int Tout, void* ws, size_t ws_bytes, void* stream);
 /* Op-level entry of mt_vconv (tests / A-B timing): bf16 x [B][L][cin] already activated, fp32
  * W [cout][cin][k], bias [cout], padding dil*(k-1)/2 ("same"), epilogue flags ef: 1 + resid,
- * 2 accumulate into y, 4 / div, 8 y = lrelu(v), 16 also y2 = lrelu(v). pack = 0 reuses the weights a
+ * 2 accumulate into y, 4 / div, 8 y = lrelu(v), 16 also y2 = lrelu(v); lens (nullable, device int32 [B]): the
+ * ragged batch, utterance b valid for its first lens[b] frames. pack = 0 reuses the weights a
  * previous call with the same ws packed (timing). One ResBlock1 conv of hifigan/models.py:90-97. */
 size_t mt_op_vconv_workspace_bytes(int cin, int cout, int k);
 int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const float* bias, int cout, int k, int dil,
-                int ef, const void* resid, void* y, void* y2, float slope, float div, int pack, void* ws,
-                size_t ws_bytes, void* stream);
+                int ef, const void* resid, void* y, void* y2, float slope, float div, const int32_t* lens, int pack,
+                void* ws, size_t ws_bytes, void* stream);
+/* The HiFi-GAN wide-stage ResBlock convs (C_in = C_out in {128, 256}, k in {3, 7, 11}) run on mt_rbconv, a variant
+ * of mt_vconv whose K loop is scheduled at compile time (1, the default; bit-identical results) or on the generic
+ * mt_vconv kernel (0). Process-wide; returns the previous setting. */
+int mt_vconv_set_rbconv(int enable);
 /* qkv [B][T][3*heads*64], mask [B][T] -> out [B][T][heads*64], reference mask semantics */
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                     void* stream);

@@ -355,9 +355,10 @@ size_t mt_op_vconv_workspace_bytes(int cin, int cout, int k) {
   (void)g;
   return pk.off;
 }
+int mt_vconv_set_rbconv(int enable) { return mt::rbconv_set(enable); }
 int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const float* bias, int cout, int k, int dil,
-                int ef, const void* resid, void* y, void* y2, float slope, float div, int pack, void* ws,
-                size_t ws_bytes, void* stream) {
+                int ef, const void* resid, void* y, void* y2, float slope, float div, const int32_t* lens, int pack,
+                void* ws, size_t ws_bytes, void* stream) {
   MT_REQUIRE(x && W && bias && y && ws, "op_vconv: null argument");
   MT_REQUIRE(mt::vconv_supported(cin, cout, k, dil, 1), "op_vconv: unsupported conv %dx%d k%d d%d", cin, cout, k, dil);
   hipStream_t st = (hipStream_t)stream;
@@ -393,6 +394,8 @@ int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const floa
   a.div = div;
   a.zero = (const mt::bf16*)(P + z_off);
   a.trash = (mt::bf16*)(P + t_off);
+  a.lens = (const int*)lens;
+  a.lmul = 1;
   return mt::launch_vconv(ef, a, st);
 }
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,

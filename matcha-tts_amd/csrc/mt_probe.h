@@ -18,7 +18,7 @@ bool probe_armed(int site);
 bool probe_any_armed();  // some site armed (its launches need per-launch host bookkeeping)
 void probe_begin(int site, hipStream_t st);
 // tag: the launching kernel's kind (PROBE_TAG_*), reported per launch by probe_detail
-enum ProbeTag { PROBE_TAG_VCONV = 0, PROBE_TAG_VPAIR = 1, PROBE_TAG_VPAIR32 = 2, PROBE_TAG_RBFUSE = 3, PROBE_TAG_VPAIR128 = 4 };
+enum ProbeTag { PROBE_TAG_VCONV = 0, PROBE_TAG_VPAIR = 1, PROBE_TAG_VPAIR32 = 2, PROBE_TAG_RBFUSE = 3, PROBE_TAG_VPAIR128 = 4, PROBE_TAG_RBCONV = 5 };
 void probe_end(int site, hipStream_t st, double flops, double bytes, int tag = PROBE_TAG_VCONV);
 // per-launch duration (ms), algorithmic FLOPs / bytes and tag of the recorded launches (synchronizes their
 // events; call before probe_stop) -> launches written (<= cap)

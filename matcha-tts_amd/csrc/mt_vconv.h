@@ -110,6 +110,11 @@ size_t vconv_packed_bytes(int cin, int cout, int k);
 int vconv_repack(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st,
                  int cin_src = -1);
 int launch_vconv(int ef, const VConvArgs& a, hipStream_t st);
+// mt_rbconv: the HiFi-GAN wide-stage ResBlock convs (C_in = C_out in {128, 256}, k in {3, 7, 11}) on a K loop scheduled
+// at compile time; launch_vconv dispatches to it (MT_RBCONV=0: off). Same results as the mt_vconv kernel, bit for bit.
+bool rbconv_handles(int ef, const VConvArgs& a);
+int launch_rbconv(int ef, const VConvArgs& a, int G, hipStream_t st);
+int rbconv_set(int enable);  // -> the previous setting
 // fp32 mode (VConvArgs::f32): [Mpad0][taps][cin_pad] fp32 -> [cin/32][taps][Mpad][32] fp32
 bool vconv_supported_f32(int cin, int cout, int k, int stride);
 size_t vconv_packed_bytes_f32(int cin, int cout, int k);

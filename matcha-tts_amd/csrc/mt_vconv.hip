@@ -1090,6 +1090,13 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   // the probe site covers the HiFi-GAN ResBlock convs (k >= 3), the bench's roofline family
   const int site = a.probe ? a.probe : PROBE_VCONV;
   const bool probed = !k1 && site > 0;
+  if (!k1 && !placed && BM == 128 && rbconv_handles(ef, a)) {  // the HiFi-GAN wide-stage ResBlock convs (mt_rbconv)
+    if (probed) probe_begin(site, st);
+    const int rc = launch_rbconv(ef, a, G, st);
+    if (rc) return rc;
+    if (probed) probe_end(site, st, flops, bytes, PROBE_TAG_RBCONV);
+    return 0;
+  }
   if (probed) probe_begin(site, st);
 #define MT_VCASE(E)                                                                                \
   case E:                                                                                          \

@@ -87,7 +87,8 @@ SIGNATURES = {
                                   c_int, c_float, P, c_int, P, c_size_t, P]),
     "mt_op_vconv_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mt_op_vconv": (c_int, [P, c_int, c_int, c_int, P, P, c_int, c_int, c_int, c_int, P, P, P, c_float, c_float,
-                            c_int, P, c_size_t, P]),
+                            P, c_int, P, c_size_t, P]),
+    "mt_vconv_set_rbconv": (c_int, [c_int]),
     "mt_op_attention": (c_int, [c_int, P, P, P, c_int, c_int, c_int, P]),
     "mt_probe_start": (c_int, [c_int, c_int]),
     "mt_probe_pause": (c_int, [c_int]),

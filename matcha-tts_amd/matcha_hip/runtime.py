@@ -549,10 +549,11 @@ def op_conv1d(x_btc: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor]
 
 def op_vconv(x_btc: torch.Tensor, W: torch.Tensor, bias: torch.Tensor, dil: int = 1, ef: int = 0,
              resid: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None,
-             slope: float = 0.1, div: float = 1.0, ws: Optional[torch.Tensor] = None, pack: bool = True):
+             slope: float = 0.1, div: float = 1.0, ws: Optional[torch.Tensor] = None, pack: bool = True,
+             lens: Optional[torch.Tensor] = None):
     """Op-level test entry of mt_vconv: one "same"-padded bf16 Conv1d on an already activated
     [B,L,C] input with the ResBlock epilogues (ef bits: 1 resid, 2 accumulate into y, 4 /div,
-    8 y=lrelu(v), 16 also y2=lrelu(v)). Returns (y, y2)."""
+    8 y=lrelu(v), 16 also y2=lrelu(v)); lens (int32 [B] on the device): a ragged batch. Returns (y, y2)."""
     require_gpu(x_btc, what="op_vconv")
     x = x_btc.to(torch.bfloat16).contiguous()
     B, L, cin = x.shape
@@ -570,10 +571,18 @@ def op_vconv(x_btc: torch.Tensor, W: torch.Tensor, bias: torch.Tensor, dil: int 
             raise ValueError("op_vconv: pack=False needs the workspace a packing call filled")
         ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
     W, bias = f32c(W), f32c(bias)
+    if lens is not None:
+        lens = lens.to(device=x.device, dtype=torch.int32).contiguous()
     check(L_.mt_op_vconv(ptr(x), B, L, cin, ptr(W), ptr(bias), cout, k, dil, int(ef), ptr(resid), ptr(y), ptr(y2),
-                         float(slope), float(div), int(bool(pack)), ws.data_ptr(), ws.numel(),
+                         float(slope), float(div), ptr(lens), int(bool(pack)), ws.data_ptr(), ws.numel(),
                          stream_handle(x.device)), "op_vconv")
     return y, y2
+
+
+def set_rbconv(enable: bool) -> bool:
+    """the HiFi-GAN wide-stage ResBlock convs on mt_rbconv (True, default) or the generic mt_vconv kernel; returns
+    the previous setting (process-wide)"""
+    return bool(lib().mt_vconv_set_rbconv(int(bool(enable))))
 
 
 def op_attention(qkv: torch.Tensor, mask: torch.Tensor, heads: int, precision="fp32") -> torch.Tensor:
@@ -603,7 +612,7 @@ def probe_pause(paused: bool) -> None:
     check(lib().mt_probe_pause(int(bool(paused))), "probe_pause")
 
 
-PROBE_TAGS = ("vconv", "vpair", "vpair32", "rbfuse", "vpair128")
+PROBE_TAGS = ("vconv", "vpair", "vpair32", "rbfuse", "vpair128", "rbconv")
 
 
 def probe_detail(cap: int = 4096) -> List[Dict[str, float]]:
