@@ -357,6 +357,10 @@ int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const floa
  * of mt_vconv whose K loop is scheduled at compile time (1, the default; bit-identical results) or on the generic
  * mt_vconv kernel (0). Process-wide; returns the previous setting. */
 int mt_vconv_set_rbconv(int enable);
+/* The decoder's convs and the upsamplers run mt_vconv with their K loop unrolled at compile time for their
+ * (C_in, taps) (1, the default; bit-identical results) or with the runtime-cursor loop (0). Process-wide; returns
+ * the previous setting. */
+int mt_vconv_set_ct(int enable);
 /* qkv [B][T][3*heads*64], mask [B][T] -> out [B][T][heads*64], reference mask semantics */
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                     void* stream);

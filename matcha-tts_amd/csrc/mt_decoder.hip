@@ -853,7 +853,7 @@ struct Decoder::GraphCache {
   struct Entry {
     const void* P;
     const void* ws;
-    int B, T, S, n_steps, solver, uni0, uni1, vconv, gnres, uniform_attn;
+    int B, T, S, n_steps, solver, uni0, uni1, vconv, gnres, uniform_attn, kpath;
     hipGraphExec_t ex;
   };
   std::vector<Entry> entries;  // most recently used last
@@ -872,12 +872,14 @@ int Decoder::chain_graph(const char* P, const Work& w, const TimeSched& ts, int 
                          int solver, const void* ws, hipGraphExec_t* out) const {
   if (!gcache) gcache = std::make_shared<GraphCache>();
   GraphCache& gc = *gcache;
-  const GraphCache::Entry key{P, ws, B, T, S, n_steps, solver, w.uni0, w.uni1, vconv, gnres, uniform_attn, nullptr};
+  // kpath: the process-wide kernel selection (compile-time K loops on / off): a graph holds the kernels it captured
+  const GraphCache::Entry key{P, ws, B, T, S, n_steps, solver, w.uni0, w.uni1, vconv, gnres, uniform_attn,
+                              vconv_path_id(), nullptr};
   for (size_t i = 0; i < gc.entries.size(); ++i) {
     const GraphCache::Entry& e = gc.entries[i];
     if (e.P == key.P && e.ws == key.ws && e.B == key.B && e.T == key.T && e.S == key.S && e.n_steps == key.n_steps &&
         e.solver == key.solver && e.uni0 == key.uni0 && e.uni1 == key.uni1 && e.vconv == key.vconv &&
-        e.gnres == key.gnres && e.uniform_attn == key.uniform_attn) {
+        e.gnres == key.gnres && e.uniform_attn == key.uniform_attn && e.kpath == key.kpath) {
       GraphCache::Entry hit = e;
       gc.entries.erase(gc.entries.begin() + (long)i);
       gc.entries.push_back(hit);

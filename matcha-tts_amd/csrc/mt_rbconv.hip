@@ -15,12 +15,11 @@
 // buffers (staged once per chunk at the chunk's first step, read by every tap shifted by t * d rows). Rows are 128 B
 // with the 16-byte unit XOR-swizzled by (row & 6): conflict-free ds_read_b128 for every shift.
 //
-// Counted waits: each wave issues, per step and in program order, [the epilogue's residual / accumulator loads on a
-// tile's last step] [5 row pieces on a chunk's first step] [2 weight pieces] [the epilogue stores on a tile's last
-// step]. The step-(q+1) data a wait needs was issued at step q-2 (weights) or at the previous chunk's first step
-// (rows); the VMEM operations issued after it are a compile-time function of the step's position in the tile
-// (rb_after), the same for every tile because the prologue issues the tail of a virtual previous tile (its residual
-// loads, the third weight step and its stores, all to valid addresses) in the steady state's order.
+// Counted waits (VcSched, mt_vconv.h): the loader waves issue, per step and in program order, [the epilogue's residual
+// / accumulator loads on a tile's last step] [row pieces of the next chunk on its first TX taps] [the weight pieces of
+// step s + 3] [the epilogue stores on a tile's last step]; the data a wait needs was issued at step s - 2 (weights)
+// or over the previous chunk's first taps (rows), so the operations issued after it are a compile-time function of
+// the step's position in the tile. Tile 0's first waits count the prologue's staging instead (wait_first).
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -37,8 +36,6 @@ constexpr int RWSLOT = RBM * 128;           // 128 rows x 64 bf16 channels
 constexpr int RNW = 4;                       // weight ring slots
 constexpr int RXROWS = RBN + 64;             // staged rows per chunk (256 frames + halo <= 64)
 constexpr int RXBUF = RXROWS * 128;
-constexpr int RNXW = RXROWS / 64;            // row pieces per wave per chunk (8 waves x 1 KiB)
-constexpr int RNWW = RBM / 64;               // weight pieces per wave per step
 constexpr int RX_OFF = RNW * RWSLOT;
 constexpr int RBIAS_OFF = RX_OFF + 2 * RXBUF;
 constexpr int RRAG_OFF = RBIAS_OFF + 256 * 4;
@@ -46,51 +43,25 @@ constexpr int RLDS = RRAG_OFF + RAG_LDS;
 static_assert(RLDS <= 160 * 1024, "LDS budget");
 constexpr int RFN = 4, RWNC = 64;
 
-// VMEM operations per wave: epilogue loads (residual, old accumulator: 8 x 16 B each) and stores (y, y2)
-template <int EF>
-constexpr int rb_nepi() { return 8 * (((EF & VE_RESID) ? 1 : 0) + ((EF & VE_ACCUM) ? 1 : 0)); }
+// Staging by LW loader waves (waves 0 .. LW-1; with LW = 4 one per SIMD, so the other wave of each SIMD never
+// stalls on DMA issue): per step WPW weight pieces each, per chunk XPW row pieces each, spread over the chunk's first
+// TX steps (>= 2 steps before they are needed). Counted waits: VcSched (mt_vconv.h).
+template <int LW>
+struct RbStage {
+  static constexpr int WPW = 16 / LW, XPW = 40 / LW;
+};
+template <int K, int LW>
+constexpr int rb_tx() {
+  const int t = K - 2 < 1 ? 1 : K - 2;
+  return t < RbStage<LW>::XPW ? t : RbStage<LW>::XPW;
+}
 template <int EF>
 constexpr int rb_nst() { return 8 * ((EF & VE_DUAL) ? 2 : 1); }
 
-// VMEM operations a wave issues in step s of a tile of S steps (K taps per chunk): everything in program order
-template <int EF, int K>
-constexpr int rb_ops(int s, int S) {
-  return (s == S - 1 ? rb_nepi<EF>() : 0) + (s % K == 0 ? RNXW : 0) + RNWW + (s == S - 1 ? rb_nst<EF>() : 0);
-}
-// issued after the weight pieces of step s (its stores on a tile's last step)
-template <int EF>
-constexpr int rb_ops_after_w(int s, int S) { return s == S - 1 ? rb_nst<EF>() : 0; }
-// issued after the row pieces of step s (its weights and stores)
-template <int EF>
-constexpr int rb_ops_after_x(int s, int S) { return RNWW + rb_ops_after_w<EF>(s, S); }
-
-// the wait at the top of step s: the data of step s + 1 must have landed. Its weights were issued at step s - 2
-// (tile-periodic: index mod S), its rows (when step s + 1 starts a chunk) at the previous chunk's first step.
-// Returns the VMEM operations issued after the youngest of them.
-template <int EF, int K>
-constexpr int rb_after(int s, int S) {
-  auto md = [S](int v) { return ((v % S) + S) % S; };
-  int nw = rb_ops_after_w<EF>(md(s - 2), S) + rb_ops<EF, K>(md(s - 1), S);
-  if ((s + 1) % K == 0) {  // step s + 1 starts a chunk: its rows came from step s + 1 - K (mod S)
-    const int sx = md(s + 1 - K);
-    int nx = rb_ops_after_x<EF>(sx, S);
-    for (int v = sx + 1; v < sx + K; ++v) nx += rb_ops<EF, K>(md(v), S);  // steps sx+1 .. s-1 ... up to s - 1
-    // sx + K - 1 == s: the loop above counted steps sx+1 .. s-1 plus step s itself; drop step s (not issued yet)
-    nx -= rb_ops<EF, K>(md(s), S);
-    nw = nw < nx ? nw : nx;
-  }
-  return nw;
-}
 }  // namespace
 
 __device__ __forceinline__ void rb_glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-
-template <int N>
-__device__ __forceinline__ void rb_wait_vmcnt() {
-  static_assert(N >= 0 && N <= 63, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 __device__ __forceinline__ void rb_barrier() {
@@ -110,8 +81,10 @@ __device__ __forceinline__ void rb_for(F&& f) {
   }
 }
 
-template <int EF, int C, int K>
+template <int EF, int C, int K, int LW>
 __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
+  constexpr int WPW = RbStage<LW>::WPW, XPW = RbStage<LW>::XPW, TX = rb_tx<K, LW>();
+  using SCH = VcSched<C / 64, K, RNW, 2, TX, WPW, XPW, rb_nst<EF>()>;
   constexpr int NCH = C / 64, S = NCH * K;        // chunks, steps per tile
   static_assert(NCH % 2 == 0 && S % 2 == 0, "schedule period (row buffers alternate per chunk)");
   constexpr int NTM = C / RBM;                    // row tiles
@@ -143,7 +116,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   struct Tile {
     int b, n0, m0;
   };
-  auto tile_of = [&](int ti) {
+  auto tile_of = [&](int ti) __attribute__((always_inline)) {
     Tile tl;
     const int tile = gl + min(ti, nmine - 1) * gstep;  // past the last tile: the last one (phantom prefetches)
     const int r = tile / NTM;
@@ -159,30 +132,33 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   };
 
   const int lrow = lane >> 3, lp = lane & 7;
-  // weight piece i of this wave: row r of the 128-row slot, 16-byte unit q (swizzled on the source address)
-  int woff[RNWW];
+  const bool loader = wave < LW;
+  // weight piece i of a loader wave: row r of the 128-row slot, 16-byte unit q (swizzled on the source address)
+  int woff[WPW];
 #pragma unroll
-  for (int i = 0; i < RNWW; ++i) {
-    const int r = 8 * (wave * RNWW + i) + lrow;
+  for (int i = 0; i < WPW; ++i) {
+    const int r = 8 * (wave * WPW + i) + lrow;
     woff[i] = r * 128 + ((lp ^ (r & 6)) * 16);
   }
   const char* wbase = reinterpret_cast<const char*>(a.w);
-  auto issue_w = [&](const Tile& tl, int c, int t, int slot) {
+  auto issue_w = [&](const Tile& tl, int c, int t, int slot) __attribute__((always_inline)) {
     const char* base = wbase + ((size_t)(c * K + t) * C + tl.m0) * 128;
     // the LDS destination goes through an opaque copy: with a known constant offset the compiler tracks the DMA's
     // LDS range and puts a vmcnt wait before every ds_read it cannot prove disjoint (all of them), draining the
     // prefetch each step; the ordering is ours (counted waits + barrier)
-    int so = slot * RWSLOT + wave * RNWW * 1024;
+    int so = slot * RWSLOT + wave * WPW * 1024;
     asm volatile("" : "+s"(so));
 #pragma unroll
-    for (int i = 0; i < RNWW; ++i) {
+    for (int i = 0; i < WPW; ++i) {
       int wo = woff[i];
       asm volatile("" : "+v"(wo));  // per-step address (see read_frag)
       rb_glds16(base + wo, smem + so + i * 1024);
     }
   };
   const int R = RBN + (K - 1) * dil;
-  auto issue_x = [&](const Tile& tl, int c, int buf) {
+  // the row pieces i (of this loader wave's XPW) with i * TX / XPW == part, of chunk c of a tile
+  auto issue_x = [&](const Tile& tl, int c, int buf, auto partc) __attribute__((always_inline)) {
+    constexpr int part = decltype(partc)::value;
     const int f0 = tl.n0 - a.pad;
     const int Lx = rag ? rlv[tl.b] : L;
     const char* xb = reinterpret_cast<const char*>(a.x) + ((size_t)tl.b * L * C + c * 64) * 2;
@@ -190,8 +166,9 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
     asm volatile("" : "+s"(xo));  // opaque LDS destination (see issue_w)
     char* dst = smem + xo;
 #pragma unroll
-    for (int i = 0; i < RNXW; ++i) {
-      const int j = wave + 8 * i;
+    for (int i = 0; i < XPW; ++i) {
+      if (i * TX / XPW != part) continue;
+      const int j = wave + LW * i;
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
@@ -216,7 +193,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   const int ch16 = wm * 64 + (g4 & 1) * 16 + (g4 >> 1) * 8;
   u32x4 rv[2][RFN], yv[2][RFN];
   // epilogue operand loads of a tile (issued at the start of its last step, consumed after its MFMAs)
-  auto epi_loads = [&](const Tile& tl) {
+  auto epi_loads = [&](const Tile& tl) __attribute__((always_inline)) {
     const size_t rowbase = (size_t)tl.b * L;
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
@@ -230,7 +207,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   };
   // mt_vconv's packed epilogue (bias, + residual, + old accumulator, / div, then lrelu / dual outputs), the same
   // operations in the same order; every lane stores (frames past L go to the trash line): RNST per tile
-  auto epilogue = [&](const Tile& tl, bool real) {
+  auto epilogue = [&](const Tile& tl, bool real) __attribute__((always_inline)) {
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -290,7 +267,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   // The per-lane fragment addresses of a step depend only on (slot, buffer, tap), so the compiler would compute
   // every step's once outside the tile loop and keep them all live (hundreds of VGPRs, scratch spills); the
   // opaque copies below make them per-step values (a handful of VALU each step).
-  auto read_frag = [&](Frag& F, int ks, int slot, int xbuf, int tap) {
+  auto read_frag = [&](Frag& F, int ks, int slot, int xbuf, int tap) __attribute__((always_inline)) {
     int lb = rbl, la = 0;
     asm volatile("" : "+v"(lb), "+v"(la));
     const char* pa = pa0 + la + slot * RWSLOT;
@@ -316,24 +293,17 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
     __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
   };
 
-  // ---- prologue: tile 0's chunk-0 rows and weights of steps 0..2, with the virtual previous tile's tail ----
+  // ---- prologue: the virtual steps v0 .. -1 stage tile 0's chunk-0 rows (part t at tap t), weights of steps 0 .. 2
   Tile cur = tile_of(0), nxt = tile_of(1);
-  issue_x(cur, 0, 0);
-  issue_w(cur, 0, 0, 0);
-  issue_w(cur, 1 / K, 1 % K, 1);
-  // the virtual previous tile's epilogue loads and stores, as stores of zeros to the trash line (VMEM operations
-  // count in vmcnt in issue order, loads and stores alike). Inline asm: the compiler neither removes them (dead
-  // stores to one address) nor orders them with vmcnt(0) waits (volatile)
-  auto dummy_stores = [&](int n) {
-    const u32x4 z = {0u, 0u, 0u, 0u};
-    char* tp = reinterpret_cast<char*>(a.trash) + 16 * lane;
-    for (int i = 0; i < n; ++i) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(tp), "v"(z) : "memory");
-  };
-  dummy_stores(rb_nepi<EF>());
-  issue_w(cur, 2 / K, 2 % K, 2);
-  dummy_stores(rb_nst<EF>());
-  // step 0's data: rows of chunk 0 and weights of step 0 (issued after them: w1, epi, w2, stores)
-  rb_wait_vmcnt<RNWW + rb_nepi<EF>() + RNWW + rb_nst<EF>()>();
+  if (loader) {
+    vc_for<SCH::v0, 0>([&](auto vc) {
+      constexpr int v = decltype(vc)::value;
+      constexpr int t = SCH::md(v) % K;
+      if constexpr (t < TX && SCH::vfloor(v) + 1 >= 0) issue_x(cur, 0, 0, std::integral_constant<int, t>{});
+      if constexpr (v + RNW - 1 >= 0) issue_w(cur, (v + RNW - 1) / K, (v + RNW - 1) % K, v + RNW - 1);
+    });
+    vc_wait_vmcnt<SCH::wait_first(-1)>();
+  }
   rb_barrier();
   Frag F0, F1;
   read_frag(F0, 0, 0, 0, 0);
@@ -352,15 +322,23 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
       // publish step s+1's data (its weights; its rows when it starts a chunk); every wave's reads of step s-1
       // are done, so its weight slot and (at a chunk's first step) the other row buffer may be restaged
       __builtin_amdgcn_sched_barrier(0);  // the waits stay after the previous step's MFMAs
-      rb_wait_vmcnt<rb_after<EF, K>(s, S)>();
+      if (loader) {
+        if constexpr (SCH::wait_first(s) == SCH::wait(s)) {
+          vc_wait_vmcnt<SCH::wait(s)>();
+        } else {
+          if (ti == 0) vc_wait_vmcnt<SCH::wait_first(s)>();
+          else vc_wait_vmcnt<SCH::wait(s)>();
+        }
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       rb_barrier();
-      if constexpr (s == S - 1 && rb_nepi<EF>() > 0) epi_loads(cur);
-      if constexpr (t == 0) {  // rows of the next chunk (this tile's c + 1, or the next tile's chunk 0)
-        if constexpr (c + 1 < NCH) issue_x(cur, c + 1, (c + 1) % 2);
-        else issue_x(nxt, 0, 0);
-      }
-      {  // weights of step s + 3 (slot of step s - 1)
+      if constexpr (s == S - 1 && (EF & (VE_RESID | VE_ACCUM)) != 0) epi_loads(cur);
+      if (loader) {
+        if constexpr (t < TX) {  // rows of the next chunk (this tile's c + 1, or the next tile's chunk 0), part t
+          if constexpr (c + 1 < NCH) issue_x(cur, c + 1, (c + 1) % 2, std::integral_constant<int, t>{});
+          else issue_x(nxt, 0, 0, std::integral_constant<int, t>{});
+        }
+        // weights of step s + 3 (slot of step s - 1)
         constexpr int s3 = (s + 3) % S, c3 = s3 / K, t3 = s3 % K;
         if constexpr (s + 3 < S) issue_w(cur, c3, t3, slot3);
         else issue_w(nxt, c3, t3, slot3);
@@ -388,9 +366,12 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
 }
 
 namespace {
+#ifndef RB_LOADERS
+#define RB_LOADERS 4
+#endif
 template <int EF, int C, int K>
 void rb_launch(int G, const VConvArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((rbconv_kernel<EF, C, K>), dim3(G), dim3(RNT), 0, st, a);
+  hipLaunchKernelGGL((rbconv_kernel<EF, C, K, RB_LOADERS>), dim3(G), dim3(RNT), 0, st, a);
 }
 // on by default; MT_RBCONV=0 in the environment or mt_vconv_set_rbconv(0): the generic mt_vconv kernel instead
 int g_rb = -1;

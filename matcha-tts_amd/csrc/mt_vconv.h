@@ -4,6 +4,8 @@
 // lrelu(x) next to x), so every operand byte goes global -> LDS by `global_load_lds_dwordx4` with no
 // VGPR round trip and no prologue transform (see mt_vconv.hip for the pipeline).
 #pragma once
+#include <type_traits>
+
 #include "mt_common.h"
 
 namespace mt {
@@ -31,6 +33,82 @@ enum : int {
                      // per tile from the producer's VE_GNSTATS partials (ResnetBlock1D block2 -> + res(x),
                      // model.py:777-790; replaces a separate gn_apply pass)
 };
+
+// Compile-time K-loop schedule (mt_vconv CTN / CTT kernels and mt_rbconv). Per loader wave and step s of a
+// tile of S = NCH * TAPS steps, in program order: [row pieces of chunk c + NXB - 1, spread over taps t < TX of chunk
+// c] [WPW weight pieces of step s + NW - 1] [NST epilogue stores on the tile's last step]. The epilogue's loads and
+// any store whose issue depends on the data (statistics outputs) are left out of the counts: operations left out
+// only make a wait stricter, and the epilogue's loads have completed before its stores (the compiler waits for them).
+template <int NCH, int TAPS, int NW, int NXB, int TX, int WPW, int XPW, int NST>
+struct VcSched {
+  static constexpr int S = NCH * TAPS;
+  static constexpr int md(int v) { return ((v % S) + S) % S; }
+  static constexpr int xr(int s) {
+    const int t = s % TAPS;
+    int n = 0;
+    if (t < TX)
+      for (int i = 0; i < XPW; ++i) n += (i * TX / XPW == t) ? 1 : 0;
+    return n;
+  }
+  static constexpr int ops(int s) { return xr(s) + WPW + (s == S - 1 ? NST : 0); }
+  static constexpr int after_w(int s) { return s == S - 1 ? NST : 0; }
+  // VMEM operations issued after the group (rows / weights) of step v, up to the wait at the top of step s
+  static constexpr int count(int v, bool rows, int s) {
+    int n = (rows ? WPW : 0) + after_w(md(v));
+    for (int u = v + 1; u < s; ++u) n += ops(md(u));
+    return n;
+  }
+  // the wait at the top of step s (s = -1: the prologue's) publishes step s + 1: its weights (staged at step
+  // s + 2 - NW) and, when it starts a chunk, that chunk's rows (their last pieces staged at step vx)
+  static constexpr int wait(int s) {
+    int n = count(s + 2 - NW, false, s);
+    if ((s + 1) % TAPS == 0) {
+      const int vx = ((s + 1) / TAPS - (NXB - 1)) * TAPS + TX - 1;
+      const int nx = count(vx, true, s);
+      n = n < nx ? n : nx;
+    }
+    return n;
+  }
+  static constexpr int v0 = (1 - NW) < (-(NXB - 1) * TAPS) ? (1 - NW) : (-(NXB - 1) * TAPS);
+  // The prologue stages only what tile 0 needs, in virtual-step order v0 .. -1 (rows of chunks >= 0, weights of
+  // steps >= 0; no stores): pops(v) operations at virtual step v. The first tile's waits whose data came from the
+  // prologue count those instead of a previous tile's (wait_first; equal to wait(s) elsewhere).
+  static constexpr int vfloor(int v) { return v >= 0 ? v / TAPS : -((-v + TAPS - 1) / TAPS); }
+  static constexpr int prows(int v) { return vfloor(v) + NXB - 1 >= 0 ? xr(md(v)) : 0; }
+  static constexpr int pw(int v) { return v + NW - 1 >= 0 ? WPW : 0; }
+  static constexpr int pops(int v) { return prows(v) + pw(v); }
+  static constexpr int count_first(int v, bool rows, int s) {
+    if (v >= 0) return count(v, rows, s);
+    int n = rows ? pw(v) : 0;
+    for (int u = v + 1; u < 0; ++u) n += pops(u);
+    for (int u = 0; u < s; ++u) n += ops(u);
+    return n;
+  }
+  static constexpr int wait_first(int s) {
+    int n = count_first(s + 2 - NW, false, s);
+    if ((s + 1) % TAPS == 0) {
+      const int vx = ((s + 1) / TAPS - (NXB - 1)) * TAPS + TX - 1;
+      const int nx = count_first(vx, true, s);
+      n = n < nx ? n : nx;
+    }
+    return n;
+  }
+};
+
+// compile-time loop: f(integral_constant<int, I>) for I in [I0, N)
+template <int I, int N, class F>
+__device__ __forceinline__ void vc_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    vc_for<I + 1, N>(f);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void vc_wait_vmcnt() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 struct VConvArgs {
   const bf16* x;      // [B][L][c0], already activated: channels [0, c0)
@@ -115,6 +193,10 @@ int launch_vconv(int ef, const VConvArgs& a, hipStream_t st);
 bool rbconv_handles(int ef, const VConvArgs& a);
 int launch_rbconv(int ef, const VConvArgs& a, int G, hipStream_t st);
 int rbconv_set(int enable);  // -> the previous setting
+// the compile-time K loop of the decoder's / upsamplers' convs (1, default) or the runtime-cursor loop (0); -> previous
+int vconv_set_ct(int enable);
+// the process-wide kernel selection above as one value (a key of the decoder's captured graphs)
+int vconv_path_id();
 // fp32 mode (VConvArgs::f32): [Mpad0][taps][cin_pad] fp32 -> [cin/32][taps][Mpad][32] fp32
 bool vconv_supported_f32(int cin, int cout, int k, int stride);
 size_t vconv_packed_bytes_f32(int cin, int cout, int k);

@@ -109,6 +109,10 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+#ifndef VC_CT_LOADERS
+#define VC_CT_LOADERS 8
+#endif
+
 template <int EF>
 constexpr int vc_npar() {  // per-channel LDS tables (MMAX floats each); VE_GNRES: gamma, beta + the GN table
   return 1 + ((EF & VE_LN) ? 1 : 0) + ((EF & VE_SNAKE) ? 2 : 0) + ((EF & VE_GNRES) ? 3 : 0);
@@ -117,7 +121,7 @@ constexpr int vc_npar() {  // per-channel LDS tables (MMAX floats each); VE_GNRE
 // F32: fp32 operands (the text encoder, whose duration path must be the reference's fp32 arithmetic): a 128-byte
 // LDS row holds 32 channels, one 16-byte fragment per lane feeds 4 exact-fp32 v_mfma_f32_16x16x4_f32 (mfma16), and
 // the epilogue stores fp32 in the accumulator layout (bias, ReLU, residual, mask only).
-template <int EF, int BMT, bool K1, int BNT = BN, bool F32 = false>
+template <int EF, int BMT, bool K1, int BNT = BN, bool F32 = false, int CTN = 0, int CTT = 0>
 __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   using TT = VT<BMT, K1, vc_npar<EF>(), BNT>;
   constexpr int BN = TT::TBN;
@@ -647,6 +651,20 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     __builtin_amdgcn_sched_group_barrier(0x008, NMF - NR, 0);
   };
 
+  // compile-time K loop (CTN > 0): tiles ti + 0 .. 2 of this workgroup, decoded once (past the last: the last, for
+  // the phantom prefetches), before any LDS-DMA is in flight (the compiler would wait for it before the LDS reads)
+  struct Tl { int b, n0, m0; };
+  auto dec = [&](int ti) {
+    Tl r;
+    tile_of(min(ti, nmine - 1), r.b, r.n0, r.m0);
+    return r;
+  };
+  Tl tq[3];
+  if constexpr (CTN > 0) {
+    tq[0] = dec(0);
+    tq[1] = dec(1);
+    tq[2] = dec(2);
+  }
   // ---- prologue: (the tables,) rows of chunks 0 .. NXB-2, weights of steps 0..2, K-slice 0 of step 0 ----
   if (tab_dma) {
     // 1 KiB per wave-instruction (lane-linear), instructions dealt round-robin over the waves; lanes past the
@@ -660,6 +678,139 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       glds16(src, smem + toff[ti] + part * 1024);
       ++issued;
     }
+  }
+  if constexpr (CTN > 0) {
+    // ================= compile-time K loop (CTN chunks x CTT taps per tile; see VcSched) =================
+    constexpr int TAPS = CTT, NCHC = CTN, SC = CTN * CTT;
+    constexpr int LW = VC_CT_LOADERS;                         // loader waves (one per SIMD when 4)
+    constexpr int WPW = (WSLOT / 1024) / LW, XPW = (XBUF / 1024) / LW;
+    static_assert(WPW * LW * 1024 == WSLOT && XPW * LW * 1024 == XBUF, "pieces per loader wave");
+    constexpr int TXA = (NXB - 1) * TAPS - 2 < 1 ? 1 : (NXB - 1) * TAPS - 2;
+    constexpr int TX = TXA < TAPS ? (TXA < XPW ? TXA : XPW) : (TAPS < XPW ? TAPS : XPW);
+    using SCH = VcSched<NCHC, TAPS, NWSLOT, NXB, TX, WPW, XPW, NST>;
+    const bool loader = wave < LW;
+    if (nch != NCHC || taps != TAPS) __builtin_trap();  // the host dispatches on (cin / 64, taps)
+    // tiles ti + 0 .. 2 of this workgroup, decoded once (past the last: the last, for the phantom prefetches)
+    int sb = 0, xbb = 0;  // ring slot / row buffer of the tile's step 0 / chunk 0 (0 when the period divides)
+    auto wslot = [&](int d) {  // ring slot of step d of the tile (d may pass the tile)
+      const int r = ((d % NWSLOT) + NWSLOT) % NWSLOT;
+      if constexpr (SC % NWSLOT == 0) return r;
+      const int v = sb + r;
+      return v >= NWSLOT ? v - NWSLOT : v;
+    };
+    auto xbuf_of = [&](int e) {  // row buffer of chunk e of the tile (e may pass the tile)
+      const int r = ((e % NXB) + NXB) % NXB;
+      if constexpr (NCHC % NXB == 0) return r;
+      const int v = xbb + r;
+      return v >= NXB ? v - NXB : v;
+    };
+    auto ct_w = [&](const Tl& tl, int c, int t, int slot) {  // a loader wave's WPW weight pieces of (c, t)
+      const char* base = reinterpret_cast<const char*>(a.w) + ((size_t)(c * TAPS + t) * a.Mpad + tl.m0) * 128;
+      // opaque LDS offset and per-step source offsets: a constant destination lets the compiler track the DMA and
+      // wait on it before every ds_read; hoisted per-step addresses would take hundreds of VGPRs
+      int so = slot * WSLOT + wave * WPW * 1024;
+      asm volatile("" : "+s"(so));
+#pragma unroll
+      for (int i = 0; i < WPW; ++i) {
+        const int r = 8 * (wave * WPW + i) + lrow;
+        int off = r * 128 + (lp ^ (r & 6)) * 16;
+        asm volatile("" : "+v"(off));
+        glds16(base + off, smem + so + i * 1024);
+      }
+    };
+    auto ct_x = [&](const Tl& tl, int c, int buf, int part) {  // a loader wave's row pieces `part` of chunk c
+      const int f0 = tl.n0 - a.pad;
+      const int Lx = rag ? rlv[tl.b] : L;
+      const bool lo = c * CHR < c0;
+      const int ldx = lo ? c0 : cin - c0;
+      const char* xb = lo ? reinterpret_cast<const char*>(a.x) + ((size_t)tl.b * L * c0 + c * CHR) * ES
+                          : reinterpret_cast<const char*>(a.x1) + ((size_t)tl.b * L * (cin - c0) + (c * CHR - c0)) * ES;
+      int xo = NWSLOT * WSLOT + buf * XBUF;
+      asm volatile("" : "+s"(xo));
+#pragma unroll
+      for (int i = 0; i < XPW; ++i) {
+        if (i * TX / XPW != part) continue;
+        const int j = wave + LW * i;
+        const int r = 8 * j + lrow;
+        const int q = lp ^ (r & 6);
+        const int f = f0 + r;
+        const bool ok = r < R && f >= 0 && f < Lx;
+        const char* src = ok ? xb + (size_t)f * ldx * ES + q * 16 : reinterpret_cast<const char*>(a.zero) + q * 16;
+        glds16(src, smem + xo + j * 1024);
+      }
+    };
+    auto rd = [&](Frag& F, int ks, int slot, int xbuf, int tap) {  // read_frag with per-step (opaque) bases
+      int lb = 0;
+      asm volatile("" : "+v"(lb));
+      const char* pa = smem + lb + slot * WSLOT + (wm * 64 + l16) * 128;
+      const int rb0 = lb + wn * WNC + l16 + tap * dil;
+      const int hb = rb0 & 6;
+      const char* pb = smem + NWSLOT * WSLOT + xbuf * XBUF + rb0 * 128;
+      const int oa = ((ks * 4 + g4) ^ ha) * 16, ob = ((ks * 4 + g4) ^ hb) * 16;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const FT*>(pa + f * 2048 + oa);
+#pragma unroll
+      for (int f = 0; f < FN; ++f) F.B[f] = *reinterpret_cast<const FT*>(pb + f * 2048 + ob);
+    };
+    // the staging ops of (relative) step v of the tile (v < 0: the prologue's virtual steps, which stage only the
+    // targets at or past tile 0)
+    auto stage_step = [&](auto vc, const Tl* tls) {
+      constexpr int v = decltype(vc)::value;
+      constexpr int sv = SCH::md(v), t = sv % TAPS;
+      if constexpr (t < TX) {
+        constexpr int g = SCH::vfloor(v) + NXB - 1;  // target chunk, relative to the tile of step 0
+        if constexpr (g >= 0) ct_x(tls[g / NCHC], g % NCHC, xbuf_of(g), t);
+      }
+      constexpr int q = v + NWSLOT - 1;  // the weight step staged at step v
+      if constexpr (q >= 0) ct_w(tls[q / SC], (q % SC) / TAPS, (q % SC) % TAPS, wslot(q));
+    };
+    static_assert((NCHC + NXB - 2) / NCHC <= 2 && (SC + NWSLOT - 2) / SC <= 2, "stage targets within 2 tiles ahead");
+    if (loader) {
+      vc_for<SCH::v0, 0>([&](auto vc) { stage_step(vc, tq); });
+      vc_wait_vmcnt<SCH::wait_first(-1)>();
+    }
+    raw_barrier();
+    Frag F0, F1;
+    rd(F0, 0, wslot(0), xbuf_of(0), 0);
+    for (int ti = 0; ti < nmine; ++ti) {
+      vc_for<0, SC>([&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        constexpr int c = s / TAPS, t = s % TAPS;
+        constexpr int s1 = s + 1, c1 = s1 / TAPS, t1 = s1 % TAPS;  // step s + 1 (chunk c1 may be the next tile's)
+        __builtin_amdgcn_sched_barrier(0);
+        if (loader) {
+          if constexpr (SCH::wait_first(s) == SCH::wait(s)) {
+            vc_wait_vmcnt<SCH::wait(s)>();
+          } else {
+            if (ti == 0) vc_wait_vmcnt<SCH::wait_first(s)>();
+            else vc_wait_vmcnt<SCH::wait(s)>();
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();
+        if constexpr (s == SC - 1 && (EF & (VE_RESID | VE_ACCUM | VE_LN | VE_MASK | VE_GNRES)) != 0) epi_loads(ti);
+        if (loader) stage_step(sc, tq);
+        rd(F1, 1, wslot(s), xbuf_of(c), t);
+        mma_slice(F0);
+        rd(F0, 0, wslot(s1), xbuf_of(c1), t1);
+        mma_slice(F1);
+        if constexpr (s == SC - 1) {
+          __builtin_amdgcn_sched_barrier(0);
+          epilogue(ti);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      });
+      if constexpr (SC % NWSLOT != 0) sb = wslot(SC);
+      if constexpr (NCHC % NXB != 0) xbb = xbuf_of(NCHC);
+      tq[0] = tq[1];
+      tq[1] = tq[2];
+      tq[2] = dec(ti + 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phantom prefetches land before the LDS is released
+    return;
   }
 #pragma unroll
   for (int i = 0; i < NXB - 1; ++i) stage_x();
@@ -984,6 +1135,47 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
 }
 
 
+// Compile-time K-loop variants (CTN chunks x CTT taps; VcSched): the decoder's convs and the upsamplers, each
+// (epilogue, tile) with the (C_in / 64, taps) pairs its launches have; other shapes run the runtime-cursor loop.
+// MT_VCONV_CT=0 in the environment or mt_vconv_set_ct(0): the runtime-cursor loop everywhere (A/B, tests: the two
+// are bit-identical, same tiles and MFMA order).
+static int g_ct = -1;
+static bool ct_on() {
+  if (g_ct < 0) {
+    const char* e = getenv("MT_VCONV_CT");
+    g_ct = e && e[0] == '0' ? 0 : 1;
+  }
+  return g_ct != 0;
+}
+int vconv_set_ct(int enable) {
+  const int prev = ct_on() ? 1 : 0;
+  g_ct = enable ? 1 : 0;
+  return prev;
+}
+int vconv_path_id() {
+  const int rb = rbconv_set(1);  // read the rbconv setting (and restore it)
+  rbconv_set(rb);
+  return (ct_on() ? 2 : 0) | rb;
+}
+template <int E, int BMV, bool K1V, int BNV>
+static void ct_try(const VConvArgs&, int, hipStream_t, bool&) {}
+template <int E, int BMV, bool K1V, int BNV, int N, int T, int... R>
+static void ct_try(const VConvArgs& a, int G, hipStream_t st, bool& done) {
+  if (a.cin / 64 == N && a.taps == T) {
+    hipLaunchKernelGGL((vconv_kernel<E, BMV, K1V, BNV, false, N, T>), dim3(G), dim3(NT), 0, st, a);
+    done = true;
+    return;
+  }
+  ct_try<E, BMV, K1V, BNV, R...>(a, G, st, done);
+}
+// launch vconv_kernel<E, BMV, K1V, BNV>, on its compile-time K loop when (C_in / 64, taps) is one of the pairs P
+template <int E, int BMV, bool K1V, int BNV, int... P>
+static void vlaunch(const VConvArgs& a, int G, hipStream_t st) {
+  bool done = false;
+  if (ct_on()) ct_try<E, BMV, K1V, BNV, P...>(a, G, st, done);
+  if (!done) hipLaunchKernelGGL((vconv_kernel<E, BMV, K1V, BNV>), dim3(G), dim3(NT), 0, st, a);
+}
+
 int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(a0.x && a0.w && a0.bias && a0.y && a0.zero && a0.trash, "vconv: null pointer");
   if (a0.f32) return launch_vconv_f32(ef, a0, st);
@@ -1122,6 +1314,25 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       else hipLaunchKernelGGL((vconv_kernel<E, 64, true>), dim3(G), dim3(NT), 0, st, a);                \
     }                                                                                                   \
     break;
+#define MT_VCASE_HCT(E)                                                                                \
+  case E:                                                                                              \
+    if (tf == 128) vlaunch<E, 128, false, 128, 3, 3, 4, 3, 8, 3, 8, 2>(a, G, st);                        \
+    else if (tf == 192) vlaunch<E, 128, false, 192, 3, 3, 4, 3, 8, 3, 8, 2>(a, G, st);                   \
+    else if (BM == 128) vlaunch<E, 128, false, BN, 3, 3, 4, 3, 8, 3, 8, 2>(a, G, st);                    \
+    else hipLaunchKernelGGL((vconv_kernel<E, 64, false, BN64>), dim3(G), dim3(NT), 0, st, a);          \
+    break;
+#define MT_VCASE1CT(E, ...)                                                                             \
+  case E:                                                                                               \
+    if (tf1 == 128) {                                                                                   \
+      if (BM == 128) vlaunch<E, 128, true, 128, __VA_ARGS__>(a, G, st);                                 \
+      else hipLaunchKernelGGL((vconv_kernel<E, 64, true, 128>), dim3(G), dim3(NT), 0, st, a);           \
+    } else if (tf1 == 192) {                                                                            \
+      vlaunch<E, 128, true, 192, __VA_ARGS__>(a, G, st);                                                \
+    } else {                                                                                            \
+      if (BM == 128) vlaunch<E, 128, true, BN, __VA_ARGS__>(a, G, st);                                  \
+      else hipLaunchKernelGGL((vconv_kernel<E, 64, true>), dim3(G), dim3(NT), 0, st, a);                \
+    }                                                                                                   \
+    break;
   if (!k1) {
     switch (ef) {
       MT_VCASE(VE_ACT)
@@ -1130,11 +1341,17 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE(VE_RESID | VE_ACCUM)
       MT_VCASE(VE_RESID | VE_DIV)
       MT_VCASE(VE_RESID | VE_ACCUM | VE_DIV)
-      MT_VCASE_H(VE_GNSTATS)
-      MT_VCASE_H(VE_MASK)
-      MT_VCASE(VE_DUAL)
+      MT_VCASE_HCT(VE_GNSTATS)
+      MT_VCASE_HCT(VE_MASK)
+      case VE_DUAL:  // the upsamplers (placed polyphase output)
+        if (BM == 128) vlaunch<VE_DUAL, 128, false, BN, 8, 2, 4, 2, 2, 2>(a, G, st);
+        else hipLaunchKernelGGL((vconv_kernel<VE_DUAL, 64, false, BN64>), dim3(G), dim3(NT), 0, st, a);
+        break;
       MT_VCASE(VE_RELU | VE_MASK)
-      MT_VCASE(VE_PMASK)
+      case VE_PMASK:  // the decoder's ConvTranspose up conv
+        if (BM == 128) vlaunch<VE_PMASK, 128, false, BN, 4, 2>(a, G, st);
+        else hipLaunchKernelGGL((vconv_kernel<VE_PMASK, 64, false, BN64>), dim3(G), dim3(NT), 0, st, a);
+        break;
       case VE_RESID | VE_MASK:
         if (bm64_128) hipLaunchKernelGGL((vconv_kernel<VE_RESID | VE_MASK, 64, false, 128>), dim3(G), dim3(NT), 0, st, a);
         else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<VE_RESID | VE_MASK, 128, false>), dim3(G), dim3(NT), 0, st, a);
@@ -1150,18 +1367,20 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE1(VE_LN)
       MT_VCASE1(VE_LN | VE_SNAKE)
       MT_VCASE1(VE_RESID)
-      MT_VCASE1(VE_RESID | VE_MASK)
-      MT_VCASE1(VE_RESID | VE_ROWSTATS)
-      MT_VCASE1(VE_RESID | VE_ROWSTATS | VE_GNRES)
-      MT_VCASE1(VE_LN | VE_LNP)
-      MT_VCASE1(VE_LN | VE_LNP | VE_SNAKE)
+      MT_VCASE1CT(VE_RESID | VE_MASK, 16, 1, 2, 1)
+      MT_VCASE1CT(VE_RESID | VE_ROWSTATS, 2, 1, 16, 1)
+      MT_VCASE1CT(VE_RESID | VE_ROWSTATS | VE_GNRES, 3, 1, 4, 1, 8, 1)
+      MT_VCASE1CT(VE_LN | VE_LNP, 4, 1)
+      MT_VCASE1CT(VE_LN | VE_LNP | VE_SNAKE, 4, 1)
       MT_VCASE1(0)
       default: set_error("vconv: 1x1 epilogue %d not compiled in", ef); return -1;
     }
   }
 #undef MT_VCASE
 #undef MT_VCASE_H
+#undef MT_VCASE_HCT
 #undef MT_VCASE1
+#undef MT_VCASE1CT
   MT_CHECK_HIP(hipGetLastError());
   if (probed) probe_end(site, st, flops, bytes);
   return 0;

@@ -89,6 +89,7 @@ SIGNATURES = {
     "mt_op_vconv": (c_int, [P, c_int, c_int, c_int, P, P, c_int, c_int, c_int, c_int, P, P, P, c_float, c_float,
                             P, c_int, P, c_size_t, P]),
     "mt_vconv_set_rbconv": (c_int, [c_int]),
+    "mt_vconv_set_ct": (c_int, [c_int]),
     "mt_op_attention": (c_int, [c_int, P, P, P, c_int, c_int, c_int, P]),
     "mt_probe_start": (c_int, [c_int, c_int]),
     "mt_probe_pause": (c_int, [c_int]),

@@ -579,6 +579,12 @@ def op_vconv(x_btc: torch.Tensor, W: torch.Tensor, bias: torch.Tensor, dil: int 
     return y, y2
 
 
+def set_vconv_ct(enable: bool) -> bool:
+    """mt_vconv's compile-time K loop for the decoder's / upsamplers' convs (True, default) or the runtime-cursor
+    loop; returns the previous setting (process-wide)"""
+    return bool(lib().mt_vconv_set_ct(int(bool(enable))))
+
+
 def set_rbconv(enable: bool) -> bool:
     """the HiFi-GAN wide-stage ResBlock convs on mt_rbconv (True, default) or the generic mt_vconv kernel; returns
     the previous setting (process-wide)"""

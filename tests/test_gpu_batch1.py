@@ -6,7 +6,7 @@ y_len % 4 != 0 leaves 1-3 padded frames, the reference's +3.4e38 fill (model.py:
 uniformly to them and the solver takes the query-independent path; y_len % 4 == 0 leaves none and the general
 Q.K^T path runs. The bench weights force 3 frames per token, so x_len 150 -> y_len 450 (padded)
 and x_len 152 -> y_len 456 (unpadded) select the two paths.
-Tolerances (SURVEY.md §8c): fp32 mel atol 2e-4 (CFM), waveform atol 1e-5 x the steps' growth -> 5e-5;
+Tolerances (SURVEY.md §8c): fp32 mel atol 2e-4 (CFM), waveform atol 1e-5 (measured 2.6e-6..3.3e-6 max |d|);
 bf16 rel-RMS 1e-2 on the normalised mel and on the denoised waveform.
 Reference: model.py:1264-1300, hifigan/models.py:181-197, hifigan/denoiser.py:62-68.
 """
@@ -83,7 +83,7 @@ def test_batch1_text_to_wav_vs_oracle(precision, n_ts, x_len):
         e_mel = (mel.cpu() - mel_o).abs().max().item()
         e_wav = (wav.cpu() - den_o).abs().max().item()
         print(f"B=1 fp32 n={n_ts} y_len={y_len} ({path}): mel max|d| {e_mel:.2e}, wav max|d| {e_wav:.2e}")
-        assert e_mel < 2e-4 and e_wav < 5e-5, (e_mel, e_wav)
+        assert e_mel < 2e-4 and e_wav < 1e-5, (e_mel, e_wav)  # SURVEY §8c atol 1e-5 (measured wav 2.6e-6..3.3e-6)
     else:
         e_mel = rel_rms((mel.cpu() - mean) / std, (mel_o - mean) / std)
         e_wav = rel_rms(wav.cpu(), den_o)
