@@ -238,7 +238,8 @@ def roofline_by_kernel(detail, frame_scale=1.0):
 
 def roofline(probe, default_workload=True, frame_scale=1.0, pmc_name="pmc_vconv.json"):
     """Dominant kernel family of the step: the LDS-DMA persistent implicit-GEMM convs that run every ResBlock
-    conv of HiFi-GAN (51 launches per step): per layer on mt_vconv, stage 1 and stage 2's k = 7 / 11 resblocks
+    conv of HiFi-GAN (51 launches per step): per layer on mt_rbconv (mt_vconv with MT_RBCONV=0), stage 1 and
+    stage 2's k = 7 / 11 resblocks
     (30 convs; C = 256/128 on B x 8/64 * T_y frames); as fused conv pairs, stage 2's k = 3 resblock on
     mt_vpair128 (3 launches) and stages 3-4 on mt_vpair / mt_vpair32 (2 x 9 launches, C = 64/32 on
     B x 128/256 * T_y frames; a pair launch is priced as its two convs); k = 3/7/11. Timed by HIP events recorded on

@@ -525,8 +525,11 @@ class MatchaTTS(nn.Module):
         est.packed(x.device)
         est._pk.trust_next((est.precision, str(x.device)))
         try:
-            y_max = int(y_lengths.max())                 # the reference's host sync (model.py:1278-1281)
-            rt.check_ids(oov)                            # nn.Embedding's IndexError (model.py:522), after it
+            # the reference's host sync (model.py:1278-1281), which also brings back the encoder's out-of-vocabulary
+            # flag (one device->host copy for both)
+            y_max, bad = torch.stack((y_lengths.max(), oov[0].to(torch.int64))).tolist()
+            if bad:
+                raise IndexError("index out of range in self (a token id of x lies outside [0, n_vocab))")
             t_pad = fix_len_compatibility(y_max)
             attn, mu_y, y_mask = rt.alignment(cum, y_lengths, t_pad, mu)
             z = self.decoder(mu_y, y_mask, n_timesteps, temperature, spks, cond=None, max_valid=y_max)

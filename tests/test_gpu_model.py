@@ -454,7 +454,9 @@ def test_launch_probe_times_vconv_launches():
     B, T = mel.shape[0], mel.shape[2]
     assert p["launches"] == 30 + 21 and p["ms"] > 0
     kinds = [d["kind"] for d in detail]
-    assert [kinds.count(k) for k in ("vconv", "vpair128", "vpair", "vpair32")] == [30, 3, 9, 9], kinds
+    # the 30 per-layer convs run mt_rbconv (the default) or mt_vconv (MT_RBCONV=0)
+    assert kinds.count("rbconv") + kinds.count("vconv") == 30, kinds
+    assert [kinds.count(k) for k in ("vpair128", "vpair", "vpair32")] == [3, 9, 9], kinds
     assert abs(sum(d["flops"] for d in detail) - p["flops"]) <= 1e-9 * p["flops"]
     assert abs(sum(d["ms"] for d in detail) - p["ms"]) <= 1e-3 * p["ms"]
     want = sum(2.0 * 6 * C * C * 21 * B * T * r for C, r in ((256, 8), (128, 64), (64, 128), (32, 256)))
