@@ -361,6 +361,10 @@ int mt_vconv_set_rbconv(int enable);
  * (C_in, taps) (1, the default; bit-identical results) or with the runtime-cursor loop (0). Process-wide; returns
  * the previous setting. */
 int mt_vconv_set_ct(int enable);
+/* The bf16 decoder's transformer FeedForward (LayerNorm, Linear 256 -> 1024, SnakeBeta, Linear 1024 -> 256, + x) as
+ * one fused launch whose 1024-wide intermediate stays on chip (1, the default; bit-identical results) or as two
+ * mt_vconv GEMM launches (0). Process-wide; returns the previous setting. */
+int mt_ffn_set(int enable);
 /* qkv [B][T][3*heads*64], mask [B][T] -> out [B][T][heads*64], reference mask semantics */
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                     void* stream);

@@ -4,6 +4,7 @@
 #include <new>
 
 #include "../../include/matcha_hip.h"
+#include "mt_ffn.h"
 #include "mt_model.h"
 #include "mt_vconv.h"
 #include "mt_probe.h"
@@ -357,6 +358,7 @@ size_t mt_op_vconv_workspace_bytes(int cin, int cout, int k) {
 }
 int mt_vconv_set_rbconv(int enable) { return mt::rbconv_set(enable); }
 int mt_vconv_set_ct(int enable) { return mt::vconv_set_ct(enable); }
+int mt_ffn_set(int enable) { return mt::ffn_set(enable); }
 int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const float* bias, int cout, int k, int dil,
                 int ef, const void* resid, void* y, void* y2, float slope, float div, const int32_t* lens, int pack,
                 void* ws, size_t ws_bytes, void* stream) {

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "mt_ffn.h"
 #include "mt_model.h"
 #include "mt_probe.h"
 #include "mt_vconv.h"
@@ -606,22 +607,47 @@ int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const fl
     if (t.qkv.vc && t.out.vc && t.ff1.vc && t.ff2.vc) {
       // bf16: the four GEMMs on mt_vconv's 1x1 pipeline; LayerNorm folded into the QKV / FF1 epilogues
       auto vargs = [&](const GemmW& g, const void* xin, void* y) { return this->vargs(g, P, w, xin, B, Tl, y); };
+      // ff(norm3(x)) + x: one fused launch (mt_ffn: the 1024-wide intermediate stays on chip), or FF1 + FF2 on
+      // mt_vconv (MT_FFN=0); LayerNorm statistics: the per-slab partials in w.lnp either way
+      auto feedforward = [&]() -> int {
+        if (ffn_on() && t.ff1.cin == C && t.ff1.cout == TE && t.ff2.cin == TE && t.ff2.cout == C) {
+          FfnArgs f{};
+          f.x = (bf16*)x;
+          f.frames = B * Tl;
+          f.ln_stats = w.lnp;
+          f.ln_eps = 1e-5f;
+          f.w1 = (const bf16*)(P + t.ff1.v_off);
+          f.b1 = (const float*)(P + t.ff1.b_off);
+          f.wsum = (const float*)(P + t.wsf_off);
+          f.alpha = (const float*)(P + t.snake_off);
+          f.ibeta = (const float*)(P + t.snake_off) + TE;
+          f.w2 = (const bf16*)(P + t.ff2.v_off);
+          f.b2 = (const float*)(P + t.ff2.b_off);
+          f.emask = mask_out ? mask : nullptr;
+          f.zero = (const bf16*)(P + zero_off);
+          f.trash = (bf16*)w.trash;
+          return launch_ffn(f, st);
+        }
+        VConvArgs f1 = vargs(t.ff1, x, w.ff);
+        f1.ln_stats = w.lnp;
+        f1.wsum = (const float*)(P + t.wsf_off);
+        f1.snake_alpha = (const float*)(P + t.snake_off);
+        f1.snake_ibeta = (const float*)(P + t.snake_off) + TE;
+        int rc1;
+        if ((rc1 = launch_vconv(VE_LN | VE_LNP | VE_SNAKE, f1, st))) return rc1;
+        VConvArgs f2 = vargs(t.ff2, w.ff, x);
+        f2.resid = (const bf16*)x;
+        // the chain's last block hands its consumers (convs reading x * mask) a masked copy in place
+        f2.emask = mask;
+        return launch_vconv(mask_out ? VE_RESID | VE_MASK : VE_RESID, f2, st);
+      };
       if (uni && heads == 2 && t.qkv.cout == 384 && t.qkv.cin == C && t.out.cout == C && t.out.cin == 128) {
         // every utterance is padded at this level: attention is query-independent (model.py:697) -> x += o_b
         // with o_b from a masked mean and two GEMVs; no QKV GEMM, no attention, no per-frame out-projection
         if ((rc = launch_uniform_attention(x, mask, B, Tl, P + t.qkv.v_off, t.qkv.cout, (const float*)(P + t.qkv.b_off),
                                            P + t.out.v_off, (const float*)(P + t.out.b_off), w.upart, w.lnp, st)))
           return rc;
-        VConvArgs f1 = vargs(t.ff1, x, w.ff);
-        f1.ln_stats = w.lnp;
-        f1.wsum = (const float*)(P + t.wsf_off);
-        f1.snake_alpha = (const float*)(P + t.snake_off);
-        f1.snake_ibeta = (const float*)(P + t.snake_off) + TE;
-        if ((rc = launch_vconv(VE_LN | VE_LNP | VE_SNAKE, f1, st))) return rc;
-        VConvArgs f2 = vargs(t.ff2, w.ff, x);
-        f2.resid = (const bf16*)x;
-        f2.emask = mask;
-        return launch_vconv(mask_out ? VE_RESID | VE_MASK : VE_RESID, f2, st);
+        return feedforward();
       }
       // LayerNorm statistics: per-slab partials from the producing conv's epilogue (VE_ROWSTATS) when it
       // wrote them, else a row-statistics pass
@@ -639,17 +665,7 @@ int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const fl
       o.resid = (const bf16*)x;
       o.row_out = w.lnp;
       if ((rc = launch_vconv(VE_RESID | VE_ROWSTATS, o, st))) return rc;
-      VConvArgs f1 = vargs(t.ff1, x, w.ff);
-      f1.ln_stats = w.lnp;
-      f1.wsum = (const float*)(P + t.wsf_off);
-      f1.snake_alpha = (const float*)(P + t.snake_off);
-      f1.snake_ibeta = (const float*)(P + t.snake_off) + TE;
-      if ((rc = launch_vconv(VE_LN | VE_LNP | VE_SNAKE, f1, st))) return rc;
-      VConvArgs f2 = vargs(t.ff2, w.ff, x);
-      f2.resid = (const bf16*)x;
-      // the chain's last block hands its consumers (convs reading x * mask) a masked copy in place
-      f2.emask = mask;
-      return launch_vconv(mask_out ? VE_RESID | VE_MASK : VE_RESID, f2, st);
+      return feedforward();
     }
   }
   if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
@@ -874,7 +890,7 @@ int Decoder::chain_graph(const char* P, const Work& w, const TimeSched& ts, int 
   GraphCache& gc = *gcache;
   // kpath: the process-wide kernel selection (compile-time K loops on / off): a graph holds the kernels it captured
   const GraphCache::Entry key{P, ws, B, T, S, n_steps, solver, w.uni0, w.uni1, vconv, gnres, uniform_attn,
-                              vconv_path_id(), nullptr};
+                              vconv_path_id() | (ffn_on() << 3), nullptr};
   for (size_t i = 0; i < gc.entries.size(); ++i) {
     const GraphCache::Entry& e = gc.entries[i];
     if (e.P == key.P && e.ws == key.ws && e.B == key.B && e.T == key.T && e.S == key.S && e.n_steps == key.n_steps &&

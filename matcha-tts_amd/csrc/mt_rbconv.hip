@@ -28,6 +28,10 @@
 #include "mt_ragged.h"
 #include "mt_vconv.h"
 
+#ifndef RB_EXP
+#define RB_EXP 0  // timing experiments (tools/exp_build.sh): bits drop parts of the epilogue (wrong results)
+#endif
+
 namespace mt {
 
 namespace {
@@ -201,6 +205,10 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
       for (int fn = 0; fn < RFN; ++fn) {
         const int n = min(tl.n0 + wn * RWNC + fn * 16 + l16, L - 1);
         const size_t o = (rowbase + n) * C + tl.m0 + ch16 + fp * 32;
+        if constexpr ((RB_EXP & 1) != 0) {  // timing experiment 1: no epilogue operand loads (wrong results)
+          rv[fp][fn] = yv[fp][fn] = u32x4{(uint32_t)o, 0u, 0u, 0u};
+          continue;
+        }
         if constexpr ((EF & VE_RESID) != 0) rv[fp][fn] = *reinterpret_cast<const u32x4*>(a.resid + o);
         if constexpr ((EF & VE_ACCUM) != 0) yv[fp][fn] = *reinterpret_cast<const u32x4*>(a.y + o);
       }
@@ -249,7 +257,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
         const bool ok = real && n < L;
         const size_t o = ((size_t)tl.b * L + n) * C + tl.m0 + ch16 + fp * 32;
         *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
-        if constexpr ((EF & VE_DUAL) != 0) {
+        if constexpr ((EF & VE_DUAL) != 0 && (RB_EXP & 2) == 0) {  // timing experiment 2: no y2 store
           swap16(o2[0][0], o2[1][0]);
           swap16(o2[0][1], o2[1][1]);
           *reinterpret_cast<u32x4*>(ok ? a.y2 + o : a.trash + 8 * lane) = u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]};

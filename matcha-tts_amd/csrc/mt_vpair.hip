@@ -30,6 +30,10 @@
 #include "mt_probe.h"
 #include "mt_vpair.h"
 
+#ifndef VPAIR_EXP
+#define VPAIR_EXP 0  // timing experiments (tools/exp_build.sh): bits drop parts of the pair kernels' work
+#endif
+
 namespace mt {
 
 namespace {
@@ -166,6 +170,13 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   // K-slice ks of tap u of a step: A = the slot's 4 row fragments of that tap, B = FN frame fragments at
   // rows rb + 16 fn of `src`
   auto read_frag = [&](Frag& F, int ks, int slot, int u, const char* src, int rb0) {
+    if constexpr ((VPAIR_EXP & 32) != 0) {  // timing experiment 32: no fragment reads (wrong results)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) asm volatile("" : "+v"(F.A[f]));
+#pragma unroll
+      for (int f = 0; f < FN; ++f) asm volatile("" : "+v"(F.B[f]));
+      return;
+    }
     const char* pa = smem + W_OFF + slot * WSLOT + u * TAPW + l16 * 128 + (((ks * 4 + g4) ^ ha) * 16);
 #pragma unroll
     for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048);
@@ -182,6 +193,10 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn)
+        if constexpr ((VPAIR_EXP & 8) != 0) {  // timing experiment: no MFMAs (wrong results)
+          asm volatile("" ::"v"(F.A[fm]), "v"(F.B[fn]));
+          if (decltype(first)::value) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else
         acc[fm][fn] = mfma16(F.A[fm], F.B[fn], decltype(first)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn]);
     constexpr int NR = 4 + FN, NMF = 4 * FN;
 #pragma unroll
@@ -194,13 +209,15 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   // one conv over `src`: ns steps of two taps (row of tap t for this lane's first fragment: rb0 + t * tstride);
   // slices in order (tap, K-slice), each read under the previous slice's MFMAs, the next step's first slice
   // under this step's last
-  Frag F0, F1;
+  Frag F0 = {}, F1 = {};
   int s = 0;
   auto conv = [&](const char* src, int rb0, int tstride, auto&& at_first_step) {
     auto step = [&](int m, auto first) {
       const bool more = m + 1 < ns, two = 2 * m + 1 < k;
-      vp_wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);  // this step's weights and the next step's
-      vp_barrier();
+      if constexpr ((VPAIR_EXP & 16) == 0) {  // timing experiment 16: no per-step wait / barrier (wrong results)
+        vp_wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);  // this step's weights and the next step's
+        vp_barrier();
+      }
       if (s + NWS - 1 < S) stage_w(s + NWS - 1);
       const int sl = s % NWS, t0 = 2 * m;
       if constexpr (decltype(first)::value) {
@@ -250,7 +267,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       }
     vp_barrier();
 #pragma unroll
-    for (int i = 0; i < XROWS * 8 / NT; ++i) {
+    for (int i = 0; i < ((VPAIR_EXP & 1) ? 0 : XROWS * 8 / NT); ++i) {
       const int e = tid + i * NT;
       u32x4 v = *reinterpret_cast<const u32x4*>(smem + e * 16);
 #pragma unroll
@@ -292,6 +309,11 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
           const int fm = 2 * fp + h;
           const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + fm * 16 + 4 * g4);
           // lrelu(acc + b1) rounded once to bf16 (conv2's operand); zero outside [0, L)
+          if constexpr ((VPAIR_EXP & 2) != 0) {  // timing experiment: no epilogue arithmetic (wrong results)
+            o[h][0] = __float_as_uint(acc[fm][fn][0] + acc[fm][fn][1]);
+            o[h][1] = __float_as_uint(acc[fm][fn][2] + acc[fm][fn][3]);
+            continue;
+          }
           o[h][0] = ok ? lrelu_pk_f(f32x2{acc[fm][fn][0], acc[fm][fn][1]} + f32x2{b4[0], b4[1]}, a.slope) : 0u;
           o[h][1] = ok ? lrelu_pk_f(f32x2{acc[fm][fn][2], acc[fm][fn][3]} + f32x2{b4[2], b4[3]}, a.slope) : 0u;
         }
@@ -338,6 +360,10 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
           // round(acc + b2 + x [+ xs] [/ nk]) and its lrelu, two channels per packed op
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
+            if constexpr ((VPAIR_EXP & 4) != 0) {  // timing experiment: no epilogue arithmetic (wrong results)
+              o1[h][u] = o2[h][u] = __float_as_uint(acc[fm][fn][2 * u] + acc[fm][fn][2 * u + 1]) ^ rr[u] ^ yy[u];
+              continue;
+            }
             f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]} + f32x2{b4[2 * u], b4[2 * u + 1]};
             v = v + unpk_bf16(rr[u]);
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
@@ -476,6 +502,10 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn)
+        if constexpr ((VPAIR_EXP & 8) != 0) {  // timing experiment: no MFMAs (wrong results)
+          asm volatile("" ::"v"(F.A[fm]), "v"(F.B[fn]));
+          if (decltype(first)::value) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else
         acc[fm][fn] = mfma16(F.A[fm], F.B[fn], decltype(first)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn]);
     constexpr int NR = 4 + FN, NMF = 4 * FN;
 #pragma unroll
@@ -539,7 +569,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
         rv[fp][fn] = *reinterpret_cast<const u32x4*>(xs + r * 128 + ((q ^ (r & 6)) * 16));
       }
     vp_barrier();
-    for (int e = tid; e < K3_XBUF / 16; e += NT) {
+    for (int e = tid; e < ((VPAIR_EXP & 1) ? 0 : K3_XBUF / 16); e += NT) {
       u32x4 v = *reinterpret_cast<const u32x4*>(xs + e * 16);
 #pragma unroll
       for (int w = 0; w < 4; ++w) v[w] = lrelu_pk(v[w], a.slope);
@@ -561,6 +591,11 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
           const int fm = 2 * fp + h;
           const f32x4 b4 = *reinterpret_cast<const f32x4*>(par + fm * 16 + 4 * g4);
           // lrelu(acc + b1) rounded once to bf16 (conv2's operand); zero outside [0, L)
+          if constexpr ((VPAIR_EXP & 2) != 0) {  // timing experiment: no epilogue arithmetic (wrong results)
+            o[h][0] = __float_as_uint(acc[fm][fn][0] + acc[fm][fn][1]);
+            o[h][1] = __float_as_uint(acc[fm][fn][2] + acc[fm][fn][3]);
+            continue;
+          }
           o[h][0] = ok ? lrelu_pk_f(f32x2{acc[fm][fn][0], acc[fm][fn][1]} + f32x2{b4[0], b4[1]}, a.slope) : 0u;
           o[h][1] = ok ? lrelu_pk_f(f32x2{acc[fm][fn][2], acc[fm][fn][3]} + f32x2{b4[2], b4[3]}, a.slope) : 0u;
         }
@@ -605,6 +640,10 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
           // round(acc + b2 + x [+ xs] [/ nk]) and its lrelu, two channels per packed op
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
+            if constexpr ((VPAIR_EXP & 4) != 0) {  // timing experiment: no epilogue arithmetic (wrong results)
+              o1[h][u] = o2[h][u] = __float_as_uint(acc[fm][fn][2 * u] + acc[fm][fn][2 * u + 1]) ^ rr[u] ^ yy[u];
+              continue;
+            }
             f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]} + f32x2{b4[2 * u], b4[2 * u + 1]};
             v = v + unpk_bf16(rr[u]);
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;

@@ -585,6 +585,13 @@ def set_vconv_ct(enable: bool) -> bool:
     return bool(lib().mt_vconv_set_ct(int(bool(enable))))
 
 
+def set_ffn(mode) -> int:
+    """the bf16 decoder's transformer FeedForward as one fused launch (True / 1, default: mt_ffn's serial schedule;
+    2: its FF1 epilogues overlapped with FF2 steps) or as two mt_vconv GEMMs (False / 0); returns the previous
+    setting (process-wide)"""
+    return int(lib().mt_ffn_set(int(mode)))
+
+
 def set_rbconv(enable: bool) -> bool:
     """the HiFi-GAN wide-stage ResBlock convs on mt_rbconv (True, default) or the generic mt_vconv kernel; returns
     the previous setting (process-wide)"""

@@ -9,6 +9,10 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "matcha-tts_amd"))
 import torch  # noqa: E402
 
+if os.environ.get("MT_LIB"):  # timing experiments: another build of the library
+    import matcha_hip._lib as _L  # noqa: E402
+    _L.LIB_PATH = os.environ["MT_LIB"]
+
 from matcha_hip import runtime as rt  # noqa: E402
 
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 5
