@@ -365,6 +365,8 @@ int mt_vconv_set_ct(int enable);
  * one fused launch whose 1024-wide intermediate stays on chip (1, the default; bit-identical results) or as two
  * mt_vconv GEMM launches (0). Process-wide; returns the previous setting. */
 int mt_ffn_set(int enable);
+/* ... on decoder levels of at least `frames` frames (B x T at that level; default 32768); returns the previous value */
+int mt_ffn_set_min_frames(int frames);
 /* qkv [B][T][3*heads*64], mask [B][T] -> out [B][T][heads*64], reference mask semantics */
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                     void* stream);

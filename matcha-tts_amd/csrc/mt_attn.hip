@@ -494,9 +494,9 @@ __global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ 
 #pragma unroll
       for (int o = 1; o < 8; o <<= 1) sm += __shfl_xor(sm, o, 64);
       const float mu = sm * (1.f / 64.f);
-      float q = 0.f;
+      float q = 0.f;  // fused multiply-adds spelled out: mt_ffn's fold of this pass computes the same bits
 #pragma unroll
-      for (int e = 0; e < 8; ++e) q += (v[e] - mu) * (v[e] - mu);
+      for (int e = 0; e < 8; ++e) q = __builtin_fmaf(v[e] - mu, v[e] - mu, q);
 #pragma unroll
       for (int o = 1; o < 8; o <<= 1) q += __shfl_xor(q, o, 64);
       if ((cl & 7) == 0) *reinterpret_cast<float2*>(row_out + 2 * (((size_t)b * T + j) * 4 + (cl >> 3))) = float2{mu, q};
@@ -508,9 +508,12 @@ __global__ __launch_bounds__(256) void attn_uni_apply_kernel(bf16* __restrict__ 
 int uniform_part_slices(int T) { return std::max(1, std::min(UNI_PSMAX, T / 24)); }
 size_t uniform_attention_floats(int B) { return (size_t)B * (UNI_PSMAX * UNI_PART + UNI_C); }
 
+const float* uniform_attention_ovec(const float* part, int B) { return part + (size_t)B * UNI_PSMAX * UNI_PART; }
+
 int launch_uniform_attention(void* x, const float* mask, int B, int T, const void* wqkv, int mq, const float* bqkv,
-                             const void* wout, const float* bout, float* part, float* row_out, hipStream_t st) {
-  MT_REQUIRE(x && mask && wqkv && bqkv && wout && bout && part && row_out && B > 0 && T > 0 && mq == 384,
+                             const void* wout, const float* bout, float* part, float* row_out, hipStream_t st,
+                             bool apply) {
+  MT_REQUIRE(x && mask && wqkv && bqkv && wout && bout && part && (row_out || !apply) && B > 0 && T > 0 && mq == 384,
              "uniform attention: arguments (C = 256, 2 heads x 64)");
   const int SP = uniform_part_slices(T);
   float* ovec = part + (size_t)B * UNI_PSMAX * UNI_PART;  // [B][256] after the slice sums (uniform_attention_floats)
@@ -518,7 +521,8 @@ int launch_uniform_attention(void* x, const float* mask, int B, int T, const voi
   hipLaunchKernelGGL(attn_uni_part_kernel, dim3(SP, B), dim3(256), 0, st, (const bf16*)x, mask, T, part, xr);
   hipLaunchKernelGGL(attn_uni_vec_kernel, dim3(B), dim3(256), 0, st, SP, (const float*)part, (const bf16*)wqkv, mq,
                      bqkv, (const bf16*)wout, bout, ovec);
-  hipLaunchKernelGGL(attn_uni_apply_kernel, dim3(SP, B), dim3(256), 0, st, (bf16*)x, T, (const float*)ovec, row_out,
+  if (apply)
+    hipLaunchKernelGGL(attn_uni_apply_kernel, dim3(SP, B), dim3(256), 0, st, (bf16*)x, T, (const float*)ovec, row_out,
                      xr);
   MT_CHECK_HIP(hipGetLastError());
   return 0;

@@ -99,6 +99,9 @@ __device__ __forceinline__ float lrelu_f(float x, float slope) { return x > 0.f 
 // v_cvt_pk_bf16_f32 (RNE) per word, lrelu as max(x, slope * x) — equal to x > 0 ? x : slope * x for every non-NaN
 // x when 0 <= slope <= 1 (files using it build with -mno-amdgpu-ieee so the max needs no NaN canonicalize)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// a * b + c with one rounding per lane (v_pk_fma_f32). Epilogues that two kernels must compute to the same bits spell
+// their multiply-adds out with it: left to -ffp-contract the compiler fuses them differently per code shape.
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_bf16(f32x2 v) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));

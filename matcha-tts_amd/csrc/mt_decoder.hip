@@ -609,9 +609,13 @@ int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const fl
       auto vargs = [&](const GemmW& g, const void* xin, void* y) { return this->vargs(g, P, w, xin, B, Tl, y); };
       // ff(norm3(x)) + x: one fused launch (mt_ffn: the 1024-wide intermediate stays on chip), or FF1 + FF2 on
       // mt_vconv (MT_FFN=0); LayerNorm statistics: the per-slab partials in w.lnp either way
-      auto feedforward = [&]() -> int {
-        if (ffn_on() && t.ff1.cin == C && t.ff1.cout == TE && t.ff2.cin == TE && t.ff2.cout == C) {
+      const bool fused_ff = ffn_on() && B * Tl >= ffn_min_frames() && t.ff1.cin == C && t.ff1.cout == TE && t.ff2.cin == TE && t.ff2.cout == C;
+      // ovec: the uniform attention's o_b, added by the fused kernel itself (its x += o_b launch skipped)
+      auto feedforward = [&](const float* ovec) -> int {
+        if (fused_ff) {
           FfnArgs f{};
+          f.ovec = ovec;
+          f.T = Tl;
           f.x = (bf16*)x;
           f.frames = B * Tl;
           f.ln_stats = w.lnp;
@@ -645,9 +649,10 @@ int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const fl
         // every utterance is padded at this level: attention is query-independent (model.py:697) -> x += o_b
         // with o_b from a masked mean and two GEMVs; no QKV GEMM, no attention, no per-frame out-projection
         if ((rc = launch_uniform_attention(x, mask, B, Tl, P + t.qkv.v_off, t.qkv.cout, (const float*)(P + t.qkv.b_off),
-                                           P + t.out.v_off, (const float*)(P + t.out.b_off), w.upart, w.lnp, st)))
+                                           P + t.out.v_off, (const float*)(P + t.out.b_off), w.upart, w.lnp, st,
+                                           !fused_ff)))
           return rc;
-        return feedforward();
+        return feedforward(fused_ff ? uniform_attention_ovec(w.upart, B) : nullptr);
       }
       // LayerNorm statistics: per-slab partials from the producing conv's epilogue (VE_ROWSTATS) when it
       // wrote them, else a row-statistics pass
@@ -665,7 +670,7 @@ int Decoder::tblock(const char* P, const Work& w, const TB& t, void* x, const fl
       o.resid = (const bf16*)x;
       o.row_out = w.lnp;
       if ((rc = launch_vconv(VE_RESID | VE_ROWSTATS, o, st))) return rc;
-      return feedforward();
+      return feedforward(nullptr);
     }
   }
   if ((rc = rowstats(dtype, x, B * Tl, C, 1e-5f, w.lns, st))) return rc;
@@ -890,7 +895,7 @@ int Decoder::chain_graph(const char* P, const Work& w, const TimeSched& ts, int 
   GraphCache& gc = *gcache;
   // kpath: the process-wide kernel selection (compile-time K loops on / off): a graph holds the kernels it captured
   const GraphCache::Entry key{P, ws, B, T, S, n_steps, solver, w.uni0, w.uni1, vconv, gnres, uniform_attn,
-                              vconv_path_id() | (ffn_on() << 3), nullptr};
+                              vconv_path_id() | (ffn_on() << 3) | (std::min(ffn_min_frames(), 1 << 25) << 5), nullptr};
   for (size_t i = 0; i < gc.entries.size(); ++i) {
     const GraphCache::Entry& e = gc.entries[i];
     if (e.P == key.P && e.ws == key.ws && e.B == key.B && e.T == key.T && e.S == key.S && e.n_steps == key.n_steps &&

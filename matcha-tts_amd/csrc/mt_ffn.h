@@ -18,6 +18,11 @@ struct FfnArgs {
   const bf16* w2;         // mt_vconv 1x1 image of ff.net.2: [16][256][64]
   const float* b2;        // [256]
   const float* emask;     // [frames] or null: y *= mask (the chain's last block hands out a masked copy)
+  // the query-independent attention's output (mt_attn.hip, launch_uniform_attention with apply = false): when set,
+  // the tile's rows are first updated x = bf16(x + ovec[utterance]) in LDS and the LayerNorm partials computed there
+  // (attn_uni_apply_kernel's arithmetic; ln_stats unused)
+  const float* ovec;      // [B][256] or null
+  int T;                  // frames per utterance (ovec's utterance of frame f: f / T)
   const bf16* zero;       // >= 128 zero bytes
   bf16* trash;            // >= 1 KiB writable
 };
@@ -27,5 +32,9 @@ struct FfnArgs {
 int launch_ffn(const FfnArgs& a, hipStream_t st);
 int ffn_set(int enable);  // -> the previous setting
 int ffn_on();
+// the fused kernel runs on levels of at least this many frames (B * T; default 32768 = one 128-frame tile per CU,
+// MT_FFN_MIN in the environment): below a full round of tiles its latency-bound tiles lose to the two GEMMs
+int ffn_min_frames();
+int ffn_set_min_frames(int frames);  // -> the previous setting
 
 }  // namespace mt

@@ -67,7 +67,7 @@ __device__ __forceinline__ void ff_for(F&& f) {
   }
 }
 
-template <bool MASK, bool OVL>
+template <bool MASK, bool OVL, bool UNI>
 __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[FLDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -146,9 +146,11 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
 #pragma unroll
     for (int fn = 0; fn < 2; ++fn) {
       const int f = min(n0 + wn * 32 + fn * 16 + l16, NF - 1);
-      const f32x4* pp = reinterpret_cast<const f32x4*>(a.ln_stats + 8 * (size_t)f);
-      lnr[fn][0] = pp[0];
-      lnr[fn][1] = pp[1];
+      if constexpr (!UNI) {
+        const f32x4* pp = reinterpret_cast<const f32x4*>(a.ln_stats + 8 * (size_t)f);
+        lnr[fn][0] = pp[0];
+        lnr[fn][1] = pp[1];
+      }
       mkr[fn] = MASK ? a.emask[f] : 1.f;
     }
   };
@@ -210,12 +212,13 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
           const f32x4 ib4 = *reinterpret_cast<const f32x4*>(tb + 3 * FE + m);
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
+            // mt_vconv's VE_LN | VE_SNAKE packed epilogue, its multiply-adds spelled out the same way (fma2)
             f32x2 v = f32x2{acc1[fm][fn][2 * u], acc1[fm][fn][2 * u + 1]};
-            v = (v - lns[fn].x * f32x2{ws4[2 * u], ws4[2 * u + 1]}) * lns[fn].y;
-            v = v + f32x2{bias4[2 * u], bias4[2 * u + 1]};
+            v = fma2(f32x2{-lns[fn].x, -lns[fn].x}, f32x2{ws4[2 * u], ws4[2 * u + 1]}, v);
+            v = fma2(v, f32x2{lns[fn].y, lns[fn].y}, f32x2{bias4[2 * u], bias4[2 * u + 1]});
             const f32x2 arg = v * f32x2{al4[2 * u], al4[2 * u + 1]};
             const f32x2 sn = f32x2{__sinf(arg.x), __sinf(arg.y)};
-            v = v + f32x2{ib4[2 * u], ib4[2 * u + 1]} * (sn * sn);
+            v = fma2(f32x2{ib4[2 * u], ib4[2 * u + 1]}, sn * sn, v);
             o[u] = pk_bf16(v);
           }
         }
@@ -242,6 +245,54 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
       for (int fn = 0; fn < 2; ++fn) acc1[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  // a tile's first step, after its barrier (the rows have landed): the LayerNorm statistics of its frames. UNI: first
+  // x = bf16(x + o_b) in place and the per-slab (mean, M2) into h's space (free until chunk 0's FF1 epilogue),
+  // with attn_uni_apply_kernel's arithmetic (mt_attn.hip), then a barrier
+  auto tile_start = [&](int n0) __attribute__((always_inline)) {
+    if constexpr (UNI) {
+      float* st = reinterpret_cast<float*>(smem + H_OFF);
+#pragma unroll 2
+      for (int i = 0; i < FBN * 32 / FNT; ++i) {  // 2 at a time: their o_b loads in flight together, few registers
+        const int task = tid + FNT * i;
+        const int r = task >> 5, cl = task & 31, slab = cl >> 3, q = cl & 7;
+        const int f = min(n0 + r, NF - 1);
+        const float* ob = a.ovec + (size_t)(f / a.T) * FC + slab * 64 + q * 8;
+        const f32x4 o0 = *reinterpret_cast<const f32x4*>(ob), o1 = *reinterpret_cast<const f32x4*>(ob + 4);
+        char* px = smem + XR_OFF + slab * FCHUNK + r * 128 + ((q ^ (r & 6)) * 16);
+        u32x4 w = *reinterpret_cast<const u32x4*>(px);
+        const float obv[8] = {o0[0], o0[1], o0[2], o0[3], o1[0], o1[1], o1[2], o1[3]};
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bf16 lo = (bf16)(__uint_as_float(w[e] << 16) + obv[2 * e]);
+          const bf16 hi = (bf16)(__uint_as_float(w[e] & 0xffff0000u) + obv[2 * e + 1]);
+          v[2 * e] = (float)lo;
+          v[2 * e + 1] = (float)hi;
+          w[e] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+        }
+        *reinterpret_cast<u32x4*>(px) = w;
+        float sm = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) sm += __shfl_xor(sm, o, 64);
+        const float mu = sm * (1.f / 64.f);
+        float q2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) q2 = __builtin_fmaf(v[e] - mu, v[e] - mu, q2);  // as attn_uni_apply_kernel
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) q2 += __shfl_xor(q2, o, 64);
+        if (q == 0) *reinterpret_cast<float2*>(st + 8 * r + 2 * slab) = float2{mu, q2};
+      }
+      ff_barrier();
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn) {
+        const int r = wn * 32 + fn * 16 + l16;
+        lnr[fn][0] = *reinterpret_cast<const f32x4*>(st + 8 * r);
+        lnr[fn][1] = *reinterpret_cast<const f32x4*>(st + 8 * r + 4);
+      }
+    }
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn) lns[fn] = ln_merge4(lnr[fn][0], lnr[fn][1], a.ln_eps);
   };
   auto ff1_epilogue = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
@@ -299,6 +350,7 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
   // that barrier); FF2(b+1) reads it three barriers later. h_0 (P) and h_7 (E, one extra barrier) are stored
   // unoverlapped. Same per-element operations and accumulation order as the serial schedule.
   u32x4 hreg[4];
+  int cur_n0 = 0;  // the OVL schedule's current tile
   // one step: U = 0..3 FF1 x chunk U, 4..7 FF2 (h chunk (U-4)>>1, output half (U-4)&1) of chunk j; the weights of step
   // s + 2 are (j2, U2); PF: prefetch the next step's first K-slice (U1: its kind); EG: the overlapped epilogue group
   // (-1: none) of chunk je; HW: store hreg into h after the barrier (XB: then one more barrier)
@@ -311,10 +363,7 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     vc_wait_vmcnt<0>();
     ff_barrier();
-    if constexpr (FI) {
-#pragma unroll
-      for (int fn = 0; fn < 2; ++fn) lns[fn] = ln_merge4(lnr[fn][0], lnr[fn][1], a.ln_eps);
-    }
+    if constexpr (FI) tile_start(cur_n0);
     issue_w(j2, U2, slot2);
     if constexpr (HW) {
 #pragma unroll
@@ -348,6 +397,7 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
     (void)F1r;
     for (int ti = 0; ti < nmine; ++ti) {
       const int n0 = (t0 + ti * gx) * FBN;
+      cur_n0 = n0;
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch)
 #pragma unroll
@@ -465,10 +515,7 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
         __builtin_amdgcn_sched_barrier(0);
         vc_wait_vmcnt<0>();
         ff_barrier();
-        if (u == 0 && j == 0) {
-#pragma unroll
-          for (int fn = 0; fn < 2; ++fn) lns[fn] = ln_merge4(lnr[fn][0], lnr[fn][1], a.ln_eps);
-        }
+        if (u == 0 && j == 0) tile_start(n0);
         // weights of step s + 2 into the slot of step s - 1 (every wave's reads of it ended before this barrier)
         if constexpr (u + 2 < 8) issue_w(j, u + 2, slot2);
         else issue_w(j + 1 < 8 ? j + 1 : 0, u + 2 - 8, slot2);  // the next chunk's (or the next tile's) steps
@@ -514,7 +561,7 @@ int g_ffn = -1;
 int ffn_knob() {
   if (g_ffn < 0) {
     const char* e = getenv("MT_FFN");
-    g_ffn = e && e[0] == '1' ? 1 : e && e[0] == '2' ? 2 : 0;  // off until validated on the GPU
+    g_ffn = e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
   }
   return g_ffn;
 }
@@ -537,15 +584,35 @@ int ffn_set(int enable) {  // 0 off, 1 serial schedule, 2 overlapped FF1 epilogu
 }
 int ffn_on() { return ffn_knob(); }
 
+namespace {
+int g_ffn_min = -1;
+}
+int ffn_min_frames() {
+  if (g_ffn_min < 0) {
+    const char* e = getenv("MT_FFN_MIN");
+    g_ffn_min = e ? std::max(0, atoi(e)) : 32768;
+  }
+  return g_ffn_min;
+}
+int ffn_set_min_frames(int frames) {
+  const int prev = ffn_min_frames();
+  g_ffn_min = std::max(0, frames);
+  return prev;
+}
+
 int launch_ffn(const FfnArgs& a, hipStream_t st) {
-  MT_REQUIRE(a.x && a.ln_stats && a.w1 && a.b1 && a.wsum && a.alpha && a.ibeta && a.w2 && a.b2 && a.zero && a.trash &&
+  MT_REQUIRE(a.x && (a.ln_stats || a.ovec) && a.w1 && a.b1 && a.wsum && a.alpha && a.ibeta && a.w2 && a.b2 && a.zero && a.trash &&
                  a.frames > 0,
              "ffn: null argument / empty");
   const int ntiles = (a.frames + FBN - 1) / FBN;
   const int G = std::min(ntiles, ffn_cus());
+  MT_REQUIRE(!a.ovec || a.T > 0, "ffn: ovec needs T");
   const bool ovl = ffn_knob() == 2;
-  void (*kern)(FfnArgs) = a.emask ? (ovl ? ffn_kernel<true, true> : ffn_kernel<true, false>)
-                                  : (ovl ? ffn_kernel<false, true> : ffn_kernel<false, false>);
+  void (*kern)(FfnArgs) =
+      a.ovec ? (a.emask ? (ovl ? ffn_kernel<true, true, true> : ffn_kernel<true, false, true>)
+                        : (ovl ? ffn_kernel<false, true, true> : ffn_kernel<false, false, true>))
+             : (a.emask ? (ovl ? ffn_kernel<true, true, false> : ffn_kernel<true, false, false>)
+                        : (ovl ? ffn_kernel<false, true, false> : ffn_kernel<false, false, false>));
   hipLaunchKernelGGL(kern, dim3(G), dim3(FNT), 0, st, a);
   MT_CHECK_HIP(hipGetLastError());
   return 0;

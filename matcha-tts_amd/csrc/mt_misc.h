@@ -75,8 +75,12 @@ size_t attention_part_bytes(int B, int T, int heads);
 constexpr int UNI_PSMAX = 32;  // most masked-sum slices per utterance (the workspace holds B x 32 x 260 floats)
 int uniform_part_slices(int T);
 size_t uniform_attention_floats(int B);  // workspace of launch_uniform_attention's `part`: slice sums + o_b
+// apply = false: the first two launches only; o_b ([B][256] floats) is left at uniform_attention_ovec(part, B) for a
+// consumer that adds it itself (mt_ffn)
 int launch_uniform_attention(void* x, const float* mask, int B, int T, const void* wqkv, int mq, const float* bqkv,
-                             const void* wout, const float* bout, float* part, float* row_out, hipStream_t st);
+                             const void* wout, const float* bout, float* part, float* row_out, hipStream_t st,
+                             bool apply = true);
+const float* uniform_attention_ovec(const float* part, int B);
 
 // the XCD-aligned block order of the decoder's streaming kernels (mt_common.h xcd_chunk; MT_XCD_TILES=0 turns it
 // and mt_vconv's XCD-major tile walk off)

@@ -167,6 +167,7 @@ struct VConvArgs {
 // LayerNorm (mean, rstd) of a 256-channel frame from its 4 slab partials (mean_i, M2_i), 64 values each,
 // packed (m0, q0, m1, q1), (m2, q2, m3, q3): Chan's merge, var = M2 / 256
 __device__ __forceinline__ float2 ln_merge4(f32x4 p01, f32x4 p23, float eps) {
+#pragma clang fp contract(off)  // the same bits at every call site (mt_vconv's LN epilogues, mt_ffn)
   const float mean = 0.25f * ((p01[0] + p01[2]) + (p23[0] + p23[2]));
   const float d0 = p01[0] - mean, d1 = p01[2] - mean, d2 = p23[0] - mean, d3 = p23[2] - mean;
   const float m2 = (p01[1] + p01[3]) + (p23[1] + p23[3]) + 64.f * ((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));

@@ -459,13 +459,15 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
             // same operations in the same order as the scalar path below
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
+              // (v - mean * wsum) * rstd + bias [+ ibeta * sin(alpha * v)^2], multiply-adds spelled out (fma2: mt_ffn
+              // computes the same bits)
               f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]};
-              v = (v - lns[fn].x * f32x2{ws4[2 * u], ws4[2 * u + 1]}) * lns[fn].y;
-              v = v + f32x2{bias4[2 * u], bias4[2 * u + 1]};
+              v = fma2(f32x2{-lns[fn].x, -lns[fn].x}, f32x2{ws4[2 * u], ws4[2 * u + 1]}, v);
+              v = fma2(v, f32x2{lns[fn].y, lns[fn].y}, f32x2{bias4[2 * u], bias4[2 * u + 1]});
               if constexpr ((EF & VE_SNAKE) != 0) {
                 const f32x2 arg = v * f32x2{al4[2 * u], al4[2 * u + 1]};
                 const f32x2 sn = f32x2{__sinf(arg.x), __sinf(arg.y)};
-                v = v + f32x2{ib4[2 * u], ib4[2 * u + 1]} * (sn * sn);
+                v = fma2(f32x2{ib4[2 * u], ib4[2 * u + 1]}, sn * sn, v);
               }
               o1[h][u] = pk_bf16(v);
               o2[h][u] = 0u;

@@ -592,6 +592,12 @@ def set_ffn(mode) -> int:
     return int(lib().mt_ffn_set(int(mode)))
 
 
+def set_ffn_min_frames(frames: int) -> int:
+    """the fused FeedForward only on decoder levels of at least `frames` frames (B x T; default 32768); returns the
+    previous value (process-wide)"""
+    return int(lib().mt_ffn_set_min_frames(int(frames)))
+
+
 def set_rbconv(enable: bool) -> bool:
     """the HiFi-GAN wide-stage ResBlock convs on mt_rbconv (True, default) or the generic mt_vconv kernel; returns
     the previous setting (process-wide)"""

@@ -21,6 +21,7 @@ def _run(models, x, xl, mode):
     from matcha_hip import runtime as rt
     m, g, den, _, _ = models
     prev = rt.set_ffn(mode)
+    prev_min = rt.set_ffn_min_frames(0)  # every level, whatever its size
     try:
         torch.manual_seed(7)  # the same CFM noise z for both runs (synthesize draws it with torch.randn_like)
         with torch.inference_mode():
@@ -28,6 +29,7 @@ def _run(models, x, xl, mode):
         torch.cuda.synchronize()
     finally:
         rt.set_ffn(prev)
+        rt.set_ffn_min_frames(prev_min)
     return mel.cpu(), yl.cpu(), wav.cpu()
 
 
@@ -61,6 +63,7 @@ def test_fused_feedforward_replaces_the_gemm_pair():
     counts = {}
     for fused in (True, False):
         prev = rt.set_ffn(fused)
+        prev_min = rt.set_ffn_min_frames(0)
         try:
             with torch.inference_mode():
                 rt.vconv_log_start(20000)
@@ -69,6 +72,7 @@ def test_fused_feedforward_replaces_the_gemm_pair():
                 recs = rt.vconv_log_stop(20000)
         finally:
             rt.set_ffn(prev)
+            rt.set_ffn_min_frames(prev_min)
         counts[fused] = (sum(1 for r in recs if r["ef"] == FF1), sum(1 for r in recs if r["cin"] == 1024))
     assert counts[True] == (0, 0), counts
     assert counts[False] == (60, 60), counts

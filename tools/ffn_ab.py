@@ -32,6 +32,7 @@ lens = torch.randint(T * 2 // 3, T - 4, (B,), generator=gen)
 mask = (torch.arange(T)[None, :] < lens[:, None]).float()[:, None, :].to(dev)
 ymax = int(lens.max())
 lib = L_.lib()
+rt.set_ffn_min_frames(int(os.environ.get("FFN_MIN", "0")))  # default here: every level fused (the library's: 32768)
 ws = torch.empty(lib.mt_cfm_workspace_bytes(eng.h, B, T, 10, L_.SOLVER_EULER), dtype=torch.uint8, device=dev)
 st = torch.cuda.current_stream(dev)
 
