@@ -362,8 +362,8 @@ int mt_vconv_set_rbconv(int enable);
  * the previous setting. */
 int mt_vconv_set_ct(int enable);
 /* The bf16 decoder's transformer FeedForward (LayerNorm, Linear 256 -> 1024, SnakeBeta, Linear 1024 -> 256, + x) as
- * one fused launch whose 1024-wide intermediate stays on chip (1, the default; bit-identical results) or as two
- * mt_vconv GEMM launches (0). Process-wide; returns the previous setting. */
+ * one fused launch whose 1024-wide intermediate stays on chip (3, the default; 1 / 2 other schedules of the same
+ * kernel; bit-identical results) or as two mt_vconv GEMM launches (0). Process-wide; returns the previous setting. */
 int mt_ffn_set(int enable);
 /* ... on decoder levels of at least `frames` frames (B x T at that level; default 32768); returns the previous value */
 int mt_ffn_set_min_frames(int frames);

@@ -67,7 +67,7 @@ __device__ __forceinline__ void ff_for(F&& f) {
   }
 }
 
-template <bool MASK, bool OVL, bool UNI>
+template <bool MASK, bool OVL, bool UNI, bool PFB = false>
 __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[FLDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -170,6 +170,24 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
     const int o = ((ks * 4 + g4) ^ (l16 & 6)) * 16;
 #pragma unroll
     for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048 + o);
+#pragma unroll
+    for (int f = 0; f < 2; ++f) F.B[f] = *reinterpret_cast<const bf16x8*>(pb + f * 2048 + o);
+  };
+  // the two halves of read_frag (PFB: the next step's frame fragments are read at this step's end, its weight
+  // fragments after its barrier, so a step's wait needs only its own weights: two steps of DMA cover)
+  auto read_A = [&](Frag& F, int ks, int slot) __attribute__((always_inline)) {
+    int la = 0;
+    asm volatile("" : "+v"(la));
+    const char* pa = smem + W_OFF + slot * FWSLOT + (wm * 64 + l16) * 128 + la;
+    const int o = ((ks * 4 + g4) ^ (l16 & 6)) * 16;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048 + o);
+  };
+  auto read_B = [&](Frag& F, int ks, int boff) __attribute__((always_inline)) {
+    int lb = 0;
+    asm volatile("" : "+v"(lb));
+    const char* pb = smem + boff + (wn * 32 + l16) * 128 + lb;
+    const int o = ((ks * 4 + g4) ^ (l16 & 6)) * 16;
 #pragma unroll
     for (int f = 0; f < 2; ++f) F.B[f] = *reinterpret_cast<const bf16x8*>(pb + f * 2048 + o);
   };
@@ -513,7 +531,12 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
         // the wait publishes this step's weights AND the next one's (its first K-slice is read at this step's end;
         // issued one step ago); at a tile's first step also the tile's rows and per-frame operands (everything)
         __builtin_amdgcn_sched_barrier(0);
-        vc_wait_vmcnt<0>();
+        if constexpr (PFB) {
+          if (u == 0 && j == 0) vc_wait_vmcnt<0>();
+          else vc_wait_vmcnt<2>();  // this step's weights (issued two steps ago); the next step's may be in flight
+        } else {
+          vc_wait_vmcnt<0>();
+        }
         ff_barrier();
         if (u == 0 && j == 0) tile_start(n0);
         // weights of step s + 2 into the slot of step s - 1 (every wave's reads of it ended before this barrier)
@@ -521,7 +544,12 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
         else issue_w(j + 1 < 8 ? j + 1 : 0, u + 2 - 8, slot2);  // the next chunk's (or the next tile's) steps
         constexpr int boff = u < 4 ? XR_OFF + u * FCHUNK : H_OFF + ((u - 4) >> 1) * FCHUNK;
         // step 0 of a tile and FF2's first step (h_j was written after the previous step): no prefetched slice
-        if (u == 4 || (u == 0 && j == 0)) read_frag(F0, 0, slot, boff);
+        if constexpr (PFB) {
+          read_A(F0, 0, slot);
+          if (u == 4 || (u == 0 && j == 0)) read_B(F0, 0, boff);
+        } else {
+          if (u == 4 || (u == 0 && j == 0)) read_frag(F0, 0, slot, boff);
+        }
         read_frag(F1, 1, slot, boff);
         if constexpr (u < 4) mma(acc1, F0, NV0{});
         else mma(acc2[(u - 4) & 1], F0, NV0{});
@@ -529,9 +557,13 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
         // step and at the tile end
         if constexpr (u != 3 && u != 7) {
           constexpr int boff1 = (u + 1) < 4 ? XR_OFF + (u + 1) * FCHUNK : H_OFF + (((u + 1) - 4) >> 1) * FCHUNK;
-          read_frag(F0, 0, slot1, boff1);
+          if constexpr (PFB) read_B(F0, 0, boff1);
+          else read_frag(F0, 0, slot1, boff1);
         } else if constexpr (u == 7) {
-          if (j < 7) read_frag(F0, 0, slot1, XR_OFF);
+          if (j < 7) {
+            if constexpr (PFB) read_B(F0, 0, XR_OFF);
+            else read_frag(F0, 0, slot1, XR_OFF);
+          }
         }
         if constexpr (u < 4) mma(acc1, F1, NV0{});
         else mma(acc2[(u - 4) & 1], F1, NV0{});
@@ -561,7 +593,7 @@ int g_ffn = -1;
 int ffn_knob() {
   if (g_ffn < 0) {
     const char* e = getenv("MT_FFN");
-    g_ffn = e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
+    g_ffn = e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : 3;
   }
   return g_ffn;
 }
@@ -577,9 +609,9 @@ int ffn_cus() {
 }
 }  // namespace
 
-int ffn_set(int enable) {  // 0 off, 1 serial schedule, 2 overlapped FF1 epilogues
+int ffn_set(int enable) {  // 0 off, 1 serial schedule, 2 overlapped FF1 epilogues, 3 serial + frame-only prefetch
   const int prev = ffn_knob();
-  g_ffn = enable < 0 ? 0 : enable > 2 ? 1 : enable;
+  g_ffn = enable < 0 ? 0 : enable > 3 ? 1 : enable;
   return prev;
 }
 int ffn_on() { return ffn_knob(); }
@@ -607,12 +639,17 @@ int launch_ffn(const FfnArgs& a, hipStream_t st) {
   const int ntiles = (a.frames + FBN - 1) / FBN;
   const int G = std::min(ntiles, ffn_cus());
   MT_REQUIRE(!a.ovec || a.T > 0, "ffn: ovec needs T");
-  const bool ovl = ffn_knob() == 2;
-  void (*kern)(FfnArgs) =
-      a.ovec ? (a.emask ? (ovl ? ffn_kernel<true, true, true> : ffn_kernel<true, false, true>)
-                        : (ovl ? ffn_kernel<false, true, true> : ffn_kernel<false, false, true>))
-             : (a.emask ? (ovl ? ffn_kernel<true, true, false> : ffn_kernel<true, false, false>)
-                        : (ovl ? ffn_kernel<false, true, false> : ffn_kernel<false, false, false>));
+  const int mode = ffn_knob();  // 1 serial, 2 overlapped FF1 epilogues, 3 serial with frame-only prefetch
+  void (*kern)(FfnArgs);
+  if (mode == 2)
+    kern = a.ovec ? (a.emask ? ffn_kernel<true, true, true> : ffn_kernel<false, true, true>)
+                  : (a.emask ? ffn_kernel<true, true, false> : ffn_kernel<false, true, false>);
+  else if (mode == 3)
+    kern = a.ovec ? (a.emask ? ffn_kernel<true, false, true, true> : ffn_kernel<false, false, true, true>)
+                  : (a.emask ? ffn_kernel<true, false, false, true> : ffn_kernel<false, false, false, true>);
+  else  // 1 (3 is the default: the frame fragments prefetched, two steps of weight-DMA cover)
+    kern = a.ovec ? (a.emask ? ffn_kernel<true, false, true> : ffn_kernel<false, false, true>)
+                  : (a.emask ? ffn_kernel<true, false, false> : ffn_kernel<false, false, false>);
   hipLaunchKernelGGL(kern, dim3(G), dim3(FNT), 0, st, a);
   MT_CHECK_HIP(hipGetLastError());
   return 0;

@@ -586,9 +586,9 @@ def set_vconv_ct(enable: bool) -> bool:
 
 
 def set_ffn(mode) -> int:
-    """the bf16 decoder's transformer FeedForward as one fused launch (True / 1, default: mt_ffn's serial schedule;
-    2: its FF1 epilogues overlapped with FF2 steps) or as two mt_vconv GEMMs (False / 0); returns the previous
-    setting (process-wide)"""
+    """the bf16 decoder's transformer FeedForward as one fused launch (mt_ffn; 3, the default: serial schedule with the
+    frame fragments prefetched; 1: serial, weight and frame fragments prefetched; 2: FF1 epilogues overlapped with FF2
+    steps) or as two mt_vconv GEMMs (False / 0); returns the previous setting (process-wide)"""
     return int(lib().mt_ffn_set(int(mode)))
 
 

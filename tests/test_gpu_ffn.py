@@ -44,7 +44,7 @@ def test_fused_feedforward_bit_identical(B, general):
         x = x[:, : int(xl[0])] * (torch.arange(int(xl[0]))[None] < xl[:, None])
     x, xl = x.to(DEV), xl.to(DEV)
     b = _run(models, x, xl, 0)
-    for mode in (1, 2):  # the serial schedule and the overlapped FF1 epilogues
+    for mode in (1, 2, 3):  # the serial schedule, the overlapped FF1 epilogues, frame-only prefetch
         a = _run(models, x, xl, mode)
         assert torch.equal(a[1], b[1])
         assert torch.equal(a[0], b[0]), (mode, (a[0] - b[0]).abs().max())

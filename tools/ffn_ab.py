@@ -43,8 +43,8 @@ def solve(out):
                                       ctypes.c_void_p(st.cuda_stream)), "solve")
 
 
-MODES = (1, 2, 0)  # mt_ffn serial, mt_ffn overlapped epilogues, the two mt_vconv launches
-NAME = {1: "fused", 2: "fused+overlap", 0: "two-launch"}
+MODES = (1, 3, 2, 0)  # mt_ffn serial, serial + frame-only prefetch, overlapped epilogues; the two mt_vconv launches
+NAME = {1: "fused", 3: "fused+pfb", 2: "fused+overlap", 0: "two-launch"}
 outs = {k: torch.empty_like(mu) for k in MODES}
 res = {k: [] for k in MODES}
 for r in range(ROUNDS):
@@ -62,6 +62,6 @@ rt.set_ffn(1)
 for fused in MODES:
     v = sorted(res[fused])
     print(f"{NAME[fused]}: median {v[len(v) // 2]:.3f} ms per solve (B={B}, T={T}; {[round(x, 3) for x in v]})", flush=True)
-for k in (1, 2):
+for k in (1, 3, 2):
     print(f"{NAME[k]} vs two-launch bit-identical: {torch.equal(outs[k], outs[0])}, "
           f"max |diff| {(outs[k] - outs[0]).abs().max().item():.3e}")
