@@ -361,11 +361,15 @@ int mt_vconv_set_rbconv(int enable);
  * (C_in, taps) (1, the default; bit-identical results) or with the runtime-cursor loop (0). Process-wide; returns
  * the previous setting. */
 int mt_vconv_set_ct(int enable);
+/* The stage 1-2 ResBlock conv1s (mt_rbconv) read the raw chain state and apply its leaky ReLU to their staged rows in
+ * LDS, so the producing convs store no activated copy (1, the default; bit-identical results), or read an activated
+ * copy the producers store (0). Process-wide; returns the previous setting. */
+int mt_vconv_set_actin(int enable);
 /* The bf16 decoder's transformer FeedForward (LayerNorm, Linear 256 -> 1024, SnakeBeta, Linear 1024 -> 256, + x) as
  * one fused launch whose 1024-wide intermediate stays on chip (3, the default; 1 / 2 other schedules of the same
  * kernel; bit-identical results) or as two mt_vconv GEMM launches (0). Process-wide; returns the previous setting. */
 int mt_ffn_set(int enable);
-/* ... on decoder levels of at least `frames` frames (B x T at that level; default 32768); returns the previous value */
+/* ... on decoder levels of at least `frames` frames (B x T at that level; default 16384); returns the previous value */
 int mt_ffn_set_min_frames(int frames);
 /* qkv [B][T][3*heads*64], mask [B][T] -> out [B][T][heads*64], reference mask semantics */
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,

@@ -622,7 +622,7 @@ int g_ffn_min = -1;
 int ffn_min_frames() {
   if (g_ffn_min < 0) {
     const char* e = getenv("MT_FFN_MIN");
-    g_ffn_min = e ? std::max(0, atoi(e)) : 32768;
+    g_ffn_min = e ? std::max(0, atoi(e)) : 16384;
   }
   return g_ffn_min;
 }

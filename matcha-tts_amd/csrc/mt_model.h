@@ -255,6 +255,8 @@ struct Vocoder {
   template <class E>
   int forward_t(const char* P, const float* mel, int B, int T, float* wav, char* ws, hipStream_t st,
                 const int* lens) const;
+  // the per-layer resblocks of wide stage i read the raw chain state (mt_rbconv VE_ACTIN): no activated copies
+  bool stage_actin(int i, int B, int L, const int* lens) const;
   int stage_vconv(const char* P, int i, int B, int L, const char* X, const char* XA, char* XS, char* Tb, char* R,
                   char* RA, char* trash, bool act_out, hipStream_t st, const int* lens = nullptr) const;
   // upsampler i runs on vconv: its input lrelu(xs) is written by the producer (conv_pre / stage i-1)

@@ -88,7 +88,8 @@ __device__ __forceinline__ void rb_for(F&& f) {
 template <int EF, int C, int K, int LW>
 __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   constexpr int WPW = RbStage<LW>::WPW, XPW = RbStage<LW>::XPW, TX = rb_tx<K, LW>();
-  using SCH = VcSched<C / 64, K, RNW, 2, TX, WPW, XPW, rb_nst<EF>()>;
+  constexpr bool ACTIN = (EF & VE_ACTIN) != 0;
+  using SCH = VcSched<C / 64, K, RNW, 2, TX, WPW, XPW, rb_nst<EF>(), ACTIN ? 2 : 1>;
   constexpr int NCH = C / 64, S = NCH * K;        // chunks, steps per tile
   static_assert(NCH % 2 == 0 && S % 2 == 0, "schedule period (row buffers alternate per chunk)");
   constexpr int NTM = C / RBM;                    // row tiles
@@ -288,6 +289,20 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
 #pragma unroll
     for (int f = 0; f < RFN; ++f) F.B[f] = *reinterpret_cast<const bf16x8*>(pb + f * 2048 + ob);
   };
+  // VE_ACTIN: lrelu over a landed row buffer in place (the chain state as stored -> the conv's input), each thread
+  // its own 16-byte units, so no wave waits for another; the next barrier publishes the result
+  auto act_pass = [&](int buf) __attribute__((always_inline)) {
+    int bo = RX_OFF + buf * RXBUF;
+    asm volatile("" : "+v"(bo));
+#pragma unroll
+    for (int i = 0; i < RXBUF / 16 / RNT; ++i) {
+      char* p = smem + bo + (tid + RNT * i) * 16;
+      u32x4 v = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) v[w] = lrelu_pk(v[w], a.slope);
+      *reinterpret_cast<u32x4*>(p) = v;
+    }
+  };
   auto mma_slice = [&](const Frag& F) {
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm)
@@ -310,9 +325,14 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
       if constexpr (t < TX && SCH::vfloor(v) + 1 >= 0) issue_x(cur, 0, 0, std::integral_constant<int, t>{});
       if constexpr (v + RNW - 1 >= 0) issue_w(cur, (v + RNW - 1) / K, (v + RNW - 1) % K, v + RNW - 1);
     });
-    vc_wait_vmcnt<SCH::wait_first(-1)>();
+    if constexpr (ACTIN) vc_wait_vmcnt<0>();  // chunk 0's rows too (RL = 2: no step before step 0 publishes them)
+    else vc_wait_vmcnt<SCH::wait_first(-1)>();
   }
   rb_barrier();
+  if constexpr (ACTIN) {
+    act_pass(0);
+    rb_barrier();
+  }
   Frag F0, F1;
   read_frag(F0, 0, 0, 0, 0);
 
@@ -352,6 +372,9 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
         else issue_w(nxt, c3, t3, slot3);
       }
       read_frag(F1, 1, slot, xbuf, t);
+      // VE_ACTIN: the next chunk's rows were published by this step's wait (RL = 2); activated here, published by the
+      // next step's barrier, read from the step after it (or by this step's successor's prefetch)
+      if constexpr (ACTIN && t == K - 2) act_pass((c + 1) % 2);
       mma_slice(F0);
       read_frag(F0, 0, slot1, xbuf1, t1);
       mma_slice(F1);
@@ -392,6 +415,22 @@ int rb_knob() {
 }
 }  // namespace
 
+namespace {
+int g_actin = -1;
+}
+int rbconv_actin_on() {
+  if (g_actin < 0) {
+    const char* e = getenv("MT_ACTIN");
+    g_actin = e && e[0] == '0' ? 0 : 1;
+  }
+  return g_actin && rb_knob();
+}
+int rbconv_actin_set(int enable) {
+  const int prev = rbconv_actin_on() ? 1 : 0;
+  g_actin = enable ? 1 : 0;
+  return prev;
+}
+
 int rbconv_set(int enable) {
   const int prev = rb_knob();
   g_rb = enable ? 1 : 0;
@@ -402,7 +441,7 @@ int rbconv_set(int enable) {
 // (not placed), one source, the ResBlock epilogues, halo <= 64 rows
 bool rbconv_handles(int ef, const VConvArgs& a) {
   if (!rb_knob()) return false;
-  const bool eps = ef == VE_ACT || ef == (VE_RESID | VE_DUAL) || ef == VE_RESID || ef == (VE_RESID | VE_ACCUM) ||
+  const bool eps = ef == VE_ACT || ef == (VE_ACT | VE_ACTIN) || ef == (VE_RESID | VE_DUAL) || ef == VE_RESID || ef == (VE_RESID | VE_ACCUM) ||
                    ef == (VE_RESID | VE_ACCUM | VE_DIV) || ef == (VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL);
   return eps && !a.f32 && (a.cin == 128 || a.cin == 256) && a.M == a.cin && a.Mpad == a.M && a.c0 == a.cin &&
          (a.taps == 3 || a.taps == 7 || a.taps == 11) && a.dil >= 1 && RBN + (a.taps - 1) * a.dil <= RXROWS &&
@@ -426,6 +465,7 @@ int launch_rbconv(int ef, const VConvArgs& a, int G, hipStream_t st) {
     break;
   switch (ef) {
     MT_RB_EF(VE_ACT)
+    MT_RB_EF(VE_ACT | VE_ACTIN)
     MT_RB_EF(VE_RESID | VE_DUAL)
     MT_RB_EF(VE_RESID)
     MT_RB_EF(VE_RESID | VE_ACCUM)

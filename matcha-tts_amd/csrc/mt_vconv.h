@@ -28,18 +28,23 @@ enum : int {
   VE_LNP = 1024,     // with VE_LN: ln_stats holds VE_ROWSTATS partials [frames][cin/64] instead of (mean, rstd)
   VE_RELU = 2048,    // max(v, 0) after the bias (text-encoder FFN, model.py:119-130)
   VE_PMASK = 4096,   // placed output: v * emask[output frame], frame = element / mask_div
+  VE_ACTIN = 16384,  // mt_rbconv, with VE_ACT: the input is the RAW chain state; lrelu is applied to each staged row
+                     // chunk in LDS (a pass over the chunk one step before its first use), so no producer writes an
+                     // activated copy (VE_DUAL) for it
   VE_GNRES = 8192,   // 1x1 only, with VE_RESID: the residual is the RAW input of a GroupNorm(M/32) + Mish + mask,
                      // applied here: resid := bf16(mish(GN(resid)) * emask[frame]) with the statistics merged
                      // per tile from the producer's VE_GNSTATS partials (ResnetBlock1D block2 -> + res(x),
                      // model.py:777-790; replaces a separate gn_apply pass)
 };
 
-// Compile-time K-loop schedule (mt_vconv CTN / CTT kernels and mt_rbconv). Per loader wave and step s of a
+// Compile-time K-loop schedule (mt_vconv CTN / CTT kernels and mt_rbconv). RL: the rows of a chunk are published
+// RL steps before its first step (1; 2 for mt_rbconv's VE_ACTIN, whose in-LDS pass over them runs in between). Per
+// loader wave and step s of a
 // tile of S = NCH * TAPS steps, in program order: [row pieces of chunk c + NXB - 1, spread over taps t < TX of chunk
 // c] [WPW weight pieces of step s + NW - 1] [NST epilogue stores on the tile's last step]. The epilogue's loads and
 // any store whose issue depends on the data (statistics outputs) are left out of the counts: operations left out
 // only make a wait stricter, and the epilogue's loads have completed before its stores (the compiler waits for them).
-template <int NCH, int TAPS, int NW, int NXB, int TX, int WPW, int XPW, int NST>
+template <int NCH, int TAPS, int NW, int NXB, int TX, int WPW, int XPW, int NST, int RL = 1>
 struct VcSched {
   static constexpr int S = NCH * TAPS;
   static constexpr int md(int v) { return ((v % S) + S) % S; }
@@ -62,8 +67,8 @@ struct VcSched {
   // s + 2 - NW) and, when it starts a chunk, that chunk's rows (their last pieces staged at step vx)
   static constexpr int wait(int s) {
     int n = count(s + 2 - NW, false, s);
-    if ((s + 1) % TAPS == 0) {
-      const int vx = ((s + 1) / TAPS - (NXB - 1)) * TAPS + TX - 1;
+    if ((s + RL) % TAPS == 0) {
+      const int vx = ((s + RL) / TAPS - (NXB - 1)) * TAPS + TX - 1;
       const int nx = count(vx, true, s);
       n = n < nx ? n : nx;
     }
@@ -86,8 +91,8 @@ struct VcSched {
   }
   static constexpr int wait_first(int s) {
     int n = count_first(s + 2 - NW, false, s);
-    if ((s + 1) % TAPS == 0) {
-      const int vx = ((s + 1) / TAPS - (NXB - 1)) * TAPS + TX - 1;
+    if ((s + RL) % TAPS == 0) {
+      const int vx = ((s + RL) / TAPS - (NXB - 1)) * TAPS + TX - 1;
       const int nx = count_first(vx, true, s);
       n = n < nx ? n : nx;
     }
@@ -194,6 +199,10 @@ int launch_vconv(int ef, const VConvArgs& a, hipStream_t st);
 bool rbconv_handles(int ef, const VConvArgs& a);
 int launch_rbconv(int ef, const VConvArgs& a, int G, hipStream_t st);
 int rbconv_set(int enable);  // -> the previous setting
+// VE_ACTIN (conv1 reads the raw chain state and activates its rows in LDS; conv2 writes no activated copy): 1 (the
+// default) or 0 (MT_ACTIN=0 in the environment); bit-identical either way; -> the previous setting
+int rbconv_actin_set(int enable);
+int rbconv_actin_on();
 // the compile-time K loop of the decoder's / upsamplers' convs (1, default) or the runtime-cursor loop (0); -> previous
 int vconv_set_ct(int enable);
 // the process-wide kernel selection above as one value (a key of the decoder's captured graphs)

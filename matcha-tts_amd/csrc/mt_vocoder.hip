@@ -414,10 +414,37 @@ size_t Vocoder::workspace_bytes(int B, int T) const {
 //   XS (+)= conv2(Tb) + state (/ nk on the last resblock)  (last pair)
 // Rounding points equal the generic per-layer path's: every stored tensor is rounded to bf16 and the
 // activated copies are lrelu of the rounded values.
+// every per-layer conv1 of stage i on mt_rbconv with VE_ACTIN (the launch arguments stage_vconv builds)
+bool Vocoder::stage_actin(int i, int B, int L, const int* lens) const {
+  if (!rbconv_actin_on() || !stage_vc(i) || stage_vp(i)) return false;
+  const int nk = (int)rb_kernels.size();
+  for (int j = 0; j < nk; ++j) {
+    if (rb_vp(i, j)) continue;
+    for (const GemmW& g : rb1[(size_t)i * nk + j]) {
+      VConvArgs a{};
+      a.B = B;
+      a.L = L;
+      a.cin = a.c0 = g.cin;
+      a.M = a.Mpad = g.cout;
+      a.taps = g.k;
+      a.dil = g.dil;
+      a.Lout = L;
+      a.ldy = g.cout;
+      a.ylim = L * g.cout;
+      a.lens = lens;
+      if (!rbconv_handles(VE_ACT | VE_ACTIN, a)) return false;
+    }
+  }
+  return true;
+}
+
 int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, const char* XA, char* XS, char* Tb,
                          char* R, char* RA, char* trash, bool act_out, hipStream_t st, const int* lens) const {
   const int nk = (int)rb_kernels.size();
   const bf16* zero = (const bf16*)(P + zero_off);
+  // VE_ACTIN: conv1 activates the raw chain state in LDS, so neither the upsampler (XA) nor conv2 (RA) stores an
+  // activated copy for it (the same bits: lrelu of the stored bf16 values either way)
+  const bool actin = stage_actin(i, B, L, lens);
   int rc;
   if (stage_vp(i)) return pair_chain(P, i, B, L, X, XS, Tb, R, RA, trash, act_out, st, lens);
   for (int j = 0; j < nk; ++j) {
@@ -433,7 +460,7 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
     for (int q = 0; q < np; ++q) {
       const bool last = q == np - 1;
       VConvArgs a{};
-      a.x = (const bf16*)stateA;
+      a.x = (const bf16*)(actin ? state : stateA);
       a.B = B;
       a.L = L;
       a.cin = c1[q].cin;
@@ -450,7 +477,7 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
       a.trash = (bf16*)trash;
       a.lens = lens;
       a.lmul = rate_upto(i + 1);
-      if ((rc = launch_vconv(VE_ACT, a, st))) return rc;
+      if ((rc = launch_vconv(actin ? VE_ACT | VE_ACTIN : VE_ACT, a, st))) return rc;
       VConvArgs b = a;
       b.x = (const bf16*)Tb;
       b.w = (const bf16*)(P + c2[q].v_off);
@@ -463,8 +490,10 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
       int ef = VE_RESID;
       if (!last) {
         b.y = (bf16*)R;
-        b.y2 = (bf16*)RA;
-        ef |= VE_DUAL;
+        if (!actin) {
+          b.y2 = (bf16*)RA;
+          ef |= VE_DUAL;
+        }
         state = R;
         stateA = RA;
       } else {
@@ -533,15 +562,17 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     bool done_up = false;
     if constexpr (std::is_same<E, bf16>::value) {
       const bool svc = stage_vc((int)i);
+      // the stage's per-layer conv1s activate their input themselves (VE_ACTIN) or read XA = lrelu(X)
+      const bool noxa = stage_vp((int)i) || (svc && stage_actin((int)i, B, u.Tout, lens));
       if (ups_vc((int)i)) {  // polyphase vconv from lrelu(xs) (RA); + XA = lrelu(X) for a vconv stage
-        if ((rc = ups_vconv(P, (int)i, B, L, RA, X, XA, svc && !stage_vp((int)i), trash, st, lens))) return rc;
+        if ((rc = ups_vconv(P, (int)i, B, L, RA, X, XA, svc && !noxa, trash, st, lens))) return rc;
         done_up = true;
       }
       if (svc) {
-        // X and XA = lrelu(X): the three resblocks' first convs read XA, their residual X
+        // X and XA = lrelu(X): the three resblocks' first convs read XA (or, VE_ACTIN, X), their residual X
         if (!done_up) {
           u.y2 = XA;
-          if ((rc = stage_vp((int)i) ? launch_conv<E, PF_LRELU, 0>(u, st) : launch_conv<E, PF_LRELU, EF_DUAL>(u, st)))
+          if ((rc = noxa ? launch_conv<E, PF_LRELU, 0>(u, st) : launch_conv<E, PF_LRELU, EF_DUAL>(u, st)))
             return rc;
         }
         L = u.Tout;

@@ -593,9 +593,15 @@ def set_ffn(mode) -> int:
 
 
 def set_ffn_min_frames(frames: int) -> int:
-    """the fused FeedForward only on decoder levels of at least `frames` frames (B x T; default 32768); returns the
+    """the fused FeedForward only on decoder levels of at least `frames` frames (B x T; default 16384); returns the
     previous value (process-wide)"""
     return int(lib().mt_ffn_set_min_frames(int(frames)))
+
+
+def set_rbconv_actin(enable: bool) -> bool:
+    """the stage 1-2 ResBlock conv1s activate the raw chain state in LDS (True, default: no activated copies stored)
+    or read the activated copies their producers store; returns the previous setting (process-wide)"""
+    return bool(lib().mt_vconv_set_actin(int(bool(enable))))
 
 
 def set_rbconv(enable: bool) -> bool:

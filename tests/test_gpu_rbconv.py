@@ -13,6 +13,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
 ACT, RD, R, RA, RAD, RADD = 8, 1 | 16, 1, 1 | 2, 1 | 2 | 4, 1 | 2 | 4 | 16
+ACTIN = 16384
 
 # (C, k, dil, B, L, ef, ragged)
 CASES = [
@@ -94,4 +95,58 @@ def test_rbconv_runs_for_the_vocoder_convs():
                 outs.append(gen(mel, lengths=lens).cpu())
         finally:
             rt.set_rbconv(prev)
+    assert torch.equal(outs[0], outs[1])
+
+
+ACTIN_CASES = [(256, 3, 1, 2, 300, False), (256, 7, 5, 2, 700, True), (256, 11, 3, 3, 640, True), (128, 7, 3, 3, 900, True),
+               (128, 11, 5, 2, 1290, False), (128, 3, 1, 1, 40, False), (128, 11, 1, 150, 1100, True),
+               (256, 7, 1, 64, 600, True)]
+
+
+@pytest.mark.parametrize("case", ACTIN_CASES, ids=lambda c: f"C{c[0]}k{c[1]}d{c[2]}B{c[3]}L{c[4]}{'r' if c[5] else ''}")
+def test_rbconv_actin_equals_activated_input(case):
+    """VE_ACTIN (conv1 reads the raw chain state and applies lrelu to its staged rows in LDS, one step before each
+    chunk's first use) against VE_ACT on the activated copy the producers stored before, lrelu(bf16 x) rounded:
+    bit-identical, over one-round, XCD-major and round-robin grids, ragged and padded"""
+    from matcha_hip import runtime as rt
+    C, k, dil, B, L, ragged = case
+    g = torch.Generator().manual_seed(C + 3 * k + dil + B + L)
+    x = torch.randn(B, L, C, generator=g).bfloat16()
+    xa = torch.maximum(x.float(), 0.1 * x.float()).bfloat16()  # lrelu of the stored values (one rounding)
+    W = (torch.randn(C, C, k, generator=g) / math.sqrt(C * k)).float()
+    b = 0.1 * torch.randn(C, generator=g)
+    lens = torch.randint(max(1, L // 3), L + 1, (B,), generator=g).int().to(DEV) if ragged else None
+    outs = []
+    for xin, ef in ((x, ACT | ACTIN), (xa, ACT)):
+        y = torch.zeros(B, L, C, dtype=torch.bfloat16, device=DEV)
+        out, _ = rt.op_vconv(xin.to(DEV), W.to(DEV), b.to(DEV), dil, ef, None, y=y, slope=0.1, lens=lens)
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
+    assert torch.isfinite(outs[0].float()).all()
+
+
+def test_actin_vocoder_bit_identical():
+    """the bf16 Generator with the stage 1-2 conv1s activating their input in LDS (no XA / RA copies stored) equals
+    the one reading the producers' activated copies, on a ragged batch"""
+    from conftest import make_generator
+    from matcha_hip import runtime as rt
+    from matcha_hip import synthetic
+    gen = make_generator("bf16")
+    sd = synthetic.make_state_dict([(k, tuple(v.shape)) for k, v in gen.state_dict().items()], 41)
+    gen.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    gen = gen.to(DEV).eval()
+    gen.remove_weight_norm()
+    g = torch.Generator().manual_seed(5)
+    B, T = 6, 220
+    mel = torch.randn(B, 80, T, generator=g).to(DEV)
+    lens = torch.tensor([220, 180, 97, 220, 33, 150]).to(DEV)
+    outs = []
+    for on in (True, False):
+        prev = rt.set_rbconv_actin(on)
+        try:
+            with torch.inference_mode():
+                outs.append(gen(mel, lengths=lens).cpu())
+        finally:
+            rt.set_rbconv_actin(prev)
     assert torch.equal(outs[0], outs[1])

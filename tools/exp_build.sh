@@ -15,7 +15,7 @@ while [ $# -gt 0 ]; do
   src=$1; defs=$2; shift 2
   base=$(basename "$src")
   extra=""
-  case "$base" in mt_rbfuse.hip|mt_vpair.hip|mt_vpair32.hip|mt_vpair128.hip) extra="-mno-amdgpu-ieee -fno-honor-nans";; esac
+  case "$base" in mt_rbfuse.hip|mt_rbconv.hip|mt_vpair.hip|mt_vpair32.hip|mt_vpair128.hip) extra="-mno-amdgpu-ieee -fno-honor-nans";; esac
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result $extra $defs \
     -c "$M/csrc/$base" -o "$M/build_exp/$name/$base.o"
   objs=$(echo "$objs" | sed "s#$M/build/$base.o#$M/build_exp/$name/$base.o#")
