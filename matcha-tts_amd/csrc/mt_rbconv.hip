@@ -28,6 +28,10 @@
 #include "mt_ragged.h"
 #include "mt_vconv.h"
 
+#ifndef RB_ACTIN_NV
+#define RB_ACTIN_NV 0  // VE_ACTIN pass step: VALU instructions scheduled after each MFMA
+#endif
+
 #ifndef RB_EXP
 #define RB_EXP 0  // timing experiments (tools/exp_build.sh): bits drop parts of the epilogue (wrong results)
 #endif
@@ -303,17 +307,28 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
       *reinterpret_cast<u32x4*>(p) = v;
     }
   };
-  auto mma_slice = [&](const Frag& F) {
+  // NV > 0 (a VE_ACTIN pass step): NV VALU instructions placed after each MFMA, so the pass runs beside them
+  auto mma_slice = [&](const Frag& F, auto nvc) {
+    constexpr int NV = decltype(nvc)::value;
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
       for (int fn = 0; fn < RFN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+    if constexpr (NV == 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      for (int i = 0; i < 8; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);             // MFMA
+        if (i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);            // VALU
+      }
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
   };
 
   // ---- prologue: the virtual steps v0 .. -1 stage tile 0's chunk-0 rows (part t at tap t), weights of steps 0 .. 2
@@ -375,9 +390,10 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
       // VE_ACTIN: the next chunk's rows were published by this step's wait (RL = 2); activated here, published by the
       // next step's barrier, read from the step after it (or by this step's successor's prefetch)
       if constexpr (ACTIN && t == K - 2) act_pass((c + 1) % 2);
-      mma_slice(F0);
+      using NVP = std::integral_constant<int, (ACTIN && t == K - 2) ? RB_ACTIN_NV : 0>;
+      mma_slice(F0, NVP{});
       read_frag(F0, 0, slot1, xbuf1, t1);
-      mma_slice(F1);
+      mma_slice(F1, NVP{});
       if constexpr (s == S - 1) {
         // the epilogue after the MFMAs: nothing of it (e.g. a copy of a residual register, whose compiler wait is
         // vmcnt(0)) may be scheduled into the MFMA block

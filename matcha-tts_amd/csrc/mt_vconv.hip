@@ -1362,7 +1362,11 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
       MT_VCASE(VE_RESID | VE_DIV | VE_DUAL)
       MT_VCASE(VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL)
       case 0:  // plain: the upsamplers whose stage activates its input itself (VE_ACTIN), compile-time K loops
+#if defined(VCONV_UP_NOCT)  // A/B build: the runtime-cursor loop
+        if (BM == 128) hipLaunchKernelGGL((vconv_kernel<0, 128, false>), dim3(G), dim3(NT), 0, st, a);
+#else
         if (BM == 128) vlaunch<0, 128, false, BN, 8, 2, 4, 2, 2, 2>(a, G, st);
+#endif
         else hipLaunchKernelGGL((vconv_kernel<0, 64, false, BN64>), dim3(G), dim3(NT), 0, st, a);
         break;
       default: set_error("vconv: epilogue %d not compiled in", ef); return -1;

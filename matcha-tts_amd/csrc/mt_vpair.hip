@@ -30,6 +30,9 @@
 #include "mt_probe.h"
 #include "mt_vpair.h"
 
+#ifndef VPAIR_PFB
+#define VPAIR_PFB 0  // 1: the ring kernel prefetches only the next step's frame fragments (its wait: this step's weights only); measured equal to 2 % slower (k = 11), so off
+#endif
 #ifndef VPAIR_EXP
 #define VPAIR_EXP 0  // timing experiments (tools/exp_build.sh): bits drop parts of the pair kernels' work
 #endif
@@ -186,6 +189,18 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       F.B[fn] = *reinterpret_cast<const bf16x8*>(src + rb * 128 + (((ks * 4 + g4) ^ (rb & 6)) * 16));
     }
   };
+  auto read_A = [&](Frag& F, int ks, int slot, int u) {
+    const char* pa = smem + W_OFF + slot * WSLOT + u * TAPW + l16 * 128 + (((ks * 4 + g4) ^ ha) * 16);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048);
+  };
+  auto read_B = [&](Frag& F, int ks, const char* src, int rb0) {
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int rb = rb0 + fn * 16;
+      F.B[fn] = *reinterpret_cast<const bf16x8*>(src + rb * 128 + (((ks * 4 + g4) ^ (rb & 6)) * 16));
+    }
+  };
   // 4 x FN MFMAs of one K-slice with the reads of another slice interleaved, one per MFMA issue slot
   // first: the conv's first K-slice starts the accumulators from the MFMA's zero C operand
   auto mma_slice = [&](const Frag& F, auto first) {
@@ -215,7 +230,10 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     auto step = [&](int m, auto first) {
       const bool more = m + 1 < ns, two = 2 * m + 1 < k;
       if constexpr ((VPAIR_EXP & 16) == 0) {  // timing experiment 16: no per-step wait / barrier (wrong results)
-        vp_wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);  // this step's weights and the next step's
+        // VPAIR_PFB: this step's weights (staged two steps ago); else also the next step's, whose first K-slice is
+        // read at this step's end
+        if constexpr (VPAIR_PFB) vp_wait_vmcnt(issued - wmk[s % NWS]);
+        else vp_wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);
         vp_barrier();
       }
       if (s + NWS - 1 < S) stage_w(s + NWS - 1);
@@ -223,6 +241,8 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       if constexpr (decltype(first)::value) {
         at_first_step();
         read_frag(F0, 0, sl, 0, src, rb0);
+      } else if constexpr (VPAIR_PFB) {
+        read_A(F0, 0, sl, 0);  // the frame fragments came with the previous step
       }
       read_frag(F1, 1, sl, 0, src, rb0 + t0 * tstride);
       mma_slice(F0, first);
@@ -232,7 +252,10 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         read_frag(F1, 1, sl, 1, src, rb0 + (t0 + 1) * tstride);
         mma_slice(F0, std::false_type{});
       }
-      if (more) read_frag(F0, 0, (s + 1) % NWS, 0, src, rb0 + (t0 + 2) * tstride);
+      if (more) {
+        if constexpr (VPAIR_PFB) read_B(F0, 0, src, rb0 + (t0 + 2) * tstride);
+        else read_frag(F0, 0, (s + 1) % NWS, 0, src, rb0 + (t0 + 2) * tstride);
+      }
       mma_slice(F1, std::false_type{});
     };
     step(0, std::true_type{});
