@@ -965,7 +965,9 @@ int Decoder::solve(const void* packed, const float* z_noise, float temperature, 
       ts.t[2 * i + 1] = t + dt * 0.5f;
     }
   }
-  if (!(graphs && !probe_any_armed() && !vclog_armed())) {
+  // eager only while the decoder's own launches are probed or logged: an armed vocoder probe (bench.py's last timed
+  // step) must not take the solve off its graph
+  if (!(graphs && !probe_armed(PROBE_VCONV_DEC) && !vclog_armed())) {
     if ((rc = init_inputs(w, z_noise, temperature, mu_y, spks, B, T, st))) return rc;
     if ((rc = solve_chain(P, w, ts, S, B, T, n_steps, solver, st))) return rc;
     return btc_to_bct(F32, w.zm, NF, 0, B, NF, T, z_out, st);
