@@ -111,6 +111,9 @@ __global__ __launch_bounds__(FNT) void ffn_kernel(FfnArgs a) {
   // weights of step (j, u): u < 4: FF1 rows j*128 .. +127 of x chunk u; u >= 4: FF2 rows ch*128 .. +127 of h chunk
   // 2j + jc (jc = (u - 4) >> 1, ch = (u - 4) & 1)
   auto issue_w = [&](int j, int u, int slot) __attribute__((always_inline)) {
+#if defined(FFN_EXP) && (FFN_EXP & 1)
+    return;  // timing ablation (tools/exp_build.sh): no weight stream, WRONG results
+#endif
     const char* base = u < 4 ? w1b + ((size_t)u * FE + j * 128) * 128
                              : w2b + ((size_t)(2 * j + ((u - 4) >> 1)) * FC + ((u - 4) & 1) * 128) * 128;
     // opaque LDS destination: a known constant range makes the compiler wait for the DMA before every ds_read it

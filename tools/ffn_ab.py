@@ -14,6 +14,9 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from matcha_hip import _lib as L_  # noqa: E402
+
+if os.environ.get("MT_LIB"):  # timing experiments: another build of the library
+    L_.LIB_PATH = os.environ["MT_LIB"]
 from matcha_hip import runtime as rt  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
