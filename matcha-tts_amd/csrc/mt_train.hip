@@ -157,17 +157,38 @@ template <int FMT> struct Half;
 template <> struct Half<1> { typedef _Float16 T; };
 template <> struct Half<2> { typedef __bf16 T; };
 
-// the A-shaped tile of gemm_load_a (128 rows x 32 k) into LDS as [row][k] in 16-bit
+// op(A) tile (128 rows x 32 k) for the 16-bit kernel. Stored [M][K]: gemm_load_a's groups. Stored [K][M] (TA): thread
+// t loads k rows 4 (t >> 5) .. + 3 of row group t & 31 (each k row's 128 floats still one contiguous 512-byte run per
+// 32 lanes), so every one of its 4 rows gets 4 consecutive k — one 8-byte LDS store per row instead of four 2-byte ones
+template <int TA>
+__device__ __forceinline__ void gemm_load_h(const GemmF32& g, const float* A, int m0, int kb, int kend, bool vec,
+                                            f32x4 (&r)[4]) {
+  if constexpr (TA) {
+    const int q = threadIdx.x >> 5, mg = threadIdx.x & 31;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = ld4(A, g.lda, kb + 4 * q + i, m0 + mg * 4, kend, g.M, vec);
+  } else {
+    gemm_load_a<0>(g, A, m0, kb, kend, vec, r);
+  }
+}
+
+// the tile of gemm_load_h into LDS as [row][k] in 16-bit
 template <int TA, typename H>
 __device__ __forceinline__ void gemm_store_h(H (*As)[GKH], const f32x4 (&r)[4]) {
   typedef H h4 __attribute__((ext_vector_type(4)));
+  if constexpr (TA) {  // r[i][j]: k = 4q + i of row 4 mg + j
+    const int q = threadIdx.x >> 5, mg = threadIdx.x & 31;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int e = threadIdx.x + 256 * i;
-    if (TA) {  // 4 consecutive rows at one k
+    for (int j = 0; j < 4; ++j) {
+      h4 v;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) As[(e & 31) * 4 + j][e >> 5] = (H)r[i][j];
-    } else {  // 4 consecutive k of one row
+      for (int i = 0; i < 4; ++i) v[i] = (H)r[i][j];
+      *reinterpret_cast<h4*>(&As[mg * 4 + j][4 * q]) = v;
+    }
+  } else {  // 4 consecutive k of one row
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = threadIdx.x + 256 * i;
       h4 v;
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = (H)r[i][j];
@@ -201,16 +222,16 @@ __global__ __launch_bounds__(256) void gemm_h_kernel(GemmF32 g, int kchunk, int 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   f32x4 ra[4], rb[4];
-  gemm_load_a<TA>(g, A, m0, kbeg, kend, va, ra);
-  gemm_load_a<1 - TB>(gb, B, n0, kbeg, kend, vb, rb);
+  gemm_load_h<TA>(g, A, m0, kbeg, kend, va, ra);
+  gemm_load_h<1 - TB>(gb, B, n0, kbeg, kend, vb, rb);
   const int fr = lane & 31, fk = 8 * (lane >> 5);
   for (int kb = kbeg; kb < kend; kb += GBK) {
     gemm_store_h<TA>(As, ra);
     gemm_store_h<1 - TB>(Bs, rb);
     __syncthreads();
     if (kb + GBK < kend) {
-      gemm_load_a<TA>(g, A, m0, kb + GBK, kend, va, ra);
-      gemm_load_a<1 - TB>(gb, B, n0, kb + GBK, kend, vb, rb);
+      gemm_load_h<TA>(g, A, m0, kb + GBK, kend, va, ra);
+      gemm_load_h<1 - TB>(gb, B, n0, kb + GBK, kend, vb, rb);
     }
 #pragma unroll
     for (int s = 0; s < GBK; s += 16) {
