@@ -123,7 +123,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   if (nmine == 0) return;
 
   struct Tile {
-    int b, n0, m0;
+    int b, n0, m0, lx;  // lx: the utterance's valid frames (ragged), read from the LDS table once per tile
   };
   auto tile_of = [&](int ti) __attribute__((always_inline)) {
     Tile tl;
@@ -133,9 +133,11 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
     if (rag) {
       tl.b = rag_find(rtc, a.B, r);
       tl.n0 = (r - rag_first(rtc, tl.b)) * RBN;
+      tl.lx = rlv[tl.b];
     } else {
       tl.b = r / ntn;
       tl.n0 = (r - tl.b * ntn) * RBN;
+      tl.lx = L;
     }
     return tl;
   };
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   auto issue_x = [&](const Tile& tl, int c, int buf, auto partc) __attribute__((always_inline)) {
     constexpr int part = decltype(partc)::value;
     const int f0 = tl.n0 - a.pad;
-    const int Lx = rag ? rlv[tl.b] : L;
+    const int Lx = tl.lx;
     const char* xb = reinterpret_cast<const char*>(a.x) + ((size_t)tl.b * L * C + c * 64) * 2;
     int xo = RX_OFF + buf * RXBUF;
     asm volatile("" : "+s"(xo));  // opaque LDS destination (see issue_w)
