@@ -503,6 +503,9 @@ def main(argv=None):
     torch.manual_seed(a.seed + rank)
 
     vctk = a.model == "vctk"
+    from matcha_hip import _lib
+    # a timing-experiment library (tools/exp_build.sh) computes wrong results; the loader refuses one already
+    assert _lib.build_experiments() == 0, "bench.py needs a production build of libmatcha_hip.so"
     m, g, den, msd, gsd = build_models(device, a.precision, a.seed, n_spks=109 if vctk else 1)
     x_cpu, xl_cpu = shard_inputs(rank, world, a.batch, a.seed)
     x, xl = x_cpu.to(device), xl_cpu.to(device)
@@ -559,6 +562,7 @@ def main(argv=None):
                    "seq_len": t_pad, "frames_per_step": tot_frames, "parallelism": f"dp{world} (utterance shards)",
                    "denoiser": denoise, "vocoder": "each utterance at its own length (ragged batch, = its one-utterance call)"},
         "rtf": round((el / a.steps) / audio_s, 6),
+        "build_experiments": _lib.build_experiments(),
     }
     if rank == 0:
         if world == 1:

@@ -48,6 +48,11 @@ extern "C" {
 
 const char* mt_last_error(void);
 int mt_abi_version(void);
+/* Nonzero when this library is a timing-experiment build (tools/exp_build.sh), whose kernels drop work and
+ * compute WRONG results: bit 0 mt_vconv (VCONV_EXP, or the VCONV_TS diagnostic build), 1 mt_rbconv (RB_EXP),
+ * 2 mt_ffn (FFN_EXP), 3 the pair kernels (VPAIR_EXP). A production build returns 0; smoke() and bench.py refuse
+ * anything else. */
+int mt_build_experiments(void);
 
 /* ---------------------------------------------------------------------------------------
  * Text encoder + duration predictor (TextEncoder.forward, model.py:517-535; Encoder :428-439,

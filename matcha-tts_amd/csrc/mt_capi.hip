@@ -15,6 +15,11 @@ const char* last_error();
 int denoise(const float* audio, int B, int L, const float* bias_spec, float strength, float* out, void* ws,
             size_t ws_bytes, hipStream_t st, const int* lens = nullptr, int lmul = 1);
 size_t denoise_workspace_bytes(int B, int L);
+// timing-experiment macros each kernel file was built with (0 in a production build)
+int vconv_exp_flags();
+int rbconv_exp_flags();
+int ffn_exp_flags();
+int vpair_exp_flags();
 int stft_magnitude(const float* audio, int B, int L, float* mag, hipStream_t st);
 int log_mel(const float* audio, int B, int L, const float* basis, float mean, float stdv, float* mel, hipStream_t st);
 }  // namespace mt
@@ -49,6 +54,11 @@ extern "C" {
 
 const char* mt_last_error(void) { return mt::last_error(); }
 int mt_abi_version(void) { return 1; }
+int mt_build_experiments(void) {
+  // bit 0: mt_vconv (VCONV_EXP / VCONV_TS), 1: mt_rbconv (RB_EXP), 2: mt_ffn (FFN_EXP), 3: the pair kernels (VPAIR_EXP)
+  return (mt::vconv_exp_flags() ? 1 : 0) | (mt::rbconv_exp_flags() ? 2 : 0) | (mt::ffn_exp_flags() ? 4 : 0) |
+         (mt::vpair_exp_flags() ? 8 : 0);
+}
 
 // ---- decoder ----
 int mt_encoder_create(int n_vocab, int n_channels, int filter_channels, int n_heads, int n_layers, int kernel_size,

@@ -635,6 +635,15 @@ int ffn_set_min_frames(int frames) {
   return prev;
 }
 
+// the FFN_EXP value this file was built with (mt_build_experiments: nonzero = a timing-experiment build)
+int ffn_exp_flags() {
+#if defined(FFN_EXP)
+  return FFN_EXP == 0 ? 0 : FFN_EXP;
+#else
+  return 0;
+#endif
+}
+
 int launch_ffn(const FfnArgs& a, hipStream_t st) {
   MT_REQUIRE(a.x && (a.ln_stats || a.ovec) && a.w1 && a.b1 && a.wsum && a.alpha && a.ibeta && a.w2 && a.b2 && a.zero && a.trash &&
                  a.frames > 0,

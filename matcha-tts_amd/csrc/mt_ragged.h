@@ -63,4 +63,24 @@ __device__ __forceinline__ int rag_find(const int* tc, int B, int r) {
 // first column tile of utterance b
 __device__ __forceinline__ int rag_first(const int* tc, int b) { return b > 0 ? tc[b - 1] : 0; }
 
+// A persistent workgroup's walk over its column tiles r0 < r1 < ... (tiles of one workgroup only increase): the
+// utterance of each by advancing from the previous one (one or two LDS reads per tile where a binary search takes
+// log2 B dependent ones), then the tile's first frame and the utterance's valid length, read once into scalar
+// registers. (A kernel that reads lv[b] where it issues its LDS-DMAs gets it re-read from LDS after every DMA: the
+// compiler cannot prove the DMA leaves that word alone.) Tiles past the last (phantom prefetches) stay in range.
+struct RagTile {
+  int b, n0, lv;
+};
+struct RagWalk {
+  int b = 0;
+  __device__ __forceinline__ RagTile at(const int* tc, const int* lv, int B, int BN, int r) {
+    while (b < B - 1 && __builtin_amdgcn_readfirstlane(tc[b]) <= r) ++b;
+    RagTile t;
+    t.b = b;
+    t.n0 = __builtin_amdgcn_readfirstlane((r - rag_first(tc, b)) * BN);
+    t.lv = __builtin_amdgcn_readfirstlane(lv[b]);
+    return t;
+  }
+};
+
 }  // namespace mt

@@ -457,6 +457,9 @@ int rbconv_set(int enable) {
 
 // the HiFi-GAN wide-stage ResBlock convs: C_in = C_out in {128, 256}, K in {3, 7, 11}, stride 1, plain output
 // (not placed), one source, the ResBlock epilogues, halo <= 64 rows
+// the RB_EXP value this file was built with (mt_build_experiments: nonzero = a timing-experiment build)
+int rbconv_exp_flags() { return RB_EXP; }
+
 bool rbconv_handles(int ef, const VConvArgs& a) {
   if (!rb_knob()) return false;
   const bool eps = ef == VE_ACT || ef == (VE_ACT | VE_ACTIN) || ef == (VE_RESID | VE_DUAL) || ef == VE_RESID || ef == (VE_RESID | VE_ACCUM) ||

@@ -930,6 +930,18 @@ int vconv_repack_s2(const void* src, int cin_pad, int C, int cout, void* dst, hi
   return 0;
 }
 
+// the VCONV_EXP value this file was built with, or 1 << 8 for the -DVCONV_TS diagnostic build (mt_build_experiments)
+int vconv_exp_flags() {
+  int f = 0;
+#if defined(VCONV_EXP)
+  f |= VCONV_EXP == 0 ? 0 : (VCONV_EXP & 0xff) | 1;
+#endif
+#if defined(VCONV_TS)
+  f |= 1 << 8;
+#endif
+  return f;
+}
+
 bool vconv_supported(int cin, int cout, int k, int dil, int stride) {
   // k >= 2 convs stage a chunk's rows during its predecessor's first step and read them a step later;
   // 1x1 convs use the K1 pipeline (rows staged two chunks ahead)

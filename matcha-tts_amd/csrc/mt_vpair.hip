@@ -28,10 +28,17 @@
 #include <cstring>
 
 #include "mt_probe.h"
+#include "mt_ts.h"
 #include "mt_vpair.h"
 
-#ifndef VPAIR_PFB
-#define VPAIR_PFB 0  // 1: the ring kernel prefetches only the next step's frame fragments (its wait: this step's weights only); measured equal to 2 % slower (k = 11), so off
+#ifndef VP_RD
+#define VP_RD 0  // experiment: fragment reads B0 first, MFMAs fn-major (staggered lgkmcnt waits)
+#endif
+#ifndef VP_DMA
+#define VP_DMA 0  // experiment: the ring kernel's weight DMA issued after the step's first K-slice of MFMAs
+#endif
+#ifndef VP_NOLGKM
+#define VP_NOLGKM 0  // experiment: the ring kernel's step barriers without the lgkmcnt(0) drain
 #endif
 #ifndef VPAIR_EXP
 #define VPAIR_EXP 0  // timing experiments (tools/exp_build.sh): bits drop parts of the pair kernels' work
@@ -85,6 +92,17 @@ __device__ __forceinline__ void vp_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
+// a K-loop step's barrier: publishes LDS-DMA data (each wave waited for its own with vmcnt) and frees the ring slot
+// of two steps back. No LDS write is in flight there, and the reads still in flight (the next step's first K-slice)
+// touch neither the slot the step's DMA overwrites nor anything another wave writes, so no lgkmcnt drain: the
+// compiler waits for them where the MFMAs use them
+__device__ __forceinline__ void vp_step_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 template <int EF>
 __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
@@ -118,16 +136,17 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   int wmk[NWS] = {};
   const int ns = (k + 1) / 2;    // steps per conv
   const int S = nmine * 2 * ns;  // weight steps of this workgroup
-  auto tile_of = [&](int ti, int& b, int& n0) {
+  RagWalk walk;
+  auto tile_of = [&](int ti) {  // (utterance, first frame, valid frames) of tile ti
     const int tile = gl + ti * G;
-    if (rag) {
-      b = rag_find(rtc, a.B, tile);
-      n0 = (tile - rag_first(rtc, b)) * BN;
-    } else {
-      b = tile / ntn;
-      n0 = (tile - b * ntn) * BN;
-    }
+    if (rag) return walk.at(rtc, rlv, a.B, BN, tile);
+    RagTile t;
+    t.b = tile / ntn;
+    t.n0 = (tile - t.b * ntn) * BN;
+    t.lv = L;
+    return t;
   };
+  RagTile nxt;  // the tile stage_x staged last (the next tile of the loop)
   auto stage_w = [&](int s) {  // taps 2m, 2m+1 (clamped to k-1) of conv1 or conv2, m = step within the conv
     const int r2 = s % (2 * ns);
     const int m = r2 < ns ? r2 : r2 - ns;
@@ -142,17 +161,16 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     wmk[s % NWS] = issued;
   };
   auto stage_x = [&](int ti) {  // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r
-    int b, n0;
-    tile_of(ti, b, n0);
-    const bf16* xb = a.x + (size_t)b * L * C;
-    const int f0 = n0 - HALO2 - h1, R1 = NF1 + 2 * h1;
+    nxt = tile_of(ti);
+    const bf16* xb = a.x + (size_t)nxt.b * L * C;
+    const int f0 = nxt.n0 - HALO2 - h1, R1 = NF1 + 2 * h1, lv = nxt.lv;
 #pragma unroll
     for (int i = 0; i < XROWS / 64; ++i) {
       const int j = wave + 8 * i;
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < (rag ? rlv[b] : L);
+      const bool ok = r < R1 && f >= 0 && f < lv;
       vp_glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + j * 1024);
     }
     issued += XROWS / 64;
@@ -181,20 +199,19 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       return;
     }
     const char* pa = smem + W_OFF + slot * WSLOT + u * TAPW + l16 * 128 + (((ks * 4 + g4) ^ ha) * 16);
+    if constexpr (VP_RD) {
+      F.B[0] = *reinterpret_cast<const bf16x8*>(src + rb0 * 128 + (((ks * 4 + g4) ^ (rb0 & 6)) * 16));
 #pragma unroll
-    for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048);
+      for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048);
 #pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      const int rb = rb0 + fn * 16;
-      F.B[fn] = *reinterpret_cast<const bf16x8*>(src + rb * 128 + (((ks * 4 + g4) ^ (rb & 6)) * 16));
+      for (int fn = 1; fn < FN; ++fn) {
+        const int rb = rb0 + fn * 16;
+        F.B[fn] = *reinterpret_cast<const bf16x8*>(src + rb * 128 + (((ks * 4 + g4) ^ (rb & 6)) * 16));
+      }
+      return;
     }
-  };
-  auto read_A = [&](Frag& F, int ks, int slot, int u) {
-    const char* pa = smem + W_OFF + slot * WSLOT + u * TAPW + l16 * 128 + (((ks * 4 + g4) ^ ha) * 16);
 #pragma unroll
     for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048);
-  };
-  auto read_B = [&](Frag& F, int ks, const char* src, int rb0) {
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       const int rb = rb0 + fn * 16;
@@ -205,14 +222,14 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   // first: the conv's first K-slice starts the accumulators from the MFMA's zero C operand
   auto mma_slice = [&](const Frag& F, auto first) {
 #pragma unroll
-    for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn)
-        if constexpr ((VPAIR_EXP & 8) != 0) {  // timing experiment: no MFMAs (wrong results)
-          asm volatile("" ::"v"(F.A[fm]), "v"(F.B[fn]));
-          if (decltype(first)::value) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
-        } else
+    for (int i = 0; i < 4 * FN; ++i) {
+      const int fm = VP_RD ? i % 4 : i / FN, fn = VP_RD ? i / 4 : i % FN;  // VP_RD: fn-major
+      if constexpr ((VPAIR_EXP & 8) != 0) {  // timing experiment: no MFMAs (wrong results)
+        asm volatile("" ::"v"(F.A[fm]), "v"(F.B[fn]));
+        if (decltype(first)::value) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else
         acc[fm][fn] = mfma16(F.A[fm], F.B[fn], decltype(first)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn]);
+    }
     constexpr int NR = 4 + FN, NMF = 4 * FN;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
@@ -226,36 +243,37 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   // under this step's last
   Frag F0 = {}, F1 = {};
   int s = 0;
+  VP_TS_DECL
   auto conv = [&](const char* src, int rb0, int tstride, auto&& at_first_step) {
     auto step = [&](int m, auto first) {
       const bool more = m + 1 < ns, two = 2 * m + 1 < k;
+#if defined(VPAIR_TS)
+      if (s % (2 * ns) < ns) VP_TS(4); else VP_TS(7);
+#endif
       if constexpr ((VPAIR_EXP & 16) == 0) {  // timing experiment 16: no per-step wait / barrier (wrong results)
-        // VPAIR_PFB: this step's weights (staged two steps ago); else also the next step's, whose first K-slice is
-        // read at this step's end
-        if constexpr (VPAIR_PFB) vp_wait_vmcnt(issued - wmk[s % NWS]);
-        else vp_wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);
-        vp_barrier();
+        // this step's weights (staged two steps ago) and the next step's, whose first K-slice is read at this
+        // step's end
+        vp_wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);
+        if (VP_NOLGKM && !decltype(first)::value) vp_step_barrier();
+        else vp_barrier();  // a conv's first step also publishes the in-place lrelu / T written before it
       }
-      if (s + NWS - 1 < S) stage_w(s + NWS - 1);
+      VP_TS(6);
+      if (!VP_DMA && s + NWS - 1 < S) stage_w(s + NWS - 1);
       const int sl = s % NWS, t0 = 2 * m;
       if constexpr (decltype(first)::value) {
         at_first_step();
         read_frag(F0, 0, sl, 0, src, rb0);
-      } else if constexpr (VPAIR_PFB) {
-        read_A(F0, 0, sl, 0);  // the frame fragments came with the previous step
       }
       read_frag(F1, 1, sl, 0, src, rb0 + t0 * tstride);
       mma_slice(F0, first);
+      if (VP_DMA && s + NWS - 1 < S) stage_w(s + NWS - 1);
       if (two) {
         read_frag(F0, 0, sl, 1, src, rb0 + (t0 + 1) * tstride);
         mma_slice(F1, std::false_type{});
         read_frag(F1, 1, sl, 1, src, rb0 + (t0 + 1) * tstride);
         mma_slice(F0, std::false_type{});
       }
-      if (more) {
-        if constexpr (VPAIR_PFB) read_B(F0, 0, src, rb0 + (t0 + 2) * tstride);
-        else read_frag(F0, 0, (s + 1) % NWS, 0, src, rb0 + (t0 + 2) * tstride);
-      }
+      if (more) read_frag(F0, 0, (s + 1) % NWS, 0, src, rb0 + (t0 + 2) * tstride);
       mma_slice(F1, std::false_type{});
     };
     step(0, std::true_type{});
@@ -272,13 +290,15 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   const float* par = reinterpret_cast<const float*>(smem + PAR_OFF);
   const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;  // + fp * 32: this lane's 8 channels after the pair swap
   for (int ti = 0; ti < nmine; ++ti) {
-    int b, n0;
-    tile_of(ti, b, n0);
-    const int Lt = rag ? rlv[b] : L;  // this utterance's frames (conv2's zero padding starts there)
+    const int b = nxt.b, n0 = nxt.n0;  // staged by the previous stage_x (tile ti)
+    const int Lt = nxt.lv;             // this utterance's frames (conv2's zero padding starts there)
     // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + HALO2 + h1), then
     // the in-place lrelu of the landed raw rows ----
+    VP_TS(10);
     vp_wait_vmcnt(issued - xmk);
+    VP_TS(0);
     vp_barrier();
+    VP_TS(1);
     u32x4 rv[2][FN], yv[2][FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
@@ -289,6 +309,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         rv[fp][fn] = *reinterpret_cast<const u32x4*>(smem + r * 128 + ((q ^ (r & 6)) * 16));
       }
     vp_barrier();
+    VP_TS(2);
 #pragma unroll
     for (int i = 0; i < ((VPAIR_EXP & 1) ? 0 : XROWS * 8 / NT); ++i) {
       const int e = tid + i * NT;
@@ -297,6 +318,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       for (int w = 0; w < 4; ++w) v[w] = lrelu_pk(v[w], a.slope);
       *reinterpret_cast<u32x4*>(smem + e * 16) = v;
     }
+    VP_TS(3);
     // ---- 2. conv1 (published by its first step's barrier) ----
     int ymk = 0;
     conv(smem, wave * WNC + l16, d, [&] {
@@ -318,6 +340,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         ymk = issued;
       }
     });
+    VP_TS(4);
     // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - HALO2 + j), zero outside [0, L)
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
@@ -346,11 +369,13 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         *reinterpret_cast<u32x4*>(smem + T_OFF + j * 128 + ((q ^ (j & 6)) * 16)) =
             u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
       }
+    VP_TS(5);
     // ---- 3. conv2 ----
     conv(smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, [&] {
       // every wave is past conv1's reads of the row buffer: stage the next tile's raw rows into it
       if (ti + 1 < nmine) stage_x(ti + 1);
     });
+    VP_TS(7);
     // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
     if constexpr ((EF & VE_ACCUM) != 0) {
       vp_wait_vmcnt(issued - ymk);
@@ -359,6 +384,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fp][fn]));  // no use of yv before the wait
     }
+    VP_TS(8);
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -407,7 +433,10 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         }
       }
     issued += 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+    VP_TS(9);
   }
+  VP_TS(11);
+  VP_TS_END(wave, lane);
 }
 
 // ---- k = 3 pairs: HBM-bound (stage 3 at B = 256: 2.5 ms per pair for 6.3 GB of x in / y out), so this variant
@@ -465,16 +494,17 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
 
   int issued = 0;
   int xmk[2] = {0, 0};
-  auto tile_of = [&](int ti, int& b, int& n0) {
+  RagWalk walk;
+  auto tile_of = [&](int ti) {  // (utterance, first frame, valid frames) of tile ti
     const int tile = gl + ti * G;
-    if (rag) {
-      b = rag_find(rtc, a.B, tile);
-      n0 = (tile - rag_first(rtc, b)) * BN;
-    } else {
-      b = tile / ntn;
-      n0 = (tile - b * ntn) * BN;
-    }
+    if (rag) return walk.at(rtc, rlv, a.B, BN, tile);
+    RagTile t;
+    t.b = tile / ntn;
+    t.n0 = (tile - t.b * ntn) * BN;
+    t.lv = L;
+    return t;
   };
+  RagTile nxt;  // the tile stage_x staged last (the next tile of the loop)
   // both convs' 3 taps: DMA j moves rows (j & 7) * 8 .. + 7 of tap j / 8 (conv (j / 8) / 3)
   for (int j = wave; j < 48; j += 8) {
     const int tp = j >> 3, r = (j & 7) * 8 + lrow;
@@ -483,16 +513,15 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
     ++issued;
   }
   auto stage_x = [&](int ti) {  // raw rows of tile ti into buffer ti & 1: row r = frame n0 - HALO2 - h1 + r
-    int b, n0;
-    tile_of(ti, b, n0);
+    nxt = tile_of(ti);
     const bool live = ti < nmine;
-    const bf16* xb = a.x + (size_t)(live ? b : 0) * L * C;
-    const int f0 = n0 - HALO2 - h1, R1 = live ? NF1 + 2 * h1 : 0;
+    const bf16* xb = a.x + (size_t)(live ? nxt.b : 0) * L * C;
+    const int f0 = nxt.n0 - HALO2 - h1, R1 = live ? NF1 + 2 * h1 : 0, lv = nxt.lv;
     for (int j = wave; j < K3_XROWS / 8; j += 8) {
       const int r = 8 * j + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < (rag ? rlv[b] : L);
+      const bool ok = r < R1 && f >= 0 && f < lv;
       vp_glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + (DB ? ti & 1 : 0) * K3_XBUF + j * 1024);
       ++issued;
     }
@@ -522,14 +551,14 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   // first: the conv's first K-slice starts the accumulators from the MFMA's zero C operand
   auto mma_slice = [&](const Frag& F, auto first) {
 #pragma unroll
-    for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn)
-        if constexpr ((VPAIR_EXP & 8) != 0) {  // timing experiment: no MFMAs (wrong results)
-          asm volatile("" ::"v"(F.A[fm]), "v"(F.B[fn]));
-          if (decltype(first)::value) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
-        } else
+    for (int i = 0; i < 4 * FN; ++i) {
+      const int fm = VP_RD ? i % 4 : i / FN, fn = VP_RD ? i / 4 : i % FN;  // VP_RD: fn-major
+      if constexpr ((VPAIR_EXP & 8) != 0) {  // timing experiment: no MFMAs (wrong results)
+        asm volatile("" ::"v"(F.A[fm]), "v"(F.B[fn]));
+        if (decltype(first)::value) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else
         acc[fm][fn] = mfma16(F.A[fm], F.B[fn], decltype(first)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn]);
+    }
     constexpr int NR = 4 + FN, NMF = 4 * FN;
 #pragma unroll
     for (int i = 0; i < NMF; ++i) {
@@ -557,15 +586,18 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   stage_x(0);
   const float* par = reinterpret_cast<const float*>(smem + K3_PAR_OFF);
   const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;
+  VP_TS_DECL
   for (int ti = 0; ti < nmine; ++ti) {
-    int b, n0;
-    tile_of(ti, b, n0);
-    const int Lt = rag ? rlv[b] : L;  // this utterance's frames (conv2's zero padding starts there)
+    const int b = nxt.b, n0 = nxt.n0;  // staged by the previous stage_x (tile ti)
+    const int Lt = nxt.lv;             // this utterance's frames (conv2's zero padding starts there)
     char* xs = smem + (DB ? ti & 1 : 0) * K3_XBUF;
     // ---- 1. rows landed (the first wait also covers the weights); old-xs loads, then the next tile's rows
     // into the other buffer (vmcnt retires in order); residual rows; in-place lrelu ----
+    VP_TS(10);
     vp_wait_vmcnt(issued - xmk[DB ? ti & 1 : 0]);
+    VP_TS(0);
     vp_barrier();
+    VP_TS(1);
     u32x4 rv[2][FN], yv[2][FN];
     int ymk = 0;
     if constexpr ((EF & VE_ACCUM) != 0) {
@@ -592,6 +624,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
         rv[fp][fn] = *reinterpret_cast<const u32x4*>(xs + r * 128 + ((q ^ (r & 6)) * 16));
       }
     vp_barrier();
+    VP_TS(2);
     for (int e = tid; e < ((VPAIR_EXP & 1) ? 0 : K3_XBUF / 16); e += NT) {
       u32x4 v = *reinterpret_cast<const u32x4*>(xs + e * 16);
 #pragma unroll
@@ -599,8 +632,10 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
       *reinterpret_cast<u32x4*>(xs + e * 16) = v;
     }
     vp_barrier();
+    VP_TS(3);
     // ---- 2. conv1 -> T ----
     conv(0, xs, wave * WNC + l16, d);
+    VP_TS(4);
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -628,10 +663,13 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
         *reinterpret_cast<u32x4*>(smem + K3_T_OFF + j * 128 + ((q ^ (j & 6)) * 16)) =
             u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
       }
+    VP_TS(5);
     vp_barrier();  // T published (single buffer: every wave is past conv1's reads of the rows)
     if constexpr (!DB) stage_x(ti + 1);
+    VP_TS(6);
     // ---- 3. conv2 -> y ----
     conv(3, smem + K3_T_OFF, wave * WNC + l16, 1);
+    VP_TS(7);
     if constexpr ((EF & VE_ACCUM) != 0) {
       vp_wait_vmcnt(issued - ymk);
 #pragma unroll
@@ -639,6 +677,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fp][fn]));
     }
+    VP_TS(8);
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -687,9 +726,15 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
         }
       }
     issued += 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+    VP_TS(9);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing row DMAs land before LDS is freed
+  VP_TS(11);
+  VP_TS_END(wave, lane);
 }
+
+// the VPAIR_EXP value this file was built with (mt_build_experiments: nonzero = a timing-experiment build)
+int vpair_exp_flags() { return VPAIR_EXP; }
 
 bool vpair_supported(int C_, int k, int d) {
   return C_ == C && k >= 2 && (k - 1) / 2 <= HALO2 && NF1 + d * (k - 1) <= XROWS;
@@ -758,5 +803,7 @@ int launch_vpair(int ef, const VPairArgs& a, hipStream_t st) {
   vclog_record(rec);
   return 0;
 }
+
+VP_TS_BINDER(vpair_ts_bind)
 
 }  // namespace mt

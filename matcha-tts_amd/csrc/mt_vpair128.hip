@@ -32,6 +32,7 @@
 #include <type_traits>
 
 #include "mt_probe.h"
+#include "mt_ts.h"
 #include "mt_vpair.h"
 
 namespace mt {
@@ -116,16 +117,17 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   int wmk[NWS] = {};
   const int ns = 2 * k;          // steps per conv: (chunk, tap), chunk-major
   const int S = nmine * 2 * ns;  // weight steps of this workgroup
-  auto tile_of = [&](int ti, int& b, int& n0) {
+  RagWalk walk;
+  auto tile_of = [&](int ti) {  // (utterance, first frame, valid frames) of tile ti
     const int tile = gl + ti * G;
-    if (rag) {
-      b = rag_find(rtc, a.B, tile);
-      n0 = (tile - rag_first(rtc, b)) * BN;
-    } else {
-      b = tile / ntn;
-      n0 = (tile - b * ntn) * BN;
-    }
+    if (rag) return walk.at(rtc, rlv, a.B, BN, tile);
+    RagTile t;
+    t.b = tile / ntn;
+    t.n0 = (tile - t.b * ntn) * BN;
+    t.lv = L;
+    return t;
   };
+  RagTile nxt;  // the tile stage_x staged last (the next tile of the loop)
   auto stage_w = [&](int s) {  // step m of conv1 or conv2: image block (chunk m / k, tap m % k)
     const int r2 = s % (2 * ns);
     const int m = r2 < ns ? r2 : r2 - ns;
@@ -139,16 +141,15 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
     wmk[s % NWS] = issued;
   };
   auto stage_x = [&](int ti) {  // raw rows of tile ti, both planes: row r = frame n0 - h2 - h1 + r
-    int b, n0;
-    tile_of(ti, b, n0);
-    const bf16* xb = a.x + (size_t)b * L * C;
-    const int f0 = n0 - h2 - h1;
+    nxt = tile_of(ti);
+    const bf16* xb = a.x + (size_t)nxt.b * L * C;
+    const int f0 = nxt.n0 - h2 - h1, lv = nxt.lv;
     for (int j = wave; j < 2 * nxi; j += 8) {
       const int p = j & 1, blk = j >> 1;
       const int r = 8 * blk + lrow;
       const int q = lp ^ (r & 6);
       const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < (rag ? rlv[b] : L);
+      const bool ok = r < R1 && f >= 0 && f < lv;
       glds16(ok ? xb + (size_t)f * C + p * 64 + q * 8 : a.zero + q * 8, smem + X_OFF + p * XPL + blk * 1024);
       ++issued;
     }
@@ -198,11 +199,16 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   // under its second
   Frag F0, F1;
   int s = 0;
+  VP_TS_DECL
   auto conv = [&](const char* src, int pst, int rb0, int tstride, auto&& at_first_step) {
     auto step = [&](int m, auto first) {
       const bool more = m + 1 < ns;
+#if defined(VPAIR_TS)
+      if (s % (2 * ns) < ns) VP_TS(4); else VP_TS(7);
+#endif
       wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);  // this step's weights and the next step's
       barrier();
+      VP_TS(6);
       if (s + NWS - 1 < S) stage_w(s + NWS - 1);
       const int sl = s % NWS;
       const int c = m >= k ? 1 : 0, t = m - c * k;
@@ -233,13 +239,15 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;  // + fp * 32: this lane's 8 channels after the pair swap
   const char* xpl = smem + X_OFF + wm * XPL;        // this wave's rows' plane of X
   for (int ti = 0; ti < nmine; ++ti) {
-    int b, n0;
-    tile_of(ti, b, n0);
-    const int Lt = rag ? rlv[b] : L;  // this utterance's frames (conv2's zero padding starts there)
+    const int b = nxt.b, n0 = nxt.n0;  // staged by the previous stage_x (tile ti)
+    const int Lt = nxt.lv;             // this utterance's frames (conv2's zero padding starts there)
     // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + h2 + h1), then the
     // in-place lrelu of the landed raw rows ----
+    VP_TS(10);
     wait_vmcnt(issued - xmk);
+    VP_TS(0);
     barrier();
+    VP_TS(1);
     u32x4 rv[2][FN], yv[2][FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
@@ -250,12 +258,14 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
         rv[fp][fn] = *reinterpret_cast<const u32x4*>(xpl + r * 128 + ((q ^ (r & 6)) * 16));
       }
     barrier();
+    VP_TS(2);
     for (int e = tid; e < 2 * XROWS * 8; e += NT) {
       u32x4 v = *reinterpret_cast<const u32x4*>(smem + X_OFF + e * 16);
 #pragma unroll
       for (int w = 0; w < 4; ++w) v[w] = lrelu_pk(v[w], a.slope);
       *reinterpret_cast<u32x4*>(smem + X_OFF + e * 16) = v;
     }
+    VP_TS(3);
     // ---- 2. conv1 (published by its first step's barrier) ----
     int ymk = 0;
     conv(smem + X_OFF, XPL, wn * WNC + l16, d, [&] {
@@ -276,6 +286,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
         ymk = issued;
       }
     });
+    VP_TS(4);
     // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - h2 + j), zero outside [0, L)
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
@@ -299,11 +310,13 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
         *reinterpret_cast<u32x4*>(smem + T_OFF + wm * TPL + j * 128 + ((q ^ (j & 6)) * 16)) =
             u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
       }
+    VP_TS(5);
     // ---- 3. conv2 ----
     conv(smem + T_OFF, TPL, wn * WNC + l16, 1, [&] {
       // every wave is past conv1's reads of the row planes: stage the next tile's raw rows into them
       if (ti + 1 < nmine) stage_x(ti + 1);
     });
+    VP_TS(7);
     // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
     if constexpr ((EF & VE_ACCUM) != 0) {
       wait_vmcnt(issued - ymk);
@@ -312,6 +325,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fp][fn]));  // no use of yv before the wait
     }
+    VP_TS(8);
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -356,7 +370,10 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
         }
       }
     issued += 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+    VP_TS(9);
   }
+  VP_TS(11);
+  VP_TS_END(wave, lane);
 }
 
 bool vpair128_supported(int k, int d) {
@@ -405,5 +422,7 @@ int launch_vpair128(int ef, const VPairArgs& a, hipStream_t st) {
   vclog_record(rec);
   return 0;
 }
+
+VP_TS_BINDER(vpair128_ts_bind)
 
 }  // namespace mt

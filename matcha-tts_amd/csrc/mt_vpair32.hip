@@ -27,6 +27,7 @@
 #include <type_traits>
 
 #include "mt_probe.h"
+#include "mt_ts.h"
 #include "mt_vpair.h"
 
 namespace mt {
@@ -110,16 +111,17 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   __syncthreads();
 
   int issued = 0, xmk = 0;
-  auto tile_of = [&](int ti, int& b, int& n0) __attribute__((always_inline)) {
+  RagWalk walk;
+  auto tile_of = [&](int ti) __attribute__((always_inline)) {  // (utterance, first frame, valid frames) of tile ti
     const int tile = gl + ti * G;
-    if (rag) {
-      b = rag_find(rtc, a.B, tile);
-      n0 = (tile - rag_first(rtc, b)) * BN;
-    } else {
-      b = tile / ntn;
-      n0 = (tile - b * ntn) * BN;
-    }
+    if (rag) return walk.at(rtc, rlv, a.B, BN, tile);
+    RagTile t;
+    t.b = tile / ntn;
+    t.n0 = (tile - t.b * ntn) * BN;
+    t.lv = L;
+    return t;
   };
+  RagTile nxt;  // the tile stage_x staged last (the next tile of the loop)
   // every tap of both convs from the generic packing [32 rows][k][32]: DMA j moves tap (j / 2) % k of conv
   // j / 2k, rows (j & 1) * 16 .. + 15
   auto stage_weights = [&]() {
@@ -132,18 +134,17 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   };
   // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r (zero rows past this workgroup's last tile)
   auto stage_x = [&](int ti) __attribute__((always_inline)) {
-    int b, n0;
-    tile_of(ti, b, n0);
+    nxt = tile_of(ti);
     const bool live = ti < nmine;
-    const bf16* xb = a.x + (size_t)(live ? b : 0) * L * C;
-    const int f0 = n0 - HALO2 - h1, R1 = live ? NF1 + 2 * h1 : 0;
+    const bf16* xb = a.x + (size_t)(live ? nxt.b : 0) * L * C;
+    const int f0 = nxt.n0 - HALO2 - h1, R1 = live ? NF1 + 2 * h1 : 0, lv = nxt.lv;
 #pragma unroll
     for (int i = 0; i < XROWS / 128; ++i) {
       const int j = wave + 8 * i;
       const int r = 16 * j + lrow;
       const int q = lp ^ swz(r);
       const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < (rag ? rlv[b] : L);
+      const bool ok = r < R1 && f >= 0 && f < lv;
       glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + j * 1024);
     }
     issued += XROWS / 128;
@@ -209,14 +210,17 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   const float* par = reinterpret_cast<const float*>(smem + PAR_OFF);
   const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;  // this lane's 8 channels after the fragment swap
   const int qc = (g4 & 1) * 2 + (g4 >> 1);         // ... as a 16-byte chunk index
+  VP_TS_DECL
   for (int ti = 0; ti < nmine; ++ti) {
-    int b, n0;
-    tile_of(ti, b, n0);
-    const int Lt = rag ? rlv[b] : L;  // this utterance's frames (conv2's zero padding starts there)
+    const int b = nxt.b, n0 = nxt.n0;  // staged by the previous stage_x (tile ti)
+    const int Lt = nxt.lv;             // this utterance's frames (conv2's zero padding starts there)
     // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + HALO2 + h1), then
     // the in-place lrelu of the landed raw rows ----
+    VP_TS(10);
     wait_vmcnt(issued - xmk);
+    VP_TS(0);
     barrier();
+    VP_TS(1);
     u32x4 rv[FN], yv[FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
@@ -224,6 +228,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       rv[fn] = *reinterpret_cast<const u32x4*>(smem + r * RB + ((qc ^ swz(r)) * 16));
     }
     barrier();
+    VP_TS(2);
 #pragma unroll
     for (int i = 0; i < XBUF / 16 / NT; ++i) {
       const int e = tid + i * NT;
@@ -233,6 +238,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       *reinterpret_cast<u32x4*>(smem + e * 16) = v;
     }
     barrier();  // activated rows published
+    VP_TS(3);
     // ---- 2. conv1 ----
     int ymk = 0;
     // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2. Issued as asm so that
@@ -251,6 +257,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       ymk = issued;
     }
     conv(0, smem, wave * WNC + l16, d);
+    VP_TS(4);
     // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - HALO2 + j), zero outside [0, L)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
@@ -269,16 +276,20 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       swap16(o[0][1], o[1][1]);
       *reinterpret_cast<u32x4*>(smem + T_OFF + j * RB + ((qc ^ swz(j)) * 16)) = u32x4{o[0][0], o[0][1], o[1][0], o[1][1]};
     }
+    VP_TS(5);
     // ---- 3. conv2 ----
     barrier();  // T published; every wave is past conv1's reads of the row buffer: stage the next tile's rows
     stage_x(ti + 1);
+    VP_TS(6);
     conv(1, smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1);
+    VP_TS(7);
     // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
     if constexpr ((EF & VE_ACCUM) != 0) {
       wait_vmcnt(issued - ymk);
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fn]));  // no use of yv before the wait
     }
+    VP_TS(8);
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       const int i = wave * WNC + fn * 16 + l16;  // output frame n0 + i
@@ -320,8 +331,11 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       }
     }
     issued += FN * ((EF & VE_DUAL) ? 2 : 1);
+    VP_TS(9);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing row / weight DMAs land before LDS is freed
+  VP_TS(11);
+  VP_TS_END(wave, lane);
 }
 
 bool vpair32_supported(int k, int d) {
@@ -367,5 +381,7 @@ int launch_vpair32(int ef, const VPairArgs& a, hipStream_t st) {
   vclog_record(rec);
   return 0;
 }
+
+VP_TS_BINDER(vpair32_ts_bind)
 
 }  // namespace mt

@@ -24,6 +24,7 @@ P = c_void_p  # device pointer / opaque handle
 SIGNATURES = {
     "mt_last_error": (c_char_p, []),
     "mt_abi_version": (c_int, []),
+    "mt_build_experiments": (c_int, []),
     "mt_encoder_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                   POINTER(c_void_p)]),
     "mt_encoder_destroy": (None, [P]),
@@ -155,8 +156,20 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        # a timing-experiment build (tools/exp_build.sh) drops kernel work and computes wrong results: only the
+        # timing tools may load one, explicitly through MT_LIB
+        if not older and hasattr(L, "mt_build_experiments") and L.mt_build_experiments() != 0:
+            raise HipPathError(
+                f"{LIB_PATH} is a timing-experiment build (mt_build_experiments() = {L.mt_build_experiments():#x}): "
+                "rebuild it with `make -C matcha-tts_amd`")
         _lib = L
     return _lib
+
+
+def build_experiments() -> int:
+    """Experiment macros the loaded library was built with (include/matcha_hip.h mt_build_experiments; 0 =
+    production build)."""
+    return int(lib().mt_build_experiments())
 
 
 def check(rc: int, what: str = "") -> None:

@@ -28,6 +28,31 @@ def test_library_exports_every_header_symbol():
     assert L.mt_abi_version() == 1
 
 
+def test_library_is_production_build():
+    from matcha_hip import _lib
+    assert _lib.lib().mt_build_experiments() == 0  # no timing-experiment macro (VPAIR_EXP, RB_EXP, ...) built in
+
+
+def test_loader_refuses_experiment_build(tmp_path, monkeypatch):
+    """A library reporting an experiment build (mt_build_experiments() != 0: tools/exp_build.sh) is refused by the
+    product loader, so smoke() / bench.py / the tests cannot run wrong-result kernels; the timing tools name such
+    a library explicitly with MT_LIB. Checked on a stub library exporting the header's symbols."""
+    import subprocess
+    from matcha_hip import _lib
+    names = header_functions()
+    src = "".join(f"int {n}(void) {{ return {8 if n == 'mt_build_experiments' else 0}; }}\n" for n in names)
+    (tmp_path / "stub.c").write_text(src)
+    so = tmp_path / "libstub.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-w", str(tmp_path / "stub.c"), "-o", str(so)], check=True)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(so))
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.delenv("MT_LIB", raising=False)
+    with pytest.raises(_lib.HipPathError, match="timing-experiment build"):
+        _lib.lib()
+    monkeypatch.setenv("MT_LIB", str(so))  # the timing tools' explicit override loads it
+    assert _lib.lib().mt_build_experiments() == 8
+
+
 def test_library_is_gfx950_code_object():
     from matcha_hip import _lib
     blob = open(_lib.LIB_PATH, "rb").read()
