@@ -53,6 +53,12 @@ int mt_abi_version(void);
  * 2 mt_ffn (FFN_EXP), 3 the pair kernels (VPAIR_EXP). A production build returns 0; smoke() and bench.py refuse
  * anything else. */
 int mt_build_experiments(void);
+/* The compile-time K-loop schedules this library instantiates (mt_vconv's CT loops and mt_rbconv; test support for
+ * tests/test_vcsched.py, host only): mt_sched_count() records; mt_sched_get(i, rec[11], wait, wait_first, cap) fills
+ * rec = {family, NCH, TAPS, NW, NXB, TX, WPW, XPW, NST, RL, prologue wait} and the vmcnt counts the kernel waits with
+ * at the top of steps s = -1 .. S-1 (entries 0 .. S; wait_first: the first tile's), returns S (negative: error). */
+int mt_sched_count(void);
+int mt_sched_get(int i, int* rec, int* wait, int* wait_first, int cap);
 
 /* ---------------------------------------------------------------------------------------
  * Text encoder + duration predictor (TextEncoder.forward, model.py:517-535; Encoder :428-439,

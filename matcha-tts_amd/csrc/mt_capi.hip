@@ -54,6 +54,13 @@ extern "C" {
 
 const char* mt_last_error(void) { return mt::last_error(); }
 int mt_abi_version(void) { return 1; }
+int mt_sched_count(void) { return mt::sched_count(); }
+int mt_sched_get(int i, int* rec, int* wait, int* wait_first, int cap) {
+  MT_REQUIRE(rec && wait && wait_first, "null buffer");
+  const int S = mt::sched_get(i, rec, wait, wait_first, cap);
+  MT_REQUIRE(S >= 0, "schedule %d: out of range or cap %d too small", i, cap);
+  return S;
+}
 int mt_build_experiments(void) {
   // bit 0: mt_vconv (VCONV_EXP / VCONV_TS), 1: mt_rbconv (RB_EXP), 2: mt_ffn (FFN_EXP), 3: the pair kernels (VPAIR_EXP)
   return (mt::vconv_exp_flags() ? 1 : 0) | (mt::rbconv_exp_flags() ? 2 : 0) | (mt::ffn_exp_flags() ? 4 : 0) |

@@ -1,4 +1,5 @@
 #include "mt_probe.h"
+#include "mt_vconv.h"
 
 #include <algorithm>
 #include <mutex>
@@ -121,6 +122,35 @@ std::vector<int> g_log;
 int g_log_cap = 0;
 bool g_log_on = false;
 }  // namespace
+
+namespace {
+struct SchedEntry {
+  int rec[SCHED_FIELDS];
+  SchedWaits waits;
+};
+std::vector<SchedEntry>& sched_table() {  // constructed on first use: registrars run during static initialisation
+  static std::vector<SchedEntry> t;
+  return t;
+}
+}  // namespace
+
+int sched_register(const int (&rec)[SCHED_FIELDS], SchedWaits waits) {
+  auto& t = sched_table();
+  for (const auto& e : t)
+    if (std::equal(e.rec, e.rec + SCHED_FIELDS, rec)) return 0;
+  SchedEntry e;
+  std::copy(rec, rec + SCHED_FIELDS, e.rec);
+  e.waits = waits;
+  t.push_back(e);
+  return 0;
+}
+int sched_count() { return (int)sched_table().size(); }
+int sched_get(int i, int* rec, int* wait, int* wait_first, int cap) {
+  auto& t = sched_table();
+  if (i < 0 || i >= (int)t.size()) return -1;
+  std::copy(t[i].rec, t[i].rec + SCHED_FIELDS, rec);
+  return t[i].waits(wait, wait_first, cap);
+}
 
 void vclog_record(const int (&rec)[VCLOG_FIELDS]) {
   if (!g_log_on) return;

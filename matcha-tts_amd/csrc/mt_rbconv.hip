@@ -420,6 +420,13 @@ namespace {
 #endif
 template <int EF, int C, int K>
 void rb_launch(int G, const VConvArgs& a, hipStream_t st) {
+  // the kernel's schedule (as rbconv_kernel derives it), registered for the CPU schedule test; VE_ACTIN's prologue
+  // waits for all of its staging (vmcnt(0))
+  constexpr int LW = RB_LOADERS, WPW = RbStage<LW>::WPW, XPW = RbStage<LW>::XPW, TX = rb_tx<K, LW>();
+  constexpr bool ACTIN = (EF & VE_ACTIN) != 0;
+  using SCH = VcSched<C / 64, K, RNW, 2, TX, WPW, XPW, rb_nst<EF>(), ACTIN ? 2 : 1>;
+  (void)SchedReg<1, C / 64, K, RNW, 2, TX, WPW, XPW, rb_nst<EF>(), ACTIN ? 2 : 1,
+                 ACTIN ? 0 : SCH::wait_first(-1)>::reg;
   hipLaunchKernelGGL((rbconv_kernel<EF, C, K, RB_LOADERS>), dim3(G), dim3(RNT), 0, st, a);
 }
 // on by default; MT_RBCONV=0 in the environment or mt_vconv_set_rbconv(0): the generic mt_vconv kernel instead

@@ -100,6 +100,32 @@ struct VcSched {
   }
 };
 
+// Host-side registry of the compile-time K-loop schedules the library instantiates, for the CPU schedule test
+// (tests/test_vcsched.py replays each against its own model of the kernels' issue order). A kernel's host launcher
+// odr-uses SchedReg<...>::reg, whose initializer records the schedule when the library is loaded.
+constexpr int SCHED_FIELDS = 11;  // family (0 mt_vconv CT, 1 mt_rbconv), NCH, TAPS, NW, NXB, TX, WPW, XPW, NST, RL,
+                                  // prologue wait (the count the kernel's prologue waits with)
+using SchedWaits = int (*)(int* wait, int* wait_first, int cap);  // s = -1 .. S-1 -> entries 0 .. S; returns S
+int sched_register(const int (&rec)[SCHED_FIELDS], SchedWaits waits);
+int sched_count();
+int sched_get(int i, int* rec, int* wait, int* wait_first, int cap);  // -> S, or -1
+template <int FAM, int NCH, int TAPS, int NW, int NXB, int TX, int WPW, int XPW, int NST, int RL, int PW>
+struct SchedReg {
+  using SCH = VcSched<NCH, TAPS, NW, NXB, TX, WPW, XPW, NST, RL>;
+  static int waits(int* w, int* wf, int cap) {
+    if (cap < SCH::S + 1) return -1;
+    for (int s = -1; s < SCH::S; ++s) {
+      w[s + 1] = SCH::wait(s);
+      wf[s + 1] = SCH::wait_first(s);
+    }
+    return SCH::S;
+  }
+  static const int reg;
+};
+template <int FAM, int NCH, int TAPS, int NW, int NXB, int TX, int WPW, int XPW, int NST, int RL, int PW>
+const int SchedReg<FAM, NCH, TAPS, NW, NXB, TX, WPW, XPW, NST, RL, PW>::reg =
+    sched_register({FAM, NCH, TAPS, NW, NXB, TX, WPW, XPW, NST, RL, PW}, &SchedReg::waits);
+
 // compile-time loop: f(integral_constant<int, I>) for I in [I0, N)
 template <int I, int N, class F>
 __device__ __forceinline__ void vc_for(F&& f) {

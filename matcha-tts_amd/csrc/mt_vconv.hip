@@ -118,6 +118,21 @@ constexpr int vc_npar() {  // per-channel LDS tables (MMAX floats each); VE_GNRE
   return 1 + ((EF & VE_LN) ? 1 : 0) + ((EF & VE_SNAKE) ? 2 : 0) + ((EF & VE_GNRES) ? 3 : 0);
 }
 
+// The compile-time K loop's staging split and schedule (bf16 vconv_kernel<EF, BMT, K1, BNT, false, CTN, CTT>): the
+// kernel and its host launcher (which registers the schedule for the CPU schedule test) take them from here.
+template <int EF, int BMT, bool K1, int BNT, int CTN, int CTT>
+struct CtSched {
+  using TT = VT<BMT, K1, vc_npar<EF>(), BNT>;
+  static constexpr int TAPS = CTT, NCHC = CTN, LW = VC_CT_LOADERS;  // LW loader waves (one per SIMD when 4)
+  static constexpr int WPW = (TT::WSLOT / 1024) / LW, XPW = (TT::XBUF / 1024) / LW;
+  static_assert(WPW * LW * 1024 == TT::WSLOT && XPW * LW * 1024 == TT::XBUF, "pieces per loader wave");
+  static constexpr int TXA = (TT::NXB - 1) * TAPS - 2 < 1 ? 1 : (TT::NXB - 1) * TAPS - 2;
+  static constexpr int TX = TXA < TAPS ? (TXA < XPW ? TXA : XPW) : (TAPS < XPW ? TAPS : XPW);
+  static constexpr int NST = 2 * TT::FN * ((EF & VE_DUAL) ? 2 : 1);  // the epilogue's stores (every lane stores)
+  using SCH = VcSched<NCHC, TAPS, TT::NWSLOT, TT::NXB, TX, WPW, XPW, NST>;
+  using REG = SchedReg<0, NCHC, TAPS, TT::NWSLOT, TT::NXB, TX, WPW, XPW, NST, 1, SCH::wait_first(-1)>;
+};
+
 // F32: fp32 operands (the text encoder, whose duration path must be the reference's fp32 arithmetic): a 128-byte
 // LDS row holds 32 channels, one 16-byte fragment per lane feeds 4 exact-fp32 v_mfma_f32_16x16x4_f32 (mfma16), and
 // the epilogue stores fp32 in the accumulator layout (bias, ReLU, residual, mask only).
@@ -683,13 +698,11 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   }
   if constexpr (CTN > 0) {
     // ================= compile-time K loop (CTN chunks x CTT taps per tile; see VcSched) =================
+    using CS = CtSched<EF, BMT, K1, BNT, CTN, CTT>;
     constexpr int TAPS = CTT, NCHC = CTN, SC = CTN * CTT;
-    constexpr int LW = VC_CT_LOADERS;                         // loader waves (one per SIMD when 4)
-    constexpr int WPW = (WSLOT / 1024) / LW, XPW = (XBUF / 1024) / LW;
-    static_assert(WPW * LW * 1024 == WSLOT && XPW * LW * 1024 == XBUF, "pieces per loader wave");
-    constexpr int TXA = (NXB - 1) * TAPS - 2 < 1 ? 1 : (NXB - 1) * TAPS - 2;
-    constexpr int TX = TXA < TAPS ? (TXA < XPW ? TXA : XPW) : (TAPS < XPW ? TAPS : XPW);
-    using SCH = VcSched<NCHC, TAPS, NWSLOT, NXB, TX, WPW, XPW, NST>;
+    constexpr int LW = CS::LW, WPW = CS::WPW, XPW = CS::XPW, TX = CS::TX;
+    static_assert(CS::NST == NST && !F32, "CtSched matches the kernel");
+    using SCH = typename CS::SCH;
     const bool loader = wave < LW;
     if (nch != NCHC || taps != TAPS) __builtin_trap();  // the host dispatches on (cin / 64, taps)
     // tiles ti + 0 .. 2 of this workgroup, decoded once (past the last: the last, for the phantom prefetches)
@@ -1175,6 +1188,7 @@ template <int E, int BMV, bool K1V, int BNV>
 static void ct_try(const VConvArgs&, int, hipStream_t, bool&) {}
 template <int E, int BMV, bool K1V, int BNV, int N, int T, int... R>
 static void ct_try(const VConvArgs& a, int G, hipStream_t st, bool& done) {
+  (void)CtSched<E, BMV, K1V, BNV, N, T>::REG::reg;  // the schedule, for the CPU schedule test
   if (a.cin / 64 == N && a.taps == T) {
     hipLaunchKernelGGL((vconv_kernel<E, BMV, K1V, BNV, false, N, T>), dim3(G), dim3(NT), 0, st, a);
     done = true;

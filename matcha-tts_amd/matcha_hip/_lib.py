@@ -25,6 +25,8 @@ SIGNATURES = {
     "mt_last_error": (c_char_p, []),
     "mt_abi_version": (c_int, []),
     "mt_build_experiments": (c_int, []),
+    "mt_sched_count": (c_int, []),
+    "mt_sched_get": (c_int, [c_int, P, P, P, c_int]),
     "mt_encoder_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                   POINTER(c_void_p)]),
     "mt_encoder_destroy": (None, [P]),
