@@ -7,6 +7,7 @@
 #include "mt_ffn.h"
 #include "mt_model.h"
 #include "mt_vconv.h"
+#include "mt_vpair.h"
 #include "mt_probe.h"
 #include "mt_train.h"
 
@@ -54,6 +55,7 @@ extern "C" {
 
 const char* mt_last_error(void) { return mt::last_error(); }
 int mt_abi_version(void) { return 1; }
+int mt_vpair_set_kernels(int mask) { return mt::vpair_set_kernels(mask); }
 int mt_sched_count(void) { return mt::sched_count(); }
 int mt_sched_get(int i, int* rec, int* wait, int* wait_first, int cap) {
   MT_REQUIRE(rec && wait && wait_first, "null buffer");

@@ -26,6 +26,13 @@ struct VPairArgs {
   int lmul;
 };
 
+// Round-5 pair-kernel variants, each bit-identical to the kernel it replaces (mt_vpair_set_kernels): bit 0 the
+// compile-time-K ring kernel (vpair_kernel<EF, 7 | 11>). All on by default; MT_VPAIRK=<mask> in the environment (read
+// once) or vpair_set_kernels() to change.
+enum : int { VPK_CTK = 1, VPK_ALL = 1 };
+int vpair_kernels();
+int vpair_set_kernels(int mask);
+
 // epilogue flags: 0 | VE_ACCUM | VE_DIV | VE_DUAL combinations (mt_vconv.h values)
 bool vpair_supported(int C, int k, int d);
 int launch_vpair(int ef, const VPairArgs& a, hipStream_t st);

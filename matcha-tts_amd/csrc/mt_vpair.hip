@@ -31,15 +31,6 @@
 #include "mt_ts.h"
 #include "mt_vpair.h"
 
-#ifndef VP_RD
-#define VP_RD 0  // experiment: fragment reads B0 first, MFMAs fn-major (staggered lgkmcnt waits)
-#endif
-#ifndef VP_DMA
-#define VP_DMA 0  // experiment: the ring kernel's weight DMA issued after the step's first K-slice of MFMAs
-#endif
-#ifndef VP_NOLGKM
-#define VP_NOLGKM 0  // experiment: the ring kernel's step barriers without the lgkmcnt(0) drain
-#endif
 #ifndef VPAIR_EXP
 #define VPAIR_EXP 0  // timing experiments (tools/exp_build.sh): bits drop parts of the pair kernels' work
 #endif
@@ -104,13 +95,43 @@ __device__ __forceinline__ void vp_step_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int EF>
+// The compile-time K loop of vpair_kernel<EF, K> (K > 0): per loader wave and tile of S = 2 NS steps, in program
+// order: step s stages the weights of step s + 2 (2 pieces; past the workgroup's last step: phantom copies of valid
+// weights, never read) after its barrier, then step 0 the old-xs loads (VE_ACCUM, 2 FN) and conv2's first step
+// (s = NS) the next tile's rows (XROWS / 64 pieces; a phantom copy of the last tile after it); the tile's epilogue
+// stores NST after step S - 1. So every vmcnt count is a constant (tests/test_vcsched.py replays the same model for
+// mt_vconv / mt_rbconv).
+template <int EF, int K>
+struct VpkSched {
+  static constexpr int NS = (K + 1) / 2, S = 2 * NS;
+  static constexpr int NACC = (EF & VE_ACCUM) ? 2 * FN : 0, NST = 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+  static constexpr int NXP = XROWS / 64;
+  static constexpr int md(int q) { return ((q % S) + S) % S; }
+  static constexpr int after_w(int q) {  // operations a step issues after its weight pieces
+    return (md(q) == 0 ? NACC : 0) + (md(q) == NS ? NXP : 0) + (md(q) == S - 1 ? NST : 0);
+  }
+  static constexpr int step_ops(int q) { return 2 + after_w(q); }
+  // top of step s: the weights of step v = s + 1 (read at this step's end when s + 1 is in the same conv), else s's
+  static constexpr int wait(int s) {
+    const int v = (s % NS) + 1 < NS ? s + 1 : s;
+    int n = after_w(v - 2);
+    for (int u = v - 1; u < s; ++u) n += step_ops(u);
+    return n;
+  }
+  // the first tile's step 0: step 1's weights are the prologue's last operation
+  static constexpr int wait_first0 = 0;
+  static constexpr int xwait = 2 * (NS - 1) + NST;  // tile start: its rows, staged at the previous tile's step NS
+  static constexpr int xwait_first = 4;             // the first tile: the prologue's rows, then weights of steps 0, 1
+  static constexpr int accwait = 2 * (S - 1) + NXP;  // the epilogue's old-xs loads (step 0)
+};
+
+template <int EF, int K = 0>
 __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4, l16 = lane & 15, lrow = lane >> 3, lp = lane & 7;
-  const int k = a.taps, d = a.dil, L = a.L;
+  const int k = K > 0 ? K : a.taps, d = a.dil, L = a.L;
   const int h1 = d * (k - 1) / 2, h2 = (k - 1) / 2;
   const int ntn = (L + BN - 1) / BN;
   // ragged batch: the live tiles of each utterance (mt_ragged.h)
@@ -160,8 +181,25 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     issued += 2;
     wmk[s % NWS] = issued;
   };
+  // K > 0: the weights of tile step q (mod S) into ring slot `slot` (an opaque offset: with a constant LDS destination
+  // the compiler tracks the DMA and waits for it before every ds_read it cannot prove disjoint)
+  auto stage_w_ct = [&](auto qc, int slot) __attribute__((always_inline)) {
+    constexpr int NSK = (K + 1) / 2, q = decltype(qc)::value % (2 * NSK);
+    constexpr int m = q < NSK ? q : q - NSK;
+    const bf16* w = q < NSK ? a.w1 : a.w2;
+    const int r = 8 * wave + lrow;
+    int so = W_OFF + slot * WSLOT + wave * 1024;
+    asm volatile("" : "+s"(so));
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16* base = w + (size_t)min(2 * m + u, k - 1) * C * 64;
+      int off = r * 64 + (lp ^ (r & 6)) * 8;
+      asm volatile("" : "+v"(off));
+      vp_glds16(base + off, smem + so + u * TAPW);
+    }
+  };
   auto stage_x = [&](int ti) {  // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r
-    nxt = tile_of(ti);
+    nxt = tile_of(K > 0 ? min(ti, nmine - 1) : ti);  // K > 0: past the last tile a phantom copy of it (never read)
     const bf16* xb = a.x + (size_t)nxt.b * L * C;
     const int f0 = nxt.n0 - HALO2 - h1, R1 = NF1 + 2 * h1, lv = nxt.lv;
 #pragma unroll
@@ -199,17 +237,6 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       return;
     }
     const char* pa = smem + W_OFF + slot * WSLOT + u * TAPW + l16 * 128 + (((ks * 4 + g4) ^ ha) * 16);
-    if constexpr (VP_RD) {
-      F.B[0] = *reinterpret_cast<const bf16x8*>(src + rb0 * 128 + (((ks * 4 + g4) ^ (rb0 & 6)) * 16));
-#pragma unroll
-      for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048);
-#pragma unroll
-      for (int fn = 1; fn < FN; ++fn) {
-        const int rb = rb0 + fn * 16;
-        F.B[fn] = *reinterpret_cast<const bf16x8*>(src + rb * 128 + (((ks * 4 + g4) ^ (rb & 6)) * 16));
-      }
-      return;
-    }
 #pragma unroll
     for (int f = 0; f < 4; ++f) F.A[f] = *reinterpret_cast<const bf16x8*>(pa + f * 2048);
 #pragma unroll
@@ -223,7 +250,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   auto mma_slice = [&](const Frag& F, auto first) {
 #pragma unroll
     for (int i = 0; i < 4 * FN; ++i) {
-      const int fm = VP_RD ? i % 4 : i / FN, fn = VP_RD ? i / 4 : i % FN;  // VP_RD: fn-major
+      const int fm = i / FN, fn = i % FN;
       if constexpr ((VPAIR_EXP & 8) != 0) {  // timing experiment: no MFMAs (wrong results)
         asm volatile("" ::"v"(F.A[fm]), "v"(F.B[fn]));
         if (decltype(first)::value) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -254,11 +281,10 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         // this step's weights (staged two steps ago) and the next step's, whose first K-slice is read at this
         // step's end
         vp_wait_vmcnt(issued - wmk[(more ? s + 1 : s) % NWS]);
-        if (VP_NOLGKM && !decltype(first)::value) vp_step_barrier();
-        else vp_barrier();  // a conv's first step also publishes the in-place lrelu / T written before it
+        vp_barrier();
       }
       VP_TS(6);
-      if (!VP_DMA && s + NWS - 1 < S) stage_w(s + NWS - 1);
+      if (s + NWS - 1 < S) stage_w(s + NWS - 1);
       const int sl = s % NWS, t0 = 2 * m;
       if constexpr (decltype(first)::value) {
         at_first_step();
@@ -266,7 +292,6 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       }
       read_frag(F1, 1, sl, 0, src, rb0 + t0 * tstride);
       mma_slice(F0, first);
-      if (VP_DMA && s + NWS - 1 < S) stage_w(s + NWS - 1);
       if (two) {
         read_frag(F0, 0, sl, 1, src, rb0 + (t0 + 1) * tstride);
         mma_slice(F1, std::false_type{});
@@ -280,12 +305,63 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     ++s;
     for (int m = 1; m < ns; ++m, ++s) step(m, std::false_type{});
   };
+  // K > 0: conv CV (0: conv1 steps 0 .. NS-1 of the tile, 1: conv2 steps NS .. S-1) unrolled: ring slots from the
+  // tile's slot base sb (S % 3 != 0 rotates it per tile), counted waits (VpkSched), step barriers without an lgkmcnt
+  // drain (vp_step_barrier) except a conv's first, which also publishes the activated rows / T
+  using SCH = VpkSched<EF, (K > 0 ? K : 3)>;
+  auto slot_of = [&](int sb, int q) __attribute__((always_inline)) {  // ring slot of tile step q (q may pass S)
+    const int v = sb + q % NWS;
+    return v >= NWS ? v - NWS : v;
+  };
+  auto conv_ct = [&](auto cvc, const char* src, int rb0, int tstride, int sb, bool first_tile,
+                     auto&& at_first_step) __attribute__((always_inline)) {
+    constexpr int CV = decltype(cvc)::value, NSK = SCH::NS;
+    vc_for<0, NSK>([&](auto mc) {
+      constexpr int m = decltype(mc)::value, st = CV * NSK + m;
+      constexpr bool more = m + 1 < NSK, two = 2 * m + 1 < K;
+      if constexpr (CV == 0) VP_TS(4); else VP_TS(7);
+      if constexpr (st == 0) {
+        if (first_tile) vc_wait_vmcnt<SCH::wait_first0>();
+        else vc_wait_vmcnt<SCH::wait(0)>();
+      } else {
+        vc_wait_vmcnt<SCH::wait(st)>();
+      }
+      if constexpr (m == 0) vp_barrier();
+      else vp_step_barrier();
+      VP_TS(6);
+      stage_w_ct(std::integral_constant<int, st + NWS - 1>{}, slot_of(sb, st + NWS - 1));
+      const int sl = slot_of(sb, st);
+      constexpr int t0 = 2 * m;
+      int lb = 0;  // opaque per-step row base: hoisted per-step fragment addresses would take hundreds of VGPRs
+      asm volatile("" : "+v"(lb));
+      if constexpr (m == 0) {
+        at_first_step();
+        read_frag(F0, 0, sl, 0, src, rb0 + lb);
+      }
+      read_frag(F1, 1, sl, 0, src, rb0 + lb + t0 * tstride);
+      mma_slice(F0, std::integral_constant<bool, m == 0>{});
+      if constexpr (two) {
+        read_frag(F0, 0, sl, 1, src, rb0 + lb + (t0 + 1) * tstride);
+        mma_slice(F1, std::false_type{});
+        read_frag(F1, 1, sl, 1, src, rb0 + lb + (t0 + 1) * tstride);
+        mma_slice(F0, std::false_type{});
+      }
+      if constexpr (more) read_frag(F0, 0, slot_of(sb, st + 1), 0, src, rb0 + lb + (t0 + 2) * tstride);
+      mma_slice(F1, std::false_type{});
+    });
+  };
 
   // ---- prologue ----
   stage_x(0);
+  if constexpr (K > 0) {
+    stage_w_ct(std::integral_constant<int, 0>{}, 0);
+    stage_w_ct(std::integral_constant<int, 1>{}, 1);
+  } else {
 #pragma unroll
-  for (int p = 0; p < NWS - 1; ++p)
-    if (p < S) stage_w(p);
+    for (int p = 0; p < NWS - 1; ++p)
+      if (p < S) stage_w(p);
+  }
+  int sb = 0;  // K > 0: ring slot of the tile's step 0
 
   const float* par = reinterpret_cast<const float*>(smem + PAR_OFF);
   const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;  // + fp * 32: this lane's 8 channels after the pair swap
@@ -295,7 +371,12 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + HALO2 + h1), then
     // the in-place lrelu of the landed raw rows ----
     VP_TS(10);
-    vp_wait_vmcnt(issued - xmk);
+    if constexpr (K > 0) {
+      if (ti == 0) vc_wait_vmcnt<SCH::xwait_first>();
+      else vc_wait_vmcnt<SCH::xwait>();
+    } else {
+      vp_wait_vmcnt(issued - xmk);
+    }
     VP_TS(0);
     vp_barrier();
     VP_TS(1);
@@ -321,7 +402,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     VP_TS(3);
     // ---- 2. conv1 (published by its first step's barrier) ----
     int ymk = 0;
-    conv(smem, wave * WNC + l16, d, [&] {
+    auto accum_loads = [&] {
       // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2. Issued as asm so
       // that the counted wait below retires them: hipcc drains EVERY in-flight LDS-DMA (vmcnt(0)) before the use
       // of a compiler-visible load result, which would expose the next tile's row staging at each epilogue.
@@ -339,7 +420,9 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         issued += 2 * FN;
         ymk = issued;
       }
-    });
+    };
+    if constexpr (K > 0) conv_ct(std::integral_constant<int, 0>{}, smem, wave * WNC + l16, d, sb, ti == 0, accum_loads);
+    else conv(smem, wave * WNC + l16, d, accum_loads);
     VP_TS(4);
     // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - HALO2 + j), zero outside [0, L)
 #pragma unroll
@@ -371,14 +454,22 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       }
     VP_TS(5);
     // ---- 3. conv2 ----
-    conv(smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, [&] {
-      // every wave is past conv1's reads of the row buffer: stage the next tile's raw rows into it
-      if (ti + 1 < nmine) stage_x(ti + 1);
-    });
+    if constexpr (K > 0) {
+      // every wave is past conv1's reads of the row buffer: stage the next tile's raw rows into it (a phantom copy of
+      // the last tile after it, so the counts stay constant)
+      conv_ct(std::integral_constant<int, 1>{}, smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, sb, false,
+              [&] { stage_x(ti + 1); });
+      sb = slot_of(sb, SCH::S);
+    } else {
+      conv(smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, [&] {
+        if (ti + 1 < nmine) stage_x(ti + 1);
+      });
+    }
     VP_TS(7);
     // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
     if constexpr ((EF & VE_ACCUM) != 0) {
-      vp_wait_vmcnt(issued - ymk);
+      if constexpr (K > 0) vc_wait_vmcnt<SCH::accwait>();
+      else vp_wait_vmcnt(issued - ymk);
 #pragma unroll
       for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -435,6 +526,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     issued += 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
     VP_TS(9);
   }
+  if constexpr (K > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phantom prefetches land before LDS is freed
   VP_TS(11);
   VP_TS_END(wave, lane);
 }
@@ -552,7 +644,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   auto mma_slice = [&](const Frag& F, auto first) {
 #pragma unroll
     for (int i = 0; i < 4 * FN; ++i) {
-      const int fm = VP_RD ? i % 4 : i / FN, fn = VP_RD ? i / 4 : i % FN;  // VP_RD: fn-major
+      const int fm = i / FN, fn = i % FN;
       if constexpr ((VPAIR_EXP & 8) != 0) {  // timing experiment: no MFMAs (wrong results)
         asm volatile("" ::"v"(F.A[fm]), "v"(F.B[fn]));
         if (decltype(first)::value) acc[fm][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -733,6 +825,20 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   VP_TS_END(wave, lane);
 }
 
+static int g_vpk = -1;
+int vpair_kernels() {
+  if (g_vpk < 0) {
+    const char* e = getenv("MT_VPAIRK");
+    g_vpk = e ? atoi(e) & VPK_ALL : VPK_ALL;
+  }
+  return g_vpk;
+}
+int vpair_set_kernels(int mask) {
+  const int prev = vpair_kernels();
+  g_vpk = mask & VPK_ALL;
+  return prev;
+}
+
 // the VPAIR_EXP value this file was built with (mt_build_experiments: nonzero = a timing-experiment build)
 int vpair_exp_flags() { return VPAIR_EXP; }
 
@@ -786,16 +892,25 @@ int launch_vpair(int ef, const VPairArgs& a, hipStream_t st) {
       default: set_error("vpair: epilogue %d not compiled in", ef); return -1;
     }
 #undef MT_VP3
-  } else switch (ef) {
-    case 0: hipLaunchKernelGGL((vpair_kernel<0>), dim3(G), dim3(NT), 0, st, a); break;
-    case VE_ACCUM: hipLaunchKernelGGL((vpair_kernel<VE_ACCUM>), dim3(G), dim3(NT), 0, st, a); break;
-    case VE_ACCUM | VE_DIV: hipLaunchKernelGGL((vpair_kernel<VE_ACCUM | VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
-    case VE_ACCUM | VE_DIV | VE_DUAL:
-      hipLaunchKernelGGL((vpair_kernel<VE_ACCUM | VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a);
-      break;
-    case VE_DIV: hipLaunchKernelGGL((vpair_kernel<VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
-    case VE_DIV | VE_DUAL: hipLaunchKernelGGL((vpair_kernel<VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a); break;
-    default: set_error("vpair: epilogue %d not compiled in", ef); return -1;
+  } else {
+    // k = 7 / 11 (the vocoder's): the compile-time K loop; other kernel sizes the runtime-k loop (same bits)
+    const bool ctk = (vpair_kernels() & VPK_CTK) != 0;
+    auto ring = [&](auto efc) {
+      constexpr int E = decltype(efc)::value;
+      if (!ctk) hipLaunchKernelGGL((vpair_kernel<E>), dim3(G), dim3(NT), 0, st, a);
+      else if (a.taps == 7) hipLaunchKernelGGL((vpair_kernel<E, 7>), dim3(G), dim3(NT), 0, st, a);
+      else if (a.taps == 11) hipLaunchKernelGGL((vpair_kernel<E, 11>), dim3(G), dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((vpair_kernel<E>), dim3(G), dim3(NT), 0, st, a);
+    };
+    switch (ef) {
+      case 0: ring(std::integral_constant<int, 0>{}); break;
+      case VE_ACCUM: ring(std::integral_constant<int, VE_ACCUM>{}); break;
+      case VE_ACCUM | VE_DIV: ring(std::integral_constant<int, VE_ACCUM | VE_DIV>{}); break;
+      case VE_ACCUM | VE_DIV | VE_DUAL: ring(std::integral_constant<int, VE_ACCUM | VE_DIV | VE_DUAL>{}); break;
+      case VE_DIV: ring(std::integral_constant<int, VE_DIV>{}); break;
+      case VE_DIV | VE_DUAL: ring(std::integral_constant<int, VE_DIV | VE_DUAL>{}); break;
+      default: set_error("vpair: epilogue %d not compiled in", ef); return -1;
+    }
   }
   MT_CHECK_HIP(hipGetLastError());
   probe_end(PROBE_VCONV, st, flops, bytes, PROBE_TAG_VPAIR);

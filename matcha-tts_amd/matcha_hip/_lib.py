@@ -93,6 +93,7 @@ SIGNATURES = {
                             P, c_int, P, c_size_t, P]),
     "mt_vconv_set_rbconv": (c_int, [c_int]),
     "mt_vconv_set_ct": (c_int, [c_int]),
+    "mt_vpair_set_kernels": (c_int, [c_int]),
     "mt_ffn_set": (c_int, [c_int]),
     "mt_vconv_set_actin": (c_int, [c_int]),
     "mt_ffn_set_min_frames": (c_int, [c_int]),

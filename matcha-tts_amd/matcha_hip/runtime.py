@@ -585,6 +585,12 @@ def set_vconv_ct(enable: bool) -> bool:
     return bool(lib().mt_vconv_set_ct(int(bool(enable))))
 
 
+def set_vpair_kernels(mask: int) -> int:
+    """the round-5 ResBlock pair kernels (bit 0: the 64-channel k = 7 / 11 compile-time K loop; default 1), each
+    bit-identical to the kernel it replaces; returns the previous mask (process-wide)"""
+    return int(lib().mt_vpair_set_kernels(int(mask)))
+
+
 def set_ffn(mode) -> int:
     """the bf16 decoder's transformer FeedForward as one fused launch (mt_ffn; 3, the default: serial schedule with the
     frame fragments prefetched; 1: serial, weight and frame fragments prefetched; 2: FF1 epilogues overlapped with FF2
