@@ -375,7 +375,11 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
           else vc_wait_vmcnt<SCH::wait(s)>();
         }
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // LDS reads still in flight here (the next step's first K-slice: its weight slot and row buffer) touch neither
+      // what this step's DMAs overwrite (the slot of step s - 1, the row buffer of chunk c - 1) nor anything another
+      // wave writes, so the barrier drains nothing; only the in-place activation pass (VE_ACTIN, at the step before)
+      // writes LDS that other waves read after it
+      if constexpr (ACTIN && t == K - 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       rb_barrier();
       if constexpr (s == S - 1 && (EF & (VE_RESID | VE_ACCUM)) != 0) epi_loads(cur);
       if (loader) {

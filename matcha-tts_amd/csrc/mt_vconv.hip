@@ -801,7 +801,8 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
             else vc_wait_vmcnt<SCH::wait(s)>();
           }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // no lgkmcnt drain: the LDS reads in flight (the next step's first K-slice) touch neither what this step's
+        // DMAs overwrite nor anything another wave writes (the GNRES table is wave-private), mt_rbconv.hip
         raw_barrier();
         if constexpr (s == SC - 1 && (EF & (VE_RESID | VE_ACCUM | VE_LN | VE_MASK | VE_GNRES)) != 0) epi_loads(ti);
         if (loader) stage_step(sc, tq);
