@@ -97,19 +97,25 @@ __device__ __forceinline__ void vp_step_barrier() {
 
 // The compile-time K loop of vpair_kernel<EF, K> (K > 0): per loader wave and tile of S = 2 NS steps, in program
 // order: step s stages the weights of step s + 2 (2 pieces; past the workgroup's last step: phantom copies of valid
-// weights, never read) after its barrier, then step 0 the old-xs loads (VE_ACCUM, 2 FN) and conv2's first step
-// (s = NS) the next tile's rows (XROWS / 64 pieces; a phantom copy of the last tile after it); the tile's epilogue
-// stores NST after step S - 1. So every vmcnt count is a constant (tests/test_vcsched.py replays the same model for
-// mt_vconv / mt_rbconv).
+// weights, never read) after its barrier, then step 0 the old-xs loads (VE_ACCUM, 2 FN) and conv2's steps the next
+// tile's rows (XROWS / 64 pieces, piece i at conv2 step i * NS / NXP: spread among the MFMAs rather than one burst;
+// a phantom copy of the last tile after it); the tile's epilogue stores NST after step S - 1. So every vmcnt count
+// is a constant (tests/test_vcsched.py replays the same model for mt_vconv / mt_rbconv).
 template <int EF, int K>
 struct VpkSched {
   static constexpr int NS = (K + 1) / 2, S = 2 * NS;
   static constexpr int NACC = (EF & VE_ACCUM) ? 2 * FN : 0, NST = 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
   static constexpr int NXP = XROWS / 64;
   static constexpr int md(int q) { return ((q % S) + S) % S; }
-  static constexpr int after_w(int q) {  // operations a step issues after its weight pieces
-    return (md(q) == 0 ? NACC : 0) + (md(q) == NS ? NXP : 0) + (md(q) == S - 1 ? NST : 0);
+  static constexpr int xpieces(int q) {  // row pieces conv2's step q (tile step) issues
+    int n = 0;
+    for (int i = 0; i < NXP; ++i) n += (md(q) >= NS && i * NS / NXP == md(q) - NS) ? 1 : 0;
+    return n;
   }
+  static constexpr int after_w(int q) {  // operations a step issues after its weight pieces
+    return (md(q) == 0 ? NACC : 0) + xpieces(q) + (md(q) == S - 1 ? NST : 0);
+  }
+  static constexpr int xlast = NS + (NXP - 1) * NS / NXP;  // the step issuing the last row piece
   static constexpr int step_ops(int q) { return 2 + after_w(q); }
   // top of step s: the weights of step v = s + 1 (read at this step's end when s + 1 is in the same conv), else s's
   static constexpr int wait(int s) {
@@ -120,7 +126,8 @@ struct VpkSched {
   }
   // the first tile's step 0: step 1's weights are the prologue's last operation
   static constexpr int wait_first0 = 0;
-  static constexpr int xwait = 2 * (NS - 1) + NST;  // tile start: its rows, staged at the previous tile's step NS
+  // tile start: its rows (the last piece issued at the previous tile's step xlast, after that step's weights)
+  static constexpr int xwait = 2 * (S - 1 - xlast) + NST;
   static constexpr int xwait_first = 4;             // the first tile: the prologue's rows, then weights of steps 0, 1
   static constexpr int accwait = 2 * (S - 1) + NXP;  // the epilogue's old-xs loads (step 0)
 };
@@ -198,19 +205,25 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       vp_glds16(base + off, smem + so + u * TAPW);
     }
   };
-  auto stage_x = [&](int ti) {  // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r
+  const bf16* sx_xb = a.x;
+  int sx_f0 = 0, sx_lv = 0;
+  auto stage_x_begin = [&](int ti) {
     nxt = tile_of(K > 0 ? min(ti, nmine - 1) : ti);  // K > 0: past the last tile a phantom copy of it (never read)
-    const bf16* xb = a.x + (size_t)nxt.b * L * C;
-    const int f0 = nxt.n0 - HALO2 - h1, R1 = NF1 + 2 * h1, lv = nxt.lv;
+    sx_xb = a.x + (size_t)nxt.b * L * C;
+    sx_f0 = nxt.n0 - HALO2 - h1, sx_lv = nxt.lv;
+  };
+  auto stage_x_piece = [&](int i) {  // this wave's row piece i (rows 8 j .. 8 j + 7, j = wave + 8 i)
+    const int j = wave + 8 * i;
+    const int r = 8 * j + lrow;
+    const int q = lp ^ (r & 6);
+    const int f = sx_f0 + r;
+    const bool ok = r < NF1 + 2 * h1 && f >= 0 && f < sx_lv;
+    vp_glds16(ok ? sx_xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + j * 1024);
+  };
+  auto stage_x = [&](int ti) {  // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r
+    stage_x_begin(ti);
 #pragma unroll
-    for (int i = 0; i < XROWS / 64; ++i) {
-      const int j = wave + 8 * i;
-      const int r = 8 * j + lrow;
-      const int q = lp ^ (r & 6);
-      const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < lv;
-      vp_glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + j * 1024);
-    }
+    for (int i = 0; i < XROWS / 64; ++i) stage_x_piece(i);
     issued += XROWS / 64;
     xmk = issued;
   };
@@ -313,8 +326,9 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     const int v = sb + q % NWS;
     return v >= NWS ? v - NWS : v;
   };
+  // at_step(m): the step's other VMEM operations after its weight DMA (VpkSched::after_w)
   auto conv_ct = [&](auto cvc, const char* src, int rb0, int tstride, int sb, bool first_tile,
-                     auto&& at_first_step) __attribute__((always_inline)) {
+                     auto&& at_step) __attribute__((always_inline)) {
     constexpr int CV = decltype(cvc)::value, NSK = SCH::NS;
     vc_for<0, NSK>([&](auto mc) {
       constexpr int m = decltype(mc)::value, st = CV * NSK + m;
@@ -334,10 +348,8 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       constexpr int t0 = 2 * m;
       int lb = 0;  // opaque per-step row base: hoisted per-step fragment addresses would take hundreds of VGPRs
       asm volatile("" : "+v"(lb));
-      if constexpr (m == 0) {
-        at_first_step();
-        read_frag(F0, 0, sl, 0, src, rb0 + lb);
-      }
+      at_step(mc);
+      if constexpr (m == 0) read_frag(F0, 0, sl, 0, src, rb0 + lb);
       read_frag(F1, 1, sl, 0, src, rb0 + lb + t0 * tstride);
       mma_slice(F0, std::integral_constant<bool, m == 0>{});
       if constexpr (two) {
@@ -421,8 +433,13 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         ymk = issued;
       }
     };
-    if constexpr (K > 0) conv_ct(std::integral_constant<int, 0>{}, smem, wave * WNC + l16, d, sb, ti == 0, accum_loads);
-    else conv(smem, wave * WNC + l16, d, accum_loads);
+    if constexpr (K > 0) {
+      conv_ct(std::integral_constant<int, 0>{}, smem, wave * WNC + l16, d, sb, ti == 0, [&](auto mc) {
+        if constexpr (decltype(mc)::value == 0) accum_loads();
+      });
+    } else {
+      conv(smem, wave * WNC + l16, d, accum_loads);
+    }
     VP_TS(4);
     // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - HALO2 + j), zero outside [0, L)
 #pragma unroll
@@ -458,7 +475,14 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
       // every wave is past conv1's reads of the row buffer: stage the next tile's raw rows into it (a phantom copy of
       // the last tile after it, so the counts stay constant)
       conv_ct(std::integral_constant<int, 1>{}, smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, sb, false,
-              [&] { stage_x(ti + 1); });
+              [&](auto mc) {
+                constexpr int m = decltype(mc)::value;
+                if constexpr (m == 0) stage_x_begin(ti + 1);
+                vc_for<0, SCH::NXP>([&](auto ic) {
+                  constexpr int i = decltype(ic)::value;
+                  if constexpr (i * SCH::NS / SCH::NXP == m) stage_x_piece(i);
+                });
+              });
       sb = slot_of(sb, SCH::S);
     } else {
       conv(smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1, [&] {
@@ -604,19 +628,26 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
     vp_glds16(w + r * 64 + (lp ^ (r & 6)) * 8, smem + K3_W_OFF + tp * TAPW + (j & 7) * 1024);
     ++issued;
   }
-  auto stage_x = [&](int ti) {  // raw rows of tile ti into buffer ti & 1: row r = frame n0 - HALO2 - h1 + r
+  const bf16* sx_xb = a.x;
+  int sx_f0 = 0, sx_R1 = 0, sx_lv = 0, sx_buf = 0;
+  auto stage_x_begin = [&](int ti) {
     nxt = tile_of(ti);
     const bool live = ti < nmine;
-    const bf16* xb = a.x + (size_t)(live ? nxt.b : 0) * L * C;
-    const int f0 = nxt.n0 - HALO2 - h1, R1 = live ? NF1 + 2 * h1 : 0, lv = nxt.lv;
-    for (int j = wave; j < K3_XROWS / 8; j += 8) {
-      const int r = 8 * j + lrow;
-      const int q = lp ^ (r & 6);
-      const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < lv;
-      vp_glds16(ok ? xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + (DB ? ti & 1 : 0) * K3_XBUF + j * 1024);
-      ++issued;
-    }
+    sx_xb = a.x + (size_t)(live ? nxt.b : 0) * L * C;
+    sx_f0 = nxt.n0 - HALO2 - h1, sx_R1 = live ? NF1 + 2 * h1 : 0, sx_lv = nxt.lv;
+    sx_buf = DB ? ti & 1 : 0;
+  };
+  auto stage_x_piece = [&](int j) {  // DMA j (rows 8 j .. 8 j + 7) of the tile begun by stage_x_begin
+    const int r = 8 * j + lrow;
+    const int q = lp ^ (r & 6);
+    const int f = sx_f0 + r;
+    const bool ok = r < sx_R1 && f >= 0 && f < sx_lv;
+    vp_glds16(ok ? sx_xb + (size_t)f * C + q * 8 : a.zero + q * 8, smem + sx_buf * K3_XBUF + j * 1024);
+    ++issued;
+  };
+  auto stage_x = [&](int ti) {  // raw rows of tile ti into buffer ti & 1: row r = frame n0 - HALO2 - h1 + r
+    stage_x_begin(ti);
+    for (int j = wave; j < K3_XROWS / 8; j += 8) stage_x_piece(j);
     xmk[DB ? ti & 1 : 0] = issued;
   };
 
@@ -660,20 +691,37 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   };
   // one conv (tp0 = 0: conv1, 3: conv2): taps ascending, two K-slices each, each slice read under the previous
   Frag F0, F1;
-  auto conv = [&](int tp0, const char* src, int rb0, int tstride) {
+  // after_tap(tp): called after tap tp's MFMAs are issued (VP_XSPREAD: the next tile's row pieces)
+  auto conv = [&](int tp0, const char* src, int rb0, int tstride, auto&& after_tap) {
     read_frag(F0, 0, tp0, src, rb0);
     read_frag(F1, 1, tp0, src, rb0);
     mma_slice(F0, std::true_type{});
     read_frag(F0, 0, tp0 + 1, src, rb0 + tstride);
     mma_slice(F1, std::false_type{});
+    after_tap(tp0);
 #pragma unroll
     for (int t = 1; t < 3; ++t) {
       read_frag(F1, 1, tp0 + t, src, rb0 + t * tstride);
       mma_slice(F0, std::false_type{});
       if (t < 2) read_frag(F0, 0, tp0 + t + 1, src, rb0 + (t + 1) * tstride);
       mma_slice(F1, std::false_type{});
+      after_tap(tp0 + t);
     }
   };
+  // DB: the next tile's rows go out one DMA piece per tap (piece p of this wave, j = wave + 8 p, after tap p of the
+  // tile's six) instead of one burst at the tile start: a burst stalls its wave on the DMA issue while nothing else
+  // is in flight, and VE_ACCUM's wait for its old-xs loads (issued before the rows) waited for the whole burst;
+  // spread, the pieces issue among the MFMAs (pairlab: 0.96x the burst's time, 0.86x with VE_ACCUM)
+  auto spread = [&](int tp) {
+    if constexpr (DB) {
+      __builtin_amdgcn_sched_barrier(0);
+      const int j = wave + 8 * tp;
+      if (j < K3_XROWS / 8) stage_x_piece(j);
+      if (tp == 5) xmk[sx_buf] = issued;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  static_assert(!DB || (K3_XROWS / 8 + 7) / 8 <= 6, "row pieces per wave fit the taps");
 
   stage_x(0);
   const float* par = reinterpret_cast<const float*>(smem + K3_PAR_OFF);
@@ -706,7 +754,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
       issued += 2 * FN;
       ymk = issued;
     }
-    if constexpr (DB) stage_x(ti + 1);
+    if constexpr (DB) stage_x_begin(ti + 1);  // its pieces issue between the convs' taps (spread)
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -726,7 +774,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
     vp_barrier();
     VP_TS(3);
     // ---- 2. conv1 -> T ----
-    conv(0, xs, wave * WNC + l16, d);
+    conv(0, xs, wave * WNC + l16, d, spread);
     VP_TS(4);
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
@@ -760,7 +808,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
     if constexpr (!DB) stage_x(ti + 1);
     VP_TS(6);
     // ---- 3. conv2 -> y ----
-    conv(3, smem + K3_T_OFF, wave * WNC + l16, 1);
+    conv(3, smem + K3_T_OFF, wave * WNC + l16, 1, spread);
     VP_TS(7);
     if constexpr ((EF & VE_ACCUM) != 0) {
       vp_wait_vmcnt(issued - ymk);
