@@ -373,8 +373,8 @@ int mt_vconv_set_rbconv(int enable);
  * the previous setting. */
 int mt_vconv_set_ct(int enable);
 /* Round-5 ResBlock pair kernels (mask; each bit-identical to the kernel it replaces): bit 0 the 64-channel k = 7 / 11
- * pairs' compile-time K loop. Default 1 (MT_VPAIRK=<mask> in the environment); process-wide; returns the previous
- * mask. */
+ * pairs' compile-time K loop, bit 1 the 128-channel k = 3 pairs' one. Default 3 (MT_VPAIRK=<mask> in the
+ * environment); process-wide; returns the previous mask. */
 int mt_vpair_set_kernels(int mask);
 /* The stage 1-2 ResBlock conv1s (mt_rbconv) read the raw chain state and apply its leaky ReLU to their staged rows in
  * LDS, so the producing convs store no activated copy (1, the default; bit-identical results), or read an activated

@@ -26,10 +26,48 @@ struct VPairArgs {
   int lmul;
 };
 
+// The compile-time K loop of the ring pair kernels (vpair_kernel<EF, K> and vpair128_kernel<EF, K>, K > 0): per wave
+// and tile of S = 2 NS steps (NS per conv), in program order: step s stages the weights of step s + 2 (2 pieces; past
+// the workgroup's last step: phantom copies of valid weights, never read) after its barrier, then step 0 the old-xs
+// loads (VE_ACCUM, 2 FN) and conv2's steps the next tile's rows (NXP pieces, piece i at conv2 step i * XSP / NXP:
+// spread among the MFMAs rather than one burst; a phantom copy of the last tile after it); the tile's epilogue stores
+// NST after step S - 1. So every vmcnt count is a constant (tests/test_vcsched.py replays the same model for mt_vconv
+// / mt_rbconv).
+template <int EF, int NS_, int NXP_, int FN_, int XSP_ = NS_>
+struct VpkSched {
+  static constexpr int NS = NS_, S = 2 * NS, NXP = NXP_, XSP = XSP_;
+  static_assert(XSP >= 1 && XSP <= NS, "rows spread over conv2's steps");
+  static constexpr int NACC = (EF & VE_ACCUM) ? 2 * FN_ : 0, NST = 2 * FN_ * ((EF & VE_DUAL) ? 2 : 1);
+  static constexpr int md(int q) { return ((q % S) + S) % S; }
+  static constexpr int xpieces(int q) {  // row pieces conv2's step q (tile step) issues
+    int n = 0;
+    for (int i = 0; i < NXP; ++i) n += (md(q) >= NS && i * XSP / NXP == md(q) - NS) ? 1 : 0;
+    return n;
+  }
+  static constexpr int after_w(int q) {  // operations a step issues after its weight pieces
+    return (md(q) == 0 ? NACC : 0) + xpieces(q) + (md(q) == S - 1 ? NST : 0);
+  }
+  static constexpr int xlast = NS + (NXP - 1) * XSP / NXP;  // the step issuing the last row piece
+  static constexpr int step_ops(int q) { return 2 + after_w(q); }
+  // top of step s: the weights of step v = s + 1 (read at this step's end when s + 1 is in the same conv), else s's
+  static constexpr int wait(int s) {
+    const int v = (s % NS) + 1 < NS ? s + 1 : s;
+    int n = after_w(v - 2);
+    for (int u = v - 1; u < s; ++u) n += step_ops(u);
+    return n;
+  }
+  // the first tile's step 0: step 1's weights are the prologue's last operation
+  static constexpr int wait_first0 = 0;
+  // tile start: its rows (the last piece issued at the previous tile's step xlast, after that step's weights)
+  static constexpr int xwait = 2 * (S - 1 - xlast) + NST;
+  static constexpr int xwait_first = 4;              // the first tile: the prologue's rows, then weights of steps 0, 1
+  static constexpr int accwait = 2 * (S - 1) + NXP;  // the epilogue's old-xs loads (step 0)
+};
+
 // Round-5 pair-kernel variants, each bit-identical to the kernel it replaces (mt_vpair_set_kernels): bit 0 the
-// compile-time-K ring kernel (vpair_kernel<EF, 7 | 11>). All on by default; MT_VPAIRK=<mask> in the environment (read
-// once) or vpair_set_kernels() to change.
-enum : int { VPK_CTK = 1, VPK_ALL = 1 };
+// 64-channel compile-time-K ring kernel (vpair_kernel<EF, 7 | 11>), bit 1 the 128-channel one (vpair128_kernel<EF, 3>).
+// All on by default; MT_VPAIRK=<mask> in the environment (read once) or vpair_set_kernels() to change.
+enum : int { VPK_CTK = 1, VPK_CTK128 = 2, VPK_ALL = 3 };
 int vpair_kernels();
 int vpair_set_kernels(int mask);
 

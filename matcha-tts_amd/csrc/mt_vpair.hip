@@ -95,42 +95,6 @@ __device__ __forceinline__ void vp_step_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// The compile-time K loop of vpair_kernel<EF, K> (K > 0): per loader wave and tile of S = 2 NS steps, in program
-// order: step s stages the weights of step s + 2 (2 pieces; past the workgroup's last step: phantom copies of valid
-// weights, never read) after its barrier, then step 0 the old-xs loads (VE_ACCUM, 2 FN) and conv2's steps the next
-// tile's rows (XROWS / 64 pieces, piece i at conv2 step i * NS / NXP: spread among the MFMAs rather than one burst;
-// a phantom copy of the last tile after it); the tile's epilogue stores NST after step S - 1. So every vmcnt count
-// is a constant (tests/test_vcsched.py replays the same model for mt_vconv / mt_rbconv).
-template <int EF, int K>
-struct VpkSched {
-  static constexpr int NS = (K + 1) / 2, S = 2 * NS;
-  static constexpr int NACC = (EF & VE_ACCUM) ? 2 * FN : 0, NST = 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
-  static constexpr int NXP = XROWS / 64;
-  static constexpr int md(int q) { return ((q % S) + S) % S; }
-  static constexpr int xpieces(int q) {  // row pieces conv2's step q (tile step) issues
-    int n = 0;
-    for (int i = 0; i < NXP; ++i) n += (md(q) >= NS && i * NS / NXP == md(q) - NS) ? 1 : 0;
-    return n;
-  }
-  static constexpr int after_w(int q) {  // operations a step issues after its weight pieces
-    return (md(q) == 0 ? NACC : 0) + xpieces(q) + (md(q) == S - 1 ? NST : 0);
-  }
-  static constexpr int xlast = NS + (NXP - 1) * NS / NXP;  // the step issuing the last row piece
-  static constexpr int step_ops(int q) { return 2 + after_w(q); }
-  // top of step s: the weights of step v = s + 1 (read at this step's end when s + 1 is in the same conv), else s's
-  static constexpr int wait(int s) {
-    const int v = (s % NS) + 1 < NS ? s + 1 : s;
-    int n = after_w(v - 2);
-    for (int u = v - 1; u < s; ++u) n += step_ops(u);
-    return n;
-  }
-  // the first tile's step 0: step 1's weights are the prologue's last operation
-  static constexpr int wait_first0 = 0;
-  // tile start: its rows (the last piece issued at the previous tile's step xlast, after that step's weights)
-  static constexpr int xwait = 2 * (S - 1 - xlast) + NST;
-  static constexpr int xwait_first = 4;             // the first tile: the prologue's rows, then weights of steps 0, 1
-  static constexpr int accwait = 2 * (S - 1) + NXP;  // the epilogue's old-xs loads (step 0)
-};
 
 template <int EF, int K = 0>
 __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
@@ -321,7 +285,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   // K > 0: conv CV (0: conv1 steps 0 .. NS-1 of the tile, 1: conv2 steps NS .. S-1) unrolled: ring slots from the
   // tile's slot base sb (S % 3 != 0 rotates it per tile), counted waits (VpkSched), step barriers without an lgkmcnt
   // drain (vp_step_barrier) except a conv's first, which also publishes the activated rows / T
-  using SCH = VpkSched<EF, (K > 0 ? K : 3)>;
+  using SCH = VpkSched<EF, (K > 0 ? (K + 1) / 2 : 2), XROWS / 64, FN>;
   auto slot_of = [&](int sb, int q) __attribute__((always_inline)) {  // ring slot of tile step q (q may pass S)
     const int v = sb + q % NWS;
     return v >= NWS ? v - NWS : v;
@@ -480,7 +444,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
                 if constexpr (m == 0) stage_x_begin(ti + 1);
                 vc_for<0, SCH::NXP>([&](auto ic) {
                   constexpr int i = decltype(ic)::value;
-                  if constexpr (i * SCH::NS / SCH::NXP == m) stage_x_piece(i);
+                  if constexpr (i * SCH::XSP / SCH::NXP == m) stage_x_piece(i);
                 });
               });
       sb = slot_of(sb, SCH::S);

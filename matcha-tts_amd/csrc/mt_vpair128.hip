@@ -52,6 +52,14 @@ constexpr int RAG_OFF = PAR_OFF + 2 * C * 4;
 constexpr int LDS_BYTES = RAG_OFF + RAG_LDS;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 static_assert(XROWS % 8 == 0, "X staged 8 rows per DMA instruction");
+// the compile-time K loop (vpair128_kernel<EF, K>, K > 0) stages a fixed XPW row pieces per wave (8 rows of one plane
+// each: 4 XPW blocks per plane, the rows past R1 zero) so that every vmcnt count is a constant; spread over the
+// first XSP of conv2's steps
+constexpr int XPW = 7;
+#ifndef VP128_XSP
+#define VP128_XSP 4
+#endif
+static_assert(32 * XPW <= XROWS, "fixed row staging fits the X planes");
 
 __device__ __forceinline__ void glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
@@ -79,16 +87,26 @@ __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
+// a compile-time K-loop step's barrier (mt_vpair.hip vp_step_barrier): no LDS write in flight, no lgkmcnt drain
+__device__ __forceinline__ void step_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 }  // namespace
 
-template <int EF>
+// K > 0: the compile-time K loop (k = K): steps unrolled, ring slots and vmcnt counts constants (VpkSched), step
+// barriers without an lgkmcnt drain except each conv's first, phantom prefetches past the workgroup's last tile
+template <int EF, int K = 0>
 __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;  // 64-row half, 48-frame quarter
   const int g4 = lane >> 4, l16 = lane & 15, lrow = lane >> 3, lp = lane & 7;
-  const int k = a.taps, d = a.dil, L = a.L;
+  const int k = K > 0 ? K : a.taps, d = a.dil, L = a.L;
   const int h1 = d * (k - 1) / 2, h2 = (k - 1) / 2;
   const int BN = NF1 - 2 * h2;  // output frames per tile
   const int R1 = NF1 + 2 * h1;  // staged rows per plane
@@ -140,20 +158,49 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
     issued += 2;
     wmk[s % NWS] = issued;
   };
-  auto stage_x = [&](int ti) {  // raw rows of tile ti, both planes: row r = frame n0 - h2 - h1 + r
-    nxt = tile_of(ti);
-    const bf16* xb = a.x + (size_t)nxt.b * L * C;
-    const int f0 = nxt.n0 - h2 - h1, lv = nxt.lv;
-    for (int j = wave; j < 2 * nxi; j += 8) {
-      const int p = j & 1, blk = j >> 1;
-      const int r = 8 * blk + lrow;
-      const int q = lp ^ (r & 6);
-      const int f = f0 + r;
-      const bool ok = r < R1 && f >= 0 && f < lv;
-      glds16(ok ? xb + (size_t)f * C + p * 64 + q * 8 : a.zero + q * 8, smem + X_OFF + p * XPL + blk * 1024);
-      ++issued;
+  // K > 0: the weights of tile step q (mod S) into ring slot `slot` (opaque offsets: with a constant LDS destination
+  // the compiler tracks the DMA and waits for it before every ds_read it cannot prove disjoint)
+  auto stage_w_ct = [&](auto qc, int slot) __attribute__((always_inline)) {
+    constexpr int NSK = 2 * (K > 0 ? K : 1), q = decltype(qc)::value % (2 * NSK);
+    constexpr int m = q < NSK ? q : q - NSK;
+    const bf16* w = (q < NSK ? a.w1 : a.w2) + (size_t)m * C * 64;
+    int so = W_OFF + slot * WSLOT + 16 * wave * 128;
+    asm volatile("" : "+s"(so));
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = 16 * wave + 8 * u + lrow;
+      int off = r * 64 + (lp ^ (r & 6)) * 8;
+      asm volatile("" : "+v"(off));
+      glds16(w + off, smem + so + 8 * u * 128);
     }
-    xmk = issued;
+  };
+  const bf16* sx_xb = a.x;
+  int sx_f0 = 0, sx_lv = 0;
+  auto stage_x_begin = [&](int ti) {
+    nxt = tile_of(K > 0 ? min(ti, nmine - 1) : ti);  // K > 0: past the last tile a phantom copy of it (never read)
+    sx_xb = a.x + (size_t)nxt.b * L * C;
+    sx_f0 = nxt.n0 - h2 - h1, sx_lv = nxt.lv;
+  };
+  auto stage_x_piece = [&](int j) {  // rows 8 blk .. 8 blk + 7 of plane p (j = 2 blk + p)
+    const int p = j & 1, blk = j >> 1;
+    const int r = 8 * blk + lrow;
+    const int q = lp ^ (r & 6);
+    const int f = sx_f0 + r;
+    const bool ok = r < R1 && f >= 0 && f < sx_lv;
+    glds16(ok ? sx_xb + (size_t)f * C + p * 64 + q * 8 : a.zero + q * 8, smem + X_OFF + p * XPL + blk * 1024);
+  };
+  auto stage_x = [&](int ti) {  // raw rows of tile ti, both planes: row r = frame n0 - h2 - h1 + r
+    stage_x_begin(ti);
+    if constexpr (K > 0) {
+#pragma unroll
+      for (int i = 0; i < XPW; ++i) stage_x_piece(wave + 8 * i);
+    } else {
+      for (int j = wave; j < 2 * nxi; j += 8) {
+        stage_x_piece(j);
+        ++issued;
+      }
+      xmk = issued;
+    }
   };
 
   auto swap16 = [](uint32_t& x, uint32_t& y) {
@@ -228,12 +275,56 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
     ++s;
     for (int m = 1; m < ns; ++m, ++s) step(m, std::false_type{});
   };
+  // K > 0: conv CV (0: conv1 = tile steps 0 .. NS-1, 1: conv2 = NS .. S-1) unrolled; the tile's ring slots from its
+  // slot base sb (S % 3 != 0 rotates it per tile)
+  using SCH = VpkSched<EF, 2 * (K > 0 ? K : 1), XPW, FN, (VP128_XSP < 2 * K ? VP128_XSP : 2 * (K > 0 ? K : 1))>;
+  auto slot_of = [&](int sb, int q) __attribute__((always_inline)) {  // ring slot of tile step q (q may pass S)
+    const int v = sb + q % NWS;
+    return v >= NWS ? v - NWS : v;
+  };
+  // at_step(m): the step's other VMEM operations after its weight DMA (VpkSched::after_w)
+  auto conv_ct = [&](auto cvc, const char* src, int pst, int rb0, int tstride, int sb, bool first_tile,
+                     auto&& at_step) __attribute__((always_inline)) {
+    constexpr int CV = decltype(cvc)::value, NSK = SCH::NS;
+    vc_for<0, NSK>([&](auto mc) {
+      constexpr int m = decltype(mc)::value, st = CV * NSK + m;
+      constexpr bool more = m + 1 < NSK;
+      constexpr int c = m >= K ? 1 : 0, t = m - c * K;
+      constexpr int c2 = m + 1 >= K ? 1 : 0, t2 = m + 1 - c2 * K;
+      if constexpr (CV == 0) VP_TS(4); else VP_TS(7);
+      if constexpr (st == 0) {
+        if (first_tile) vc_wait_vmcnt<SCH::wait_first0>();
+        else vc_wait_vmcnt<SCH::wait(0)>();
+      } else {
+        vc_wait_vmcnt<SCH::wait(st)>();
+      }
+      if constexpr (m == 0) barrier();
+      else step_barrier();
+      VP_TS(6);
+      stage_w_ct(std::integral_constant<int, st + NWS - 1>{}, slot_of(sb, st + NWS - 1));
+      const int sl = slot_of(sb, st);
+      int lb = 0;  // opaque per-step row base: hoisted per-step fragment addresses would take hundreds of VGPRs
+      asm volatile("" : "+v"(lb));
+      at_step(mc);
+      if constexpr (m == 0) read_frag(F0, 0, sl, src, rb0 + lb);
+      read_frag(F1, 1, sl, src + c * pst, rb0 + lb + t * tstride);
+      mma_slice(F0, std::integral_constant<bool, m == 0>{});
+      if constexpr (more) read_frag(F0, 0, slot_of(sb, st + 1), src + c2 * pst, rb0 + lb + t2 * tstride);
+      mma_slice(F1, std::false_type{});
+    });
+  };
 
   // ---- prologue ----
   stage_x(0);
+  if constexpr (K > 0) {
+    stage_w_ct(std::integral_constant<int, 0>{}, 0);
+    stage_w_ct(std::integral_constant<int, 1>{}, 1);
+  } else {
 #pragma unroll
-  for (int p = 0; p < NWS - 1; ++p)
-    if (p < S) stage_w(p);
+    for (int p = 0; p < NWS - 1; ++p)
+      if (p < S) stage_w(p);
+  }
+  int sb = 0;  // K > 0: ring slot of the tile's step 0
 
   const float* par = reinterpret_cast<const float*>(smem + PAR_OFF);
   const int ch16 = (g4 & 1) * 16 + (g4 >> 1) * 8;  // + fp * 32: this lane's 8 channels after the pair swap
@@ -244,7 +335,12 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
     // ---- 1. the residual rows of this lane's outputs (output frame n0 + i = raw row i + h2 + h1), then the
     // in-place lrelu of the landed raw rows ----
     VP_TS(10);
-    wait_vmcnt(issued - xmk);
+    if constexpr (K > 0) {
+      if (ti == 0) vc_wait_vmcnt<SCH::xwait_first>();
+      else vc_wait_vmcnt<SCH::xwait>();
+    } else {
+      wait_vmcnt(issued - xmk);
+    }
     VP_TS(0);
     barrier();
     VP_TS(1);
@@ -268,7 +364,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
     VP_TS(3);
     // ---- 2. conv1 (published by its first step's barrier) ----
     int ymk = 0;
-    conv(smem + X_OFF, XPL, wn * WNC + l16, d, [&] {
+    auto accum_loads = [&] {
       // VE_ACCUM: the old-xs rows of this tile's outputs, loaded now and consumed after conv2 (asm, so the
       // counted wait below retires them instead of a compiler vmcnt(0) that would drain the row staging)
       if constexpr ((EF & VE_ACCUM) != 0) {
@@ -285,7 +381,14 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
         issued += 2 * FN;
         ymk = issued;
       }
-    });
+    };
+    if constexpr (K > 0) {
+      conv_ct(std::integral_constant<int, 0>{}, smem + X_OFF, XPL, wn * WNC + l16, d, sb, ti == 0, [&](auto mc) {
+        if constexpr (decltype(mc)::value == 0) accum_loads();
+      });
+    } else {
+      conv(smem + X_OFF, XPL, wn * WNC + l16, d, accum_loads);
+    }
     VP_TS(4);
     // epilogue: lrelu(round(acc + b1)) -> T row j (frame n0 - h2 + j), zero outside [0, L)
 #pragma unroll
@@ -312,14 +415,28 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
       }
     VP_TS(5);
     // ---- 3. conv2 ----
-    conv(smem + T_OFF, TPL, wn * WNC + l16, 1, [&] {
-      // every wave is past conv1's reads of the row planes: stage the next tile's raw rows into them
-      if (ti + 1 < nmine) stage_x(ti + 1);
-    });
+    // every wave is past conv1's reads of the row planes: stage the next tile's raw rows into them (K > 0: spread
+    // over conv2's first steps, a phantom copy of the last tile after it, so the counts stay constant)
+    if constexpr (K > 0) {
+      conv_ct(std::integral_constant<int, 1>{}, smem + T_OFF, TPL, wn * WNC + l16, 1, sb, false, [&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        if constexpr (m == 0) stage_x_begin(ti + 1);
+        vc_for<0, XPW>([&](auto ic) {
+          constexpr int i = decltype(ic)::value;
+          if constexpr (i * SCH::XSP / XPW == m) stage_x_piece(wave + 8 * i);
+        });
+      });
+      sb = slot_of(sb, SCH::S);
+    } else {
+      conv(smem + T_OFF, TPL, wn * WNC + l16, 1, [&] {
+        if (ti + 1 < nmine) stage_x(ti + 1);
+      });
+    }
     VP_TS(7);
     // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
     if constexpr ((EF & VE_ACCUM) != 0) {
-      wait_vmcnt(issued - ymk);
+      if constexpr (K > 0) vc_wait_vmcnt<SCH::accwait>();
+      else wait_vmcnt(issued - ymk);
 #pragma unroll
       for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -372,6 +489,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
     issued += 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
     VP_TS(9);
   }
+  if constexpr (K > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the phantom DMA lands before the wave ends
   VP_TS(11);
   VP_TS_END(wave, lane);
 }
@@ -405,15 +523,20 @@ int launch_vpair128(int ef, const VPairArgs& a, hipStream_t st) {
   const double flops = 2.0 * 2.0 * C * C * a.taps * (double)a.B * a.L;
   const double bytes = 2.0 * (2.0 * 2.0 * C * (double)a.B * a.L) + 2.0 * 2.0 * C * C * a.taps;
   probe_begin(PROBE_VCONV, st);
+  // the compile-time K loop for k = 3 (mt_vpair_set_kernels bit VPK_CTK128) when its fixed row staging covers R1
+  const bool ct3 = a.taps == 3 && (vpair_kernels() & VPK_CTK128) != 0 && NF1 + 2 * a.dil <= 32 * XPW;
+  auto go = [&](auto ec) {
+    constexpr int E = decltype(ec)::value;
+    if (ct3) hipLaunchKernelGGL((vpair128_kernel<E, 3>), dim3(G), dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((vpair128_kernel<E>), dim3(G), dim3(NT), 0, st, a);
+  };
   switch (ef) {
-    case 0: hipLaunchKernelGGL((vpair128_kernel<0>), dim3(G), dim3(NT), 0, st, a); break;
-    case VE_ACCUM: hipLaunchKernelGGL((vpair128_kernel<VE_ACCUM>), dim3(G), dim3(NT), 0, st, a); break;
-    case VE_ACCUM | VE_DIV: hipLaunchKernelGGL((vpair128_kernel<VE_ACCUM | VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
-    case VE_ACCUM | VE_DIV | VE_DUAL:
-      hipLaunchKernelGGL((vpair128_kernel<VE_ACCUM | VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a);
-      break;
-    case VE_DIV: hipLaunchKernelGGL((vpair128_kernel<VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
-    case VE_DIV | VE_DUAL: hipLaunchKernelGGL((vpair128_kernel<VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a); break;
+    case 0: go(std::integral_constant<int, 0>{}); break;
+    case VE_ACCUM: go(std::integral_constant<int, VE_ACCUM>{}); break;
+    case VE_ACCUM | VE_DIV: go(std::integral_constant<int, VE_ACCUM | VE_DIV>{}); break;
+    case VE_ACCUM | VE_DIV | VE_DUAL: go(std::integral_constant<int, VE_ACCUM | VE_DIV | VE_DUAL>{}); break;
+    case VE_DIV: go(std::integral_constant<int, VE_DIV>{}); break;
+    case VE_DIV | VE_DUAL: go(std::integral_constant<int, VE_DIV | VE_DUAL>{}); break;
     default: set_error("vpair128: epilogue %d not compiled in", ef); return -1;
   }
   MT_CHECK_HIP(hipGetLastError());

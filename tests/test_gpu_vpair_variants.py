@@ -1,6 +1,6 @@
-"""Round-5 ResBlock pair kernels against the kernels they replace (mt_vpair_set_kernels): the 64-channel k = 7 / 11
-pairs' compile-time K loop (unrolled steps, constant ring slots and vmcnt counts, phantom prefetches past the last
-tile). Same fragments, MFMA accumulation order and rounding points, so the Generator's waveform must be BIT-identical
+"""Round-5 ResBlock pair kernels against the kernels they replace (mt_vpair_set_kernels): the compile-time K loops
+(unrolled steps, constant ring slots and vmcnt counts, phantom prefetches past the last tile) of the 64-channel k = 7 /
+11 pairs and the 128-channel k = 3 pairs (d = 1, 3, 5; fixed row staging spread over conv2's steps). Same fragments, MFMA accumulation order and rounding points, so the Generator's waveform must be BIT-identical
 with the variant on and off (hifigan/models.py:90-97, 183-192), on a ragged batch (one-utterance tiles at each length)
 and on a padded one, with multi-round grids (tile counts per workgroup of both parities: the k = 7 kernel's ring
 slot base rotates per tile) and at batch 1 (one-round grids).
@@ -12,6 +12,7 @@ from conftest import make_generator
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
+VPK_ALL = 3  # mt_vpair.h: VPK_CTK | VPK_CTK128
 
 
 def _gen(seed=8):
@@ -45,7 +46,7 @@ def test_round5_pair_kernels_bit_identical(B, T, ragged):
         lens = torch.randint(T // 3, T + 1, (B,), generator=torch.Generator().manual_seed(T))
         lens[0] = T
         lens = lens.to(DEV)
-    on = _run(g, mel, lens, 1)
+    on = _run(g, mel, lens, VPK_ALL)
     assert torch.isfinite(on).all()
     off = _run(g, mel, lens, 0)
     assert torch.equal(on, off), (on - off).abs().max()
