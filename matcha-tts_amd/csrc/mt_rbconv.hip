@@ -26,14 +26,24 @@
 
 #include "mt_probe.h"
 #include "mt_ragged.h"
+#include "mt_ts.h"
 #include "mt_vconv.h"
 
 #ifndef RB_ACTIN_NV
 #define RB_ACTIN_NV 0  // VE_ACTIN pass step: VALU instructions scheduled after each MFMA
 #endif
 
+#ifndef RB_RAGWALK
+#define RB_RAGWALK 1  // ragged tile lookup: 1 the incremental walk (mt_ragged.h RagWalk), 0 a binary search per tile
+#endif
+
+#ifndef RB_DMA_AT
+#define RB_DMA_AT 1  // where a step's loader DMA issue sits: 0 after the barrier, 1 between its K-slices, 2 after both
+#endif
+
 #ifndef RB_EXP
-#define RB_EXP 0  // timing experiments (tools/exp_build.sh): bits drop parts of the epilogue (wrong results)
+#define RB_EXP 0  // timing experiments (tools/exp_build.sh, tools/rblab): bits drop parts of the work (wrong results):
+                  // 1 epilogue operand loads, 2 the y2 store, 4 the K loop's DMA issue, 8 its step barriers, 16 MFMAs
 #endif
 
 namespace mt {
@@ -125,15 +135,21 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   struct Tile {
     int b, n0, m0, lx;  // lx: the utterance's valid frames (ragged), read from the LDS table once per tile
   };
+  RagWalk walk;  // RB_RAGWALK: the workgroup's rows r only increase (tile_of(ti) is called for ti = 0, 1, 2, ...)
   auto tile_of = [&](int ti) __attribute__((always_inline)) {
     Tile tl;
     const int tile = gl + min(ti, nmine - 1) * gstep;  // past the last tile: the last one (phantom prefetches)
     const int r = tile / NTM;
     tl.m0 = (tile - r * NTM) * RBM;
     if (rag) {
+#if RB_RAGWALK
+      const RagTile rt = walk.at(rtc, rlv, a.B, RBN, r);
+      tl.b = rt.b, tl.n0 = rt.n0, tl.lx = rt.lv;
+#else
       tl.b = rag_find(rtc, a.B, r);
       tl.n0 = (r - rag_first(rtc, tl.b)) * RBN;
       tl.lx = rlv[tl.b];
+#endif
     } else {
       tl.b = r / ntn;
       tl.n0 = (r - tl.b * ntn) * RBN;
@@ -315,7 +331,10 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-      for (int fn = 0; fn < RFN; ++fn) acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+      for (int fn = 0; fn < RFN; ++fn) {
+        if constexpr ((RB_EXP & 16) != 0) asm volatile("" : "+v"(acc[fm][fn]) : "v"(F.A[fm]), "v"(F.B[fn]));
+        else acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+      }
     if constexpr (NV == 0) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -334,6 +353,9 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   };
 
   // ---- prologue: the virtual steps v0 .. -1 stage tile 0's chunk-0 rows (part t at tap t), weights of steps 0 .. 2
+  // (phase stamps of the diagnostic build, tools/rblab: 0 wait, 1 barrier, 2 DMA issue, 3 MFMA block, 4 activation
+  // pass, 5 epilogue, 6 tile head, 7 prologue, 11 drain)
+  VP_TS_DECL
   Tile cur = tile_of(0), nxt = tile_of(1);
   if (loader) {
     vc_for<SCH::v0, 0>([&](auto vc) {
@@ -352,6 +374,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   }
   Frag F0, F1;
   read_frag(F0, 0, 0, 0, 0);
+  VP_TS(7);
 
   // ---- the tile loop: one unrolled tile per iteration. The ring slot of step s of tile ti is (ti * S + s) % 4: a
   // constant when S % 4 == 0 (C = 256), else (C = 128, S = 2K = 2 mod 4) the tile's parity adds 2 ----
@@ -367,6 +390,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
       // publish step s+1's data (its weights; its rows when it starts a chunk); every wave's reads of step s-1
       // are done, so its weight slot and (at a chunk's first step) the other row buffer may be restaged
       __builtin_amdgcn_sched_barrier(0);  // the waits stay after the previous step's MFMAs
+      if constexpr (s > 0) VP_TS(3);
       if (loader) {
         if constexpr (SCH::wait_first(s) == SCH::wait(s)) {
           vc_wait_vmcnt<SCH::wait(s)>();
@@ -380,31 +404,51 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
       // wave writes, so the barrier drains nothing; only the in-place activation pass (VE_ACTIN, at the step before)
       // writes LDS that other waves read after it
       if constexpr (ACTIN && t == K - 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      rb_barrier();
+      VP_TS(0);
+      if constexpr ((RB_EXP & 8) == 0) rb_barrier();
+      VP_TS(1);
       if constexpr (s == S - 1 && (EF & (VE_RESID | VE_ACCUM)) != 0) epi_loads(cur);
-      if (loader) {
-        if constexpr (t < TX) {  // rows of the next chunk (this tile's c + 1, or the next tile's chunk 0), part t
-          if constexpr (c + 1 < NCH) issue_x(cur, c + 1, (c + 1) % 2, std::integral_constant<int, t>{});
-          else issue_x(nxt, 0, 0, std::integral_constant<int, t>{});
+      auto dma = [&]() __attribute__((always_inline)) {
+        if (loader && (RB_EXP & 4) == 0) {
+          if constexpr (t < TX) {  // rows of the next chunk (this tile's c + 1, or the next tile's chunk 0), part t
+            if constexpr (c + 1 < NCH) issue_x(cur, c + 1, (c + 1) % 2, std::integral_constant<int, t>{});
+            else issue_x(nxt, 0, 0, std::integral_constant<int, t>{});
+          }
+          // weights of step s + 3 (slot of step s - 1)
+          constexpr int s3 = (s + 3) % S, c3 = s3 / K, t3 = s3 % K;
+          if constexpr (s + 3 < S) issue_w(cur, c3, t3, slot3);
+          else issue_w(nxt, c3, t3, slot3);
         }
-        // weights of step s + 3 (slot of step s - 1)
-        constexpr int s3 = (s + 3) % S, c3 = s3 / K, t3 = s3 % K;
-        if constexpr (s + 3 < S) issue_w(cur, c3, t3, slot3);
-        else issue_w(nxt, c3, t3, slot3);
-      }
+      };
+      if constexpr (RB_DMA_AT == 0) dma();
+      VP_TS(2);
       read_frag(F1, 1, slot, xbuf, t);
       // VE_ACTIN: the next chunk's rows were published by this step's wait (RL = 2); activated here, published by the
       // next step's barrier, read from the step after it (or by this step's successor's prefetch)
-      if constexpr (ACTIN && t == K - 2) act_pass((c + 1) % 2);
+      if constexpr (ACTIN && t == K - 2) {
+        act_pass((c + 1) % 2);
+        VP_TS(4);
+      }
       using NVP = std::integral_constant<int, (ACTIN && t == K - 2) ? RB_ACTIN_NV : 0>;
       mma_slice(F0, NVP{});
+      if constexpr (RB_DMA_AT == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        dma();
+        __builtin_amdgcn_sched_barrier(0);
+      }
       read_frag(F0, 0, slot1, xbuf1, t1);
       mma_slice(F1, NVP{});
+      if constexpr (RB_DMA_AT == 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        dma();
+      }
       if constexpr (s == S - 1) {
         // the epilogue after the MFMAs: nothing of it (e.g. a copy of a residual register, whose compiler wait is
         // vmcnt(0)) may be scheduled into the MFMA block
         __builtin_amdgcn_sched_barrier(0);
+        VP_TS(3);
         epilogue(cur, true);
+        VP_TS(5);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -413,9 +457,12 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
     });
     cur = nxt;
     nxt = tile_of(ti + 2);
+    VP_TS(6);
   }
   // the prefetches past the last tile (valid addresses, never read) must land before the workgroup's LDS is freed
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  VP_TS(11);
+  VP_TS_END(wave, lane);
 }
 
 namespace {
@@ -468,6 +515,8 @@ int rbconv_set(int enable) {
 
 // the HiFi-GAN wide-stage ResBlock convs: C_in = C_out in {128, 256}, K in {3, 7, 11}, stride 1, plain output
 // (not placed), one source, the ResBlock epilogues, halo <= 64 rows
+VP_TS_BINDER(rbconv_ts_bind)
+
 // the RB_EXP value this file was built with (mt_build_experiments: nonzero = a timing-experiment build)
 int rbconv_exp_flags() { return RB_EXP; }
 
