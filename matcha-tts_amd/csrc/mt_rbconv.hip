@@ -205,11 +205,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
     }
   };
 
-  f32x4 acc[4][RFN];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < RFN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[4][RFN];  // a tile's first K-slice starts from the MFMA's zero C operand (no zeroing pass)
 
   const int g4 = lane >> 4, l16 = lane & 15;
   auto swap16 = [](uint32_t& x, uint32_t& y) {
@@ -326,14 +322,15 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
     }
   };
   // NV > 0 (a VE_ACTIN pass step): NV VALU instructions placed after each MFMA, so the pass runs beside them
-  auto mma_slice = [&](const Frag& F, auto nvc) {
+  auto mma_slice = [&](const Frag& F, auto nvc, auto firstc) {
+    constexpr bool FIRST = decltype(firstc)::value;
     constexpr int NV = decltype(nvc)::value;
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
       for (int fn = 0; fn < RFN; ++fn) {
         if constexpr ((RB_EXP & 16) != 0) asm volatile("" : "+v"(acc[fm][fn]) : "v"(F.A[fm]), "v"(F.B[fn]));
-        else acc[fm][fn] = mfma16(F.A[fm], F.B[fn], acc[fm][fn]);
+        else acc[fm][fn] = mfma16(F.A[fm], F.B[fn], FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fm][fn]);
       }
     if constexpr (NV == 0) {
 #pragma unroll
@@ -430,14 +427,14 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
         VP_TS(4);
       }
       using NVP = std::integral_constant<int, (ACTIN && t == K - 2) ? RB_ACTIN_NV : 0>;
-      mma_slice(F0, NVP{});
+      mma_slice(F0, NVP{}, std::integral_constant<bool, s == 0>{});
       if constexpr (RB_DMA_AT == 1) {
         __builtin_amdgcn_sched_barrier(0);
         dma();
         __builtin_amdgcn_sched_barrier(0);
       }
       read_frag(F0, 0, slot1, xbuf1, t1);
-      mma_slice(F1, NVP{});
+      mma_slice(F1, NVP{}, std::false_type{});
       if constexpr (RB_DMA_AT == 2) {
         __builtin_amdgcn_sched_barrier(0);
         dma();
@@ -449,10 +446,6 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
         VP_TS(3);
         epilogue(cur, true);
         VP_TS(5);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < RFN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     });
     cur = nxt;

@@ -147,9 +147,12 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   std::vector<double> t(builds.size(), 0.0);
-  const int rounds = 4;
+  const int rounds = 2 * (int)builds.size();
+  // each round starts at another build: the first block of a round runs measurably slower (clock ramp after the
+  // host sync), a bias that would otherwise always fall on the base build
   for (int r = 0; r < rounds; ++r)
-    for (size_t j = 0; j < builds.size(); ++j) {
+    for (size_t jj = 0; jj < builds.size(); ++jj) {
+      const size_t j = (jj + r) % builds.size();
       CK(hipEventRecord(e0, 0));
       for (int i = 0; i < reps; ++i) builds[j].l(ef, &a, G, 0);
       CK(hipEventRecord(e1, 0));
