@@ -89,19 +89,41 @@ def launch_ranks(n, argv):
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this driver
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    import signal
+
+    def stop_all():  # every rank still alive: terminate, then kill after a grace period
+        for q in procs:
+            if q.poll() is None:
+                q.terminate()
+        deadline = time.time() + 10.0
+        for q in procs:
+            try:
+                q.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+
+    def on_term(signum, frame):  # the driver's timeout: no orphaned ranks keep holding their GPUs
+        stop_all()
+        sys.exit(128 + signum)
+
+    prev = signal.signal(signal.SIGTERM, on_term)
     rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code
-                for q in live:  # one rank failed: the job has failed, stop the ranks we started
-                    q.terminate()
-        time.sleep(0.05)
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in live:  # one rank failed: the job has failed, stop the ranks we started
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        stop_all()
+        signal.signal(signal.SIGTERM, prev)
     return rc
 
 
@@ -266,10 +288,17 @@ def roofline(probe, default_workload=True, frame_scale=1.0, pmc_name="pmc_vconv.
     gbs = nbytes / (ms * 1e-3) / 1e9
     peak_f, peak_b = PEAK_FLOPS / 1e12, PEAK_BW / 1e9
     ridge = PEAK_FLOPS / PEAK_BW
-    traffic, pmc_file = None, _latest_profile(pmc_name)
+    traffic, pmc_file, stale = None, _latest_profile(pmc_name), None
     if pmc_file and default_workload:  # the PMC passes ran this workload (pmc_name: the default or the B=256 one)
         try:
-            traffic = json.load(open(pmc_file)).get("hbm_bytes_per_launch")
+            pmc = json.load(open(pmc_file))
+            # only when they measured this run's family: same kernel sources and path knobs (tools/pmc_traffic.py)
+            sys.path.insert(0, os.path.join(HERE, "tools"))
+            from pmc_traffic import family_key
+            if pmc.get("family_key") == family_key(HERE):
+                traffic = pmc.get("hbm_bytes_per_launch")
+            else:
+                stale = f"{os.path.relpath(pmc_file, HERE)} measured another kernel build / path"
         except Exception:
             traffic = None
     if intensity >= ridge:
@@ -280,6 +309,7 @@ def roofline(probe, default_workload=True, frame_scale=1.0, pmc_name="pmc_vconv.
             "frac": round(achieved / peak, 4), "traffic": traffic,
             "traffic_ratio": round(traffic / nbytes, 3) if traffic else None,
             "traffic_source": os.path.relpath(pmc_file, HERE) if traffic else None,
+            "traffic_stale": stale,
             "kernel": "LDS-DMA implicit-GEMM convs, HiFi-GAN stage 1-4 ResBlock convs: rbconv_kernel (stages 1-2 per layer, "
                       "compile-time K loop), vpair128 (stage 2 k=3 pairs), vpair / vpair32 (stages 3-4 pairs)",
             "launches": n, "launch_ms": round(ms, 4), "flops_per_launch": flops,

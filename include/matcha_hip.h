@@ -337,8 +337,8 @@ int mtt_adam(float* p, const float* g, float* m, float* v, size_t n, const float
  * the DDP-averaged gradient), out = min(1, max_norm / (norm + 1e-6)) * inv_world (torch.nn.utils.clip_grad_norm_) */
 int mtt_clip_factor(const float* sumsq, float max_norm, float inv_world, float* out, float* norm_out, void* stream);
 /* torch.cuda.amp.GradScaler.unscale_ ("16-mixed", train_standalone.py:868): g *= inv_scale in place, and
- * *found = the number of non-finite elements of the unscaled gradient (the per-element found-inf check of
- * torch._amp_foreach_non_finite_check_and_unscale_); scratch >= 1024 floats */
+ * *found = the number of non-finite elements of g as stored, checked before the multiply (the per-element
+ * found-inf check of torch._amp_foreach_non_finite_check_and_unscale_); scratch >= 1024 floats */
 int mtt_unscale(float* g, size_t n, float inv_scale, float* found, float* scratch, void* stream);
 
 /* ---------------------------------------------------------------------------------------

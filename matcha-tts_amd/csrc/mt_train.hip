@@ -592,9 +592,9 @@ __global__ __launch_bounds__(256) void unscale_kernel(float* __restrict__ g, siz
   __shared__ float red[256];
   float bad = 0.f;
   for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-    const float v = g[i] * inv_scale;
-    g[i] = v;
-    bad += isfinite(v) ? 0.f : 1.f;
+    const float x = g[i];  // checked as stored, before the multiply (torch._amp_foreach_non_finite_check_and_unscale_)
+    bad += isfinite(x) ? 0.f : 1.f;
+    g[i] = x * inv_scale;
   }
   red[threadIdx.x] = bad;
   __syncthreads();

@@ -1311,6 +1311,11 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   // the probe site covers the HiFi-GAN ResBlock convs (k >= 3), the bench's roofline family
   const int site = a.probe ? a.probe : PROBE_VCONV;
   const bool probed = !k1 && site > 0;
+  // VE_ACTIN exists only on mt_rbconv; its producers store no activated copy, so a launch it does not take must fail
+  // here by name (the vocoder's stage_actin predicts acceptance from the same shape fields)
+  MT_REQUIRE(!(ef & VE_ACTIN) || (!k1 && !placed && BM == 128 && rbconv_handles(ef, a)),
+             "vconv: VE_ACTIN launch not taken by mt_rbconv (cin %d M %d k %d d %d B %d): stage_actin and the launch "
+             "arguments disagree", a.cin, a.M, a.taps, a.dil, a.B);
   if (!k1 && !placed && BM == 128 && rbconv_handles(ef, a)) {  // the HiFi-GAN wide-stage ResBlock convs (mt_rbconv)
     if (probed) probe_begin(site, st);
     const int rc = launch_rbconv(ef, a, G, st);

@@ -1017,9 +1017,9 @@ class MatchaTrainer:
     def optimizer_step(self):
         """gradient_clip_val 5.0 (norm of the world-averaged gradient) then torch.optim.Adam (lr, defaults).
         "16-mixed" runs Lightning's MixedPrecision sequence: GradScaler.unscale_ (the summed, loss-scaled buffer times
-        1 / (world * scale) in place, with torch's per-element found-inf check on the unscaled values), the clip on
-        the unscaled gradient, then GradScaler.step / update: a non-finite element skips the update and halves the
-        scale, ``growth_interval`` finite steps in a row double it. The found-inf flag is read on the host, as
+        1 / (world * scale) in place, with torch's per-element found-inf check on the values as stored, before the
+        multiply), the clip on the unscaled gradient, then GradScaler.step / update: a non-finite element skips the
+        update and halves the scale, ``growth_interval`` finite steps in a row double it. The found-inf flag is read on the host, as
         GradScaler.step does (``found_inf.item()``); the all-reduced buffer is the same on every rank."""
         g = self.grads.flat
         scale = empty(2, like=g)

@@ -8,9 +8,27 @@ Per kernel name, only the launches with that kernel's largest grid are used (the
 denoiser's bias-spectrum run on a 1 x 80 x 88 zero mel); the per-launch figure averages over all of them, so a
 family of kernels (vconv + vpair) is weighted by its launch mix."""
 import csv
+import hashlib
 import json
+import os
 import re
 import sys
+
+# what decides the family's HBM passes: its kernels' sources and the path knobs (bench.py attaches the traffic only
+# to a run whose own family key matches)
+FAMILY_SOURCES = ("mt_rbconv.hip", "mt_vpair.hip", "mt_vpair32.hip", "mt_vpair128.hip", "mt_vpair.h", "mt_vconv.h",
+                  "mt_vconv.hip", "mt_vocoder.hip")
+FAMILY_KNOBS = ("MT_RBCONV", "MT_ACTIN", "MT_VPAIRK", "MT_VPAIR3", "MT_XCD_TILES")
+
+
+def family_key(root):
+    h = hashlib.sha1()
+    for f in FAMILY_SOURCES:
+        with open(os.path.join(root, "matcha-tts_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    for k in FAMILY_KNOBS:
+        h.update(f"{k}={os.environ.get(k, '')};".encode())
+    return h.hexdigest()[:16]
 
 
 def per_launch(path, sub, counter):
@@ -24,12 +42,14 @@ def per_launch(path, sub, counter):
     return sum(vals) / len(vals), len(vals), sorted(set(gmax.values())), names
 
 
-fetch, nf, grid, name = per_launch(sys.argv[1], sys.argv[3], "FETCH_SIZE")
-write, nw, _, _ = per_launch(sys.argv[2], sys.argv[3], "WRITE_SIZE")
-out = {"kernels": name, "grid_sizes": grid, "launches_fetch_pass": nf, "launches_write_pass": nw,
-       "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
-       "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024)),
-       "correction": "2 x FETCH_SIZE (gfx950 reports half of wide coalesced reads) + WRITE_SIZE, KiB -> B",
-       "command": sys.argv[5]}
-json.dump(out, open(sys.argv[4], "w"), indent=1)
-print(json.dumps(out))
+if __name__ == "__main__":
+    fetch, nf, grid, name = per_launch(sys.argv[1], sys.argv[3], "FETCH_SIZE")
+    write, nw, _, _ = per_launch(sys.argv[2], sys.argv[3], "WRITE_SIZE")
+    out = {"kernels": name, "grid_sizes": grid, "launches_fetch_pass": nf, "launches_write_pass": nw,
+           "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
+           "hbm_bytes_per_launch": int(round((2 * fetch + write) * 1024)),
+           "correction": "2 x FETCH_SIZE (gfx950 reports half of wide coalesced reads) + WRITE_SIZE, KiB -> B",
+           "command": sys.argv[5],
+           "family_key": family_key(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))}
+    json.dump(out, open(sys.argv[4], "w"), indent=1)
+    print(json.dumps(out))
