@@ -74,7 +74,7 @@ constexpr int rb_tx() {
   return t < RbStage<LW>::XPW ? t : RbStage<LW>::XPW;
 }
 template <int EF>
-constexpr int rb_nst() { return 8 * ((EF & VE_DUAL) ? 2 : 1); }
+constexpr int rb_nst() { return 2 * RFN * ((EF & VE_DUAL) ? 2 : 1); }  // the epilogue's stores per wave and tile
 
 }  // namespace
 
