@@ -74,7 +74,9 @@ constexpr int rb_tx() {
   return t < RbStage<LW>::XPW ? t : RbStage<LW>::XPW;
 }
 template <int EF>
-constexpr int rb_nst() { return 2 * RFN * ((EF & VE_DUAL) ? 2 : 1); }  // the epilogue's stores per wave and tile
+constexpr int rb_nst() {  // the epilogue's stores per wave and tile
+  return 2 * RFN * ((EF & VE_DUAL) && !(EF & VE_Y2ONLY) ? 2 : 1);
+}
 
 }  // namespace
 
@@ -275,7 +277,8 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
         const int n = tl.n0 + wn * RWNC + fn * 16 + l16;
         const bool ok = real && n < L;
         const size_t o = ((size_t)tl.b * L + n) * C + tl.m0 + ch16 + fp * 32;
-        *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
+        if constexpr ((EF & VE_Y2ONLY) == 0)
+          *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
         if constexpr ((EF & VE_DUAL) != 0 && (RB_EXP & 2) == 0) {  // timing experiment 2: no y2 store
           swap16(o2[0][0], o2[1][0]);
           swap16(o2[0][1], o2[1][1]);
@@ -516,7 +519,8 @@ int rbconv_exp_flags() { return RB_EXP; }
 bool rbconv_handles(int ef, const VConvArgs& a) {
   if (!rb_knob()) return false;
   const bool eps = ef == VE_ACT || ef == (VE_ACT | VE_ACTIN) || ef == (VE_RESID | VE_DUAL) || ef == VE_RESID || ef == (VE_RESID | VE_ACCUM) ||
-                   ef == (VE_RESID | VE_ACCUM | VE_DIV) || ef == (VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL);
+                   ef == (VE_RESID | VE_ACCUM | VE_DIV) || ef == (VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL) ||
+                   ef == (VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL | VE_Y2ONLY);
   return eps && !a.f32 && (a.cin == 128 || a.cin == 256) && a.M == a.cin && a.Mpad == a.M && a.c0 == a.cin &&
          (a.taps == 3 || a.taps == 7 || a.taps == 11) && a.dil >= 1 && RBN + (a.taps - 1) * a.dil <= RXROWS &&
          a.Lout == a.L && a.ldy == a.M && a.yshift == 0 && a.ylim == a.L * a.M && a.B <= RAG_MAXB;
@@ -545,6 +549,7 @@ int launch_rbconv(int ef, const VConvArgs& a, int G, hipStream_t st) {
     MT_RB_EF(VE_RESID | VE_ACCUM)
     MT_RB_EF(VE_RESID | VE_ACCUM | VE_DIV)
     MT_RB_EF(VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL)
+    MT_RB_EF(VE_RESID | VE_ACCUM | VE_DIV | VE_DUAL | VE_Y2ONLY)
     default: set_error("rbconv: epilogue %d", ef); return -1;
   }
 #undef MT_RB_EF

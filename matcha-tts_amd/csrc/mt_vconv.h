@@ -31,6 +31,9 @@ enum : int {
   VE_ACTIN = 16384,  // mt_rbconv, with VE_ACT: the input is the RAW chain state; lrelu is applied to each staged row
                      // chunk in LDS (a pass over the chunk one step before its first use), so no producer writes an
                      // activated copy (VE_DUAL) for it
+  VE_Y2ONLY = 32768, // with VE_DUAL: store y2 only (the raw y is dead: the vocoder's stage output, whose next
+                     // upsampler reads lrelu(y) alone); mt_rbconv and the 64-channel ring pairs; every other kernel
+                     // drops the flag and stores y as well (its launcher strips it)
   VE_GNRES = 8192,   // 1x1 only, with VE_RESID: the residual is the RAW input of a GroupNorm(M/32) + Mish + mask,
                      // applied here: resid := bf16(mish(GN(resid)) * emask[frame]) with the statistics merged
                      // per tile from the producer's VE_GNSTATS partials (ResnetBlock1D block2 -> + res(x),

@@ -1311,6 +1311,8 @@ int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   // the probe site covers the HiFi-GAN ResBlock convs (k >= 3), the bench's roofline family
   const int site = a.probe ? a.probe : PROBE_VCONV;
   const bool probed = !k1 && site > 0;
+  // VE_Y2ONLY: only mt_rbconv honours it; the generic kernels store y as well (correct either way)
+  if ((ef & VE_Y2ONLY) && !(!k1 && !placed && BM == 128 && rbconv_handles(ef, a))) ef &= ~VE_Y2ONLY;
   // VE_ACTIN exists only on mt_rbconv; its producers store no activated copy, so a launch it does not take must fail
   // here by name (the vocoder's stage_actin predicts acceptance from the same shape fields)
   MT_REQUIRE(!(ef & VE_ACTIN) || (!k1 && !placed && BM == 128 && rbconv_handles(ef, a)),

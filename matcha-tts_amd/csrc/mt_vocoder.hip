@@ -331,7 +331,7 @@ int Vocoder::pair_resblock(const char* P, int i, int j, int B, int L, const char
       if (j == nk - 1) ef |= VE_DIV;
       if (j == nk - 1 && act_out) {  // lrelu(xs) for the next upsampler
         a.y2 = (bf16*)RA;
-        ef |= VE_DUAL;
+        ef |= VE_DUAL | VE_Y2ONLY;  // the upsampler reads RA alone: the raw xs is dead (not stored)
       }
     }
     if ((rc = c32 ? launch_vpair32(ef, a, st) : C == 128 ? launch_vpair128(ef, a, st) : launch_vpair(ef, a, st)))
@@ -502,7 +502,7 @@ int Vocoder::stage_vconv(const char* P, int i, int B, int L, const char* X, cons
         if (j == nk - 1) ef |= VE_DIV;
         if (j == nk - 1 && act_out) {  // lrelu(xs) for the next upsampler, in RA (this pair's conv1 read it)
           b.y2 = (bf16*)RA;
-          ef |= VE_DUAL;
+          ef |= VE_DUAL | VE_Y2ONLY;  // the upsampler reads RA alone: the raw xs is dead (not stored)
         }
       }
       if ((rc = launch_vconv(ef, b, st))) return rc;

@@ -37,7 +37,8 @@ template <int EF, int NS_, int NXP_, int FN_, int XSP_ = NS_>
 struct VpkSched {
   static constexpr int NS = NS_, S = 2 * NS, NXP = NXP_, XSP = XSP_;
   static_assert(XSP >= 1 && XSP <= NS, "rows spread over conv2's steps");
-  static constexpr int NACC = (EF & VE_ACCUM) ? 2 * FN_ : 0, NST = 2 * FN_ * ((EF & VE_DUAL) ? 2 : 1);
+  static constexpr int NACC = (EF & VE_ACCUM) ? 2 * FN_ : 0;
+  static constexpr int NST = 2 * FN_ * ((EF & VE_DUAL) && !(EF & VE_Y2ONLY) ? 2 : 1);
   static constexpr int md(int q) { return ((q % S) + S) % S; }
   static constexpr int xpieces(int q) {  // row pieces conv2's step q (tile step) issues
     int n = 0;

@@ -504,14 +504,15 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         swap16(o1[0][1], o1[1][1]);
         const bool ok = i < BN && n0 + i < L;
         const size_t o = ((size_t)b * L + n0 + i) * C + fp * 32 + ch16;
-        *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
+        if constexpr ((EF & VE_Y2ONLY) == 0)
+          *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
         if constexpr ((EF & VE_DUAL) != 0) {
           swap16(o2[0][0], o2[1][0]);
           swap16(o2[0][1], o2[1][1]);
           *reinterpret_cast<u32x4*>(ok ? a.y2 + o : a.trash + 8 * lane) = u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]};
         }
       }
-    issued += 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+    issued += 2 * FN * ((EF & VE_DUAL) && !(EF & VE_Y2ONLY) ? 2 : 1);
     VP_TS(9);
   }
   if constexpr (K > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phantom prefetches land before LDS is freed
@@ -882,6 +883,7 @@ int launch_vpair(int ef, const VPairArgs& a, hipStream_t st) {
     return !e ? 1 : !strcmp(e, "0") ? 0 : !strcmp(e, "2") ? 2 : !strcmp(e, "3") ? 3 : 1;
   }();
   const bool k3 = a.taps == 3 && a.dil <= 8 && k3mode != 0;
+  if (k3 || !(ef & VE_DUAL)) ef &= ~VE_Y2ONLY;  // only the ring kernel drops the raw store (VE_Y2ONLY)
   const int bn = !k3 ? BN : k3mode == 3 ? K3G<3, false>::BN : K3G<2, true>::BN;
   const long ntiles = (long)a.B * ((a.L + bn - 1) / bn);
   const int G = (int)std::min<long>(ntiles, vp_cu_count());
@@ -919,6 +921,9 @@ int launch_vpair(int ef, const VPairArgs& a, hipStream_t st) {
       case VE_ACCUM: ring(std::integral_constant<int, VE_ACCUM>{}); break;
       case VE_ACCUM | VE_DIV: ring(std::integral_constant<int, VE_ACCUM | VE_DIV>{}); break;
       case VE_ACCUM | VE_DIV | VE_DUAL: ring(std::integral_constant<int, VE_ACCUM | VE_DIV | VE_DUAL>{}); break;
+      case VE_ACCUM | VE_DIV | VE_DUAL | VE_Y2ONLY:
+        ring(std::integral_constant<int, VE_ACCUM | VE_DIV | VE_DUAL | VE_Y2ONLY>{});
+        break;
       case VE_DIV: ring(std::integral_constant<int, VE_DIV>{}); break;
       case VE_DIV | VE_DUAL: ring(std::integral_constant<int, VE_DIV | VE_DUAL>{}); break;
       default: set_error("vpair: epilogue %d not compiled in", ef); return -1;

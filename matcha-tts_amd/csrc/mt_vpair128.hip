@@ -510,6 +510,7 @@ static int vp128_cu_count() {
 }
 
 int launch_vpair128(int ef, const VPairArgs& a, hipStream_t st) {
+  ef &= ~VE_Y2ONLY;  // stores y as well (VE_Y2ONLY is an option, mt_vconv.h)
   MT_REQUIRE(a.x && a.w1 && a.w2 && a.b1 && a.b2 && a.y && a.zero && a.trash && a.B > 0 && a.L > 0,
              "vpair128: null argument / empty");
   MT_REQUIRE(vpair128_supported(a.taps, a.dil), "vpair128: k %d d %d", a.taps, a.dil);

@@ -354,6 +354,7 @@ static int cu_count() {
 }
 
 int launch_vpair32(int ef, const VPairArgs& a, hipStream_t st) {
+  ef &= ~VE_Y2ONLY;  // stores y as well (VE_Y2ONLY is an option, mt_vconv.h)
   MT_REQUIRE(a.x && a.w1 && a.w2 && a.b1 && a.b2 && a.y && a.zero && a.trash && a.B > 0 && a.L > 0,
              "vpair32: null argument / empty");
   MT_REQUIRE(vpair32_supported(a.taps, a.dil) && a.taps % 2 == 1, "vpair32: k %d d %d", a.taps, a.dil);

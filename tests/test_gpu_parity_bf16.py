@@ -90,9 +90,11 @@ def test_decoder_bf16_taps_bench_shape_vs_oracle(B):
     assert errs["out"] <= ac_errs["out"], (errs["out"], ac_errs["out"])
 
 
-def test_generator_bf16_no_worse_than_reference_autocast():
+@pytest.mark.parametrize("B,T", [(2, 160), (1, 728)])
+def test_generator_bf16_no_worse_than_reference_autocast(B, T):
     """HiFi-GAN in bf16 against the fp32 oracle, next to the reference's own autocast-bf16 on the same weights and
-    mel (B=2, T=160): the HIP path's drift stays within the §8c bar and at or below autocast's."""
+    mel (B=2, T=160, and one bench-length utterance, T=728 mel frames = 186k samples through every stage at full
+    tile counts): the HIP path's drift stays within the §8c bar and at or below autocast's."""
     from hifigan.config import v1
     from matcha_hip import synthetic
     from oracle import matcha_oracle as O
@@ -103,7 +105,7 @@ def test_generator_bf16_no_worse_than_reference_autocast():
     gen = gen.to(DEV).eval()
     gen.remove_weight_norm()
     gs = {k: v.cpu() for k, v in gen.state_dict().items()}
-    mel = torch.randn(2, 80, 160, generator=torch.Generator().manual_seed(9)) * 2.1 - 5.5
+    mel = torch.randn(B, 80, T, generator=torch.Generator().manual_seed(9)) * 2.1 - 5.5
     wav = gen(mel.to(DEV)).cpu()
     with torch.inference_mode():
         ref = O.generator_forward(gs, mel, v1)

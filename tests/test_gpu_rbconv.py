@@ -37,10 +37,11 @@ CASES = [
 ]
 
 
-def _run(case, rb):
+def _run(case, rb, extra_ef=0):
     from matcha_hip import runtime as rt
     C, k, dil, B, L, ef, ragged = case
     g = torch.Generator().manual_seed(C + 7 * k + 13 * dil + B + L + ef)
+    ef |= extra_ef  # flags that must not change the inputs drawn
     x = torch.randn(B, L, C, generator=g).bfloat16()
     W = (torch.randn(C, C, k, generator=g) / math.sqrt(C * k)).float()
     b = 0.1 * torch.randn(C, generator=g)
@@ -69,6 +70,29 @@ def test_rbconv_bit_identical_to_vconv(case):
     if a2 is not None:
         assert torch.equal(a2, b2)
     assert torch.isfinite(a.float()).all()
+
+
+Y2ONLY = 32768
+
+
+@pytest.mark.parametrize("C,k,dil,B,L,ragged", [(128, 11, 1, 3, 1100, True), (256, 11, 1, 2, 513, True),
+                                                (128, 7, 1, 37, 1300, False)])
+def test_rbconv_y2only_stores_the_same_y2_and_no_y(C, k, dil, B, L, ragged):
+    """VE_Y2ONLY (the vocoder's stage-output conv2 when the next upsampler reads lrelu(xs) alone, mt_vconv.h):
+    the activated copy is bit-identical to the VE_DUAL launch's and the raw y is not stored (it keeps the values
+    the VE_ACCUM epilogue read), on the compile-time-schedule kernel whose per-tile store count changes; the generic
+    kernel (mt_vconv) ignores the flag and stores y as before."""
+    case = (C, k, dil, B, L, RADD, ragged)
+    a, a2 = _run(case, True)
+    c, c2 = _run(case, True, extra_ef=Y2ONLY)
+    d, d2 = _run(case, False, extra_ef=Y2ONLY)
+    assert torch.equal(a2, c2) and torch.equal(a2, d2)
+    assert torch.equal(a, d)  # mt_vconv: y stored
+    g = torch.Generator().manual_seed(C + 7 * k + 13 * dil + B + L + RADD)
+    torch.randn(B, L, C, generator=g), torch.randn(C, C, k, generator=g), torch.randn(C, generator=g)
+    torch.randn(B, L, C, generator=g)
+    y0 = torch.randn(B, L, C, generator=g).bfloat16()
+    assert torch.equal(c, y0)  # mt_rbconv: y untouched
 
 
 def test_rbconv_runs_for_the_vocoder_convs():
