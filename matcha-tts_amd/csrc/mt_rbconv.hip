@@ -37,6 +37,10 @@
 #define RB_RAGWALK 1  // ragged tile lookup: 1 the incremental walk (mt_ragged.h RagWalk), 0 a binary search per tile
 #endif
 
+#ifndef RB_EPI_AT
+#define RB_EPI_AT 2  // the step (counted from the tile's end) that issues the epilogue's loads
+#endif
+
 #ifndef RB_DMA_AT
 #define RB_DMA_AT 1  // where a step's loader DMA issue sits: 0 after the barrier, 1 between its K-slices, 2 after both
 #endif
@@ -407,7 +411,9 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
       VP_TS(0);
       if constexpr ((RB_EXP & 8) == 0) rb_barrier();
       VP_TS(1);
-      if constexpr (s == S - 1 && (EF & (VE_RESID | VE_ACCUM)) != 0) epi_loads(cur);
+      // the epilogue's residual / old-xs loads, RB_EPI_AT steps before the tile's last (compiler-visible loads: the
+      // epilogue's use waits for them, the counted waits leave them out)
+      if constexpr (s == S - RB_EPI_AT && (EF & (VE_RESID | VE_ACCUM)) != 0) epi_loads(cur);
       auto dma = [&]() __attribute__((always_inline)) {
         if (loader && (RB_EXP & 4) == 0) {
           if constexpr (t < TX) {  // rows of the next chunk (this tile's c + 1, or the next tile's chunk 0), part t
