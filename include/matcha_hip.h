@@ -386,6 +386,10 @@ int mt_vconv_set_actin(int enable);
 int mt_ffn_set(int enable);
 /* ... on decoder levels of at least `frames` frames (B x T at that level; default 16384); returns the previous value */
 int mt_ffn_set_min_frames(int frames);
+/* Decoder kernel variants (mask; each bit-identical to the launches it replaces): bit 0 the final projection + ODE
+ * update (final_proj of mish(GroupNorm) * mask, z += dt * v) on a dedicated kernel instead of the generic conv
+ * kernel. Default 1 (MT_DECK=<mask> in the environment); process-wide; returns the previous mask. */
+int mt_decoder_set_kernels(int mask);
 /* qkv [B][T][3*heads*64], mask [B][T] -> out [B][T][heads*64], reference mask semantics */
 int mt_op_attention(int dtype, const void* qkv, const float* mask, void* out, int B, int T, int heads,
                     void* stream);

@@ -380,6 +380,7 @@ int mt_vconv_set_ct(int enable) { return mt::vconv_set_ct(enable); }
 int mt_ffn_set(int enable) { return mt::ffn_set(enable); }
 int mt_vconv_set_actin(int enable) { return mt::rbconv_actin_set(enable); }
 int mt_ffn_set_min_frames(int frames) { return mt::ffn_set_min_frames(frames); }
+int mt_decoder_set_kernels(int mask) { return mt::dec_set_kernels(mask); }
 int mt_op_vconv(const void* x, int B, int L, int cin, const float* W, const float* bias, int cout, int k, int dil,
                 int ef, const void* resid, void* y, void* y2, float slope, float div, const int32_t* lens, int pack,
                 void* ws, size_t ws_bytes, void* stream) {

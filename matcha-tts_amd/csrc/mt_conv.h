@@ -99,4 +99,10 @@ int launch_conv_dyn(int dtype, int pf, int ef, const ConvArgs& a, hipStream_t st
 // op-level entry (mt_op_conv1d): same kernels, separate symbols (TAG=1) for profiling
 int launch_conv_op(int dtype, int pf, const ConvArgs& a, hipStream_t stream, int variant = -1);
 
+// The bf16 decoder's final projection + ODE update (launch_conv<bf16, PF_GN | PF_MASK, EF_MASK | EF_EULER>'s
+// arithmetic, bit-identical) on a dedicated kernel: the GroupNorm / Mish transform in registers, the weight image
+// in LDS. Geometry: 1x1, C_in 256 -> 80 (n_feats), no ragged lengths (proj_euler_supported).
+bool proj_euler_supported(const ConvArgs& a);
+int launch_proj_euler(const ConvArgs& a, hipStream_t stream);
+
 }  // namespace mt

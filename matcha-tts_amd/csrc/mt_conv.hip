@@ -481,6 +481,158 @@ __global__ __launch_bounds__(TL::NT) void conv_kernel(ConvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// The decoder's last launch per evaluation: final_proj (1x1, 256 -> n_feats) of the final block's
+// mish(GroupNorm(conv)) * mask, times the mask, and the ODE update z += dt * v (model.py Decoder.forward's
+// final_block / final_proj, flow_matching.py solve_euler; the midpoint solver's half step). The generic
+// conv_kernel<bf16, TG6, PF_GN | PF_MASK, EF_MASK | EF_EULER> stages 128 x 128 tiles through LDS with the
+// GroupNorm + Mish transform in its commit phase, two K stages and no overlap: 30 us per launch at B = 32,
+// 174 us at B = 256 (≈ 0.55 TB/s on a 95 MB operand). Here each lane transforms in registers exactly the
+// 8-channel pieces it hands the MFMA (B operand: frame lane & 15, channels 32 ks + 8 (lane >> 4)), the
+// n_feats x 256 weight image is staged in LDS once per workgroup, and nothing else goes through LDS.
+// Workgroup: 4 waves x 16 frames of one utterance; grid (ceil(T / 64), B). Same operations in the same
+// order as the generic kernel (GroupNorm merge, transform, bf16 rounding, K order 0..255 from a zero
+// accumulator, bias, mask, update): bit-identical results.
+constexpr int PJ_C = 256;
+constexpr int PJ_ROW = PJ_C * 2 + 16;  // LDS row bytes: a fragment's 16 rows hit 16 distinct 16-byte bank slots
+
+template <int MB>  // n_feats = 16 * MB
+__global__ __launch_bounds__(256) void proj_euler_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) char wl[16 * MB * PJ_ROW];
+  __shared__ float ga[PJ_C], gsh[PJ_C], lnm[8], lnr[8];
+  constexpr int NWP = (16 * MB * (PJ_C / 8) + 255) / 256;  // 16-byte weight pieces per thread
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, kq = lane >> 4;
+  const int b = blockIdx.y, T = a.Tin;
+  const int f = blockIdx.x * 64 + wave * 16 + (lane & 15);
+  const bool fok = f < T;
+  const size_t row = (size_t)b * T + (fok ? f : T - 1);
+  // every global load first: the lane's 8 operand pieces, this thread's share of the weight image, the masks
+  const bf16* xp = reinterpret_cast<const bf16*>(a.x0) + row * PJ_C + 8 * kq;
+  Vec16<bf16> xv[PJ_C / 32];
+#pragma unroll
+  for (int ks = 0; ks < PJ_C / 32; ++ks) xv[ks] = load16(xp + 32 * ks);
+  const bf16* wp = reinterpret_cast<const bf16*>(a.w);
+  Vec16<bf16> wv[NWP];
+#pragma unroll
+  for (int i = 0; i < NWP; ++i) {
+    const int v = min(tid + 256 * i, 16 * MB * (PJ_C / 8) - 1);
+    wv[i] = load16(wp + (size_t)(v / (PJ_C / 8)) * a.cin_pad + (v % (PJ_C / 8)) * 8);
+  }
+  const float mk = a.pmask[row], em = a.emask[row];
+  // GroupNorm coefficients of utterance b (conv_kernel's pre-phase, same merge order)
+  {
+    constexpr int G = PJ_C >> 5;
+    if (tid < 64) {
+      int lpg = 64;
+      while (lpg * G > 64) lpg >>= 1;
+      const int g = tid / lpg, sub = tid % lpg;
+      double s1 = 0.0, s2 = 0.0;
+      if (g < G) {
+        const double* p = a.gn_in + (size_t)(b * G + g) * a.gn_ntiles * 2;
+        for (int i = sub; i < a.gn_ntiles; i += lpg) {
+          s1 += p[2 * i];
+          s2 += p[2 * i + 1];
+        }
+      }
+      for (int o = lpg >> 1; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      if (sub == 0 && g < G) {
+        const double n = 32.0 * (double)a.gn_T;
+        const double mean = s1 / n;
+        double var = s2 / n - mean * mean;
+        var = var < 0.0 ? 0.0 : var;
+        lnm[g] = (float)mean;
+        lnr[g] = (float)(1.0 / sqrt(var + (double)a.gn_eps));
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < PJ_C; c += 256) {
+      const int g = c >> 5;
+      const float sc = lnr[g] * a.gn_g[c];
+      ga[c] = sc;
+      gsh[c] = -sc * lnm[g] + a.gn_b[c];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NWP; ++i) {
+    const int v = tid + 256 * i;
+    if (v < 16 * MB * (PJ_C / 8))
+      store16(reinterpret_cast<bf16*>(wl + (v / (PJ_C / 8)) * PJ_ROW + (v % (PJ_C / 8)) * 16), wv[i]);
+  }
+  __syncthreads();
+  // operand: mish(GroupNorm(x)) * mask, rounded to bf16 (the generic kernel's commit transform)
+#pragma unroll
+  for (int ks = 0; ks < PJ_C / 32; ++ks) {
+    Vec16<bf16> val = xv[ks];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int cc = 32 * ks + 8 * kq + k;
+      float x = val.get(k);
+      x = mish_e<bf16>(x * ga[cc] + gsh[cc]);
+      x = x * mk;
+      val.set(k, x);
+    }
+    xv[ks] = val;
+  }
+  f32x4 acc[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) acc[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const char* abase = wl + (lane & 15) * PJ_ROW + kq * 16;
+#pragma unroll
+  for (int ks = 0; ks < PJ_C / 32; ++ks)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const Vec16<bf16> af = load16(reinterpret_cast<const bf16*>(abase + mb * 16 * PJ_ROW + ks * 64));
+      acc[mb] = mfma16(af.v, xv[ks].v, acc[mb]);
+    }
+  if (!fok) return;
+  // epilogue (conv_kernel's EF_MASK | EF_EULER): rows 16 mb + 4 (lane >> 4) + r of frame f
+  const size_t orow = (size_t)b * a.Tout + f;
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int ch = 16 * mb + 4 * kq;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = acc[mb][r] + a.bias[ch + r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = v[r] * em;
+    bf16* xz = reinterpret_cast<bf16*>(a.xin_z) + orow * a.ld_xin + ch;
+    float* zp = a.zmaster + orow * a.cout + ch;
+    const f32x4 z4 = *reinterpret_cast<const f32x4*>(zp);
+    f32x4 zn4;
+    bf16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float inc = v[r] * a.dt;
+      if (a.half_step) inc = inc * 0.5f;
+      const float zn = z4[r] + inc;
+      zn4[r] = zn;
+      o[r] = (bf16)(zn * em);  // the estimator-input slot is read as x * mask only
+    }
+    if (a.update_master) *reinterpret_cast<f32x4*>(zp) = zn4;
+    *reinterpret_cast<bf16x4*>(xz) = o;
+  }
+}
+
+bool proj_euler_supported(const ConvArgs& a) {
+  return a.taps == 1 && a.stride == 1 && a.pad == 0 && a.ups == 1 && a.cin == PJ_C && a.c0 == PJ_C &&
+         a.cin_pad == PJ_C && a.M == 80 && a.cout == 80 && a.Tout == a.Tin && a.Ncols == a.Tin && !a.lens &&
+         a.ld_xin % 4 == 0 && a.gn_ntiles > 0;
+}
+
+int launch_proj_euler(const ConvArgs& a, hipStream_t stream) {
+  MT_REQUIRE(proj_euler_supported(a), "proj_euler: geometry (1x1, 256 -> 80, no ragged lengths)");
+  MT_REQUIRE(a.x0 && a.w && a.bias && a.pmask && a.emask && a.gn_in && a.gn_g && a.gn_b && a.zmaster && a.xin_z,
+             "proj_euler: null pointer");
+  MT_REQUIRE((reinterpret_cast<uintptr_t>(a.zmaster) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.xin_z) & 7) == 0,
+             "proj_euler: z / estimator-input alignment");
+  hipLaunchKernelGGL(proj_euler_kernel<5>, dim3((unsigned)((a.Tin + 63) / 64), (unsigned)a.B), dim3(256), 0, stream, a);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
 enum : int { CFG_BIG = 1, CFG_SMALLN = 2, CFG_64 = 4, CFG_32 = 8, CFG_16 = 16, CFG_G6 = 32, CFG_C5 = 64 };

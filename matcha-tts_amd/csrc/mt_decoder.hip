@@ -9,6 +9,7 @@
 //                    Euler/midpoint update z += pred*dt written to the fp32 master and to the
 //                    estimator input slot for the next evaluation.
 #include <math.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <type_traits>
@@ -21,6 +22,20 @@
 namespace mt {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int g_deck = -1;
+int dec_kernels() {
+  if (g_deck < 0) {
+    const char* e = getenv("MT_DECK");
+    g_deck = e ? atoi(e) & DECK_ALL : DECK_ALL;
+  }
+  return g_deck;
+}
+int dec_set_kernels(int mask) {
+  const int prev = dec_kernels();
+  g_deck = mask & DECK_ALL;
+  return prev;
+}
 
 static int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
@@ -842,6 +857,8 @@ int Decoder::eval(const char* P, const Work& w, int B, int T, int ev, const Eule
   f.dt = eu.dt;
   f.half_step = eu.half_step;
   f.update_master = eu.update_master;
+  if (std::is_same<E, bf16>::value && (dec_kernels() & DECK_PROJ) && proj_euler_supported(f))
+    return launch_proj_euler(f, st);
   return launch_conv<E, PF_GN | PF_MASK, EF_MASK | EF_EULER>(f, st);
 }
 
@@ -874,7 +891,7 @@ struct Decoder::GraphCache {
   struct Entry {
     const void* P;
     const void* ws;
-    int B, T, S, n_steps, solver, uni0, uni1, vconv, gnres, uniform_attn, kpath;
+    int B, T, S, n_steps, solver, uni0, uni1, vconv, gnres, uniform_attn, kpath, deck;
     hipGraphExec_t ex;
   };
   std::vector<Entry> entries;  // most recently used last
@@ -895,12 +912,13 @@ int Decoder::chain_graph(const char* P, const Work& w, const TimeSched& ts, int 
   GraphCache& gc = *gcache;
   // kpath: the process-wide kernel selection (compile-time K loops on / off): a graph holds the kernels it captured
   const GraphCache::Entry key{P, ws, B, T, S, n_steps, solver, w.uni0, w.uni1, vconv, gnres, uniform_attn,
-                              vconv_path_id() | (ffn_on() << 3) | (std::min(ffn_min_frames(), 1 << 25) << 5), nullptr};
+                              vconv_path_id() | (ffn_on() << 3) | (std::min(ffn_min_frames(), 1 << 25) << 5),
+                              dec_kernels(), nullptr};
   for (size_t i = 0; i < gc.entries.size(); ++i) {
     const GraphCache::Entry& e = gc.entries[i];
     if (e.P == key.P && e.ws == key.ws && e.B == key.B && e.T == key.T && e.S == key.S && e.n_steps == key.n_steps &&
         e.solver == key.solver && e.uni0 == key.uni0 && e.uni1 == key.uni1 && e.vconv == key.vconv &&
-        e.gnres == key.gnres && e.uniform_attn == key.uniform_attn && e.kpath == key.kpath) {
+        e.gnres == key.gnres && e.uniform_attn == key.uniform_attn && e.kpath == key.kpath && e.deck == key.deck) {
       GraphCache::Entry hit = e;
       gc.entries.erase(gc.entries.begin() + (long)i);
       gc.entries.push_back(hit);

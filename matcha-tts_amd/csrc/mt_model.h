@@ -58,6 +58,13 @@ void gemm_geom(const GemmW& g, int Tin, int* Tout, int* Ncols);
 ConvArgs gemm_args(const GemmW& g, const char* P, int B, int Tin);
 size_t align256(size_t x);
 
+// Decoder kernel variants, each bit-identical to the launches it replaces (mt_decoder_set_kernels): DECK_PROJ the
+// final projection + ODE update on proj_euler_kernel (mt_conv.hip) instead of the generic conv kernel. On by
+// default; MT_DECK=<mask> in the environment (read once) or dec_set_kernels() to change.
+enum : int { DECK_PROJ = 1, DECK_ALL = 1 };
+int dec_kernels();
+int dec_set_kernels(int mask);  // -> the previous mask
+
 // -------------------------------------------------------------------------------------
 // U-Net estimator (model.py:834-1048) + CFM solver (model.py:1084-1109)
 // -------------------------------------------------------------------------------------

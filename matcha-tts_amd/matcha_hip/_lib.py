@@ -97,6 +97,7 @@ SIGNATURES = {
     "mt_ffn_set": (c_int, [c_int]),
     "mt_vconv_set_actin": (c_int, [c_int]),
     "mt_ffn_set_min_frames": (c_int, [c_int]),
+    "mt_decoder_set_kernels": (c_int, [c_int]),
     "mt_op_attention": (c_int, [c_int, P, P, P, c_int, c_int, c_int, P]),
     "mt_probe_start": (c_int, [c_int, c_int]),
     "mt_probe_pause": (c_int, [c_int]),

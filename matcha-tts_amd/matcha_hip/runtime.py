@@ -604,6 +604,12 @@ def set_ffn_min_frames(frames: int) -> int:
     return int(lib().mt_ffn_set_min_frames(int(frames)))
 
 
+def set_decoder_kernels(mask: int) -> int:
+    """the decoder kernel variants (bit 0: the dedicated final projection + ODE update kernel; default 1), each
+    bit-identical to what it replaces; returns the previous mask (process-wide)"""
+    return int(lib().mt_decoder_set_kernels(int(mask)))
+
+
 def set_rbconv_actin(enable: bool) -> bool:
     """the stage 1-2 ResBlock conv1s activate the raw chain state in LDS (True, default: no activated copies stored)
     or read the activated copies their producers store; returns the previous setting (process-wide)"""
