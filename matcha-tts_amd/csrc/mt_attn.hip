@@ -380,8 +380,11 @@ __global__ __launch_bounds__(256) void attn_uni_part_kernel(const bf16* __restri
 }
 
 // the utterance's attention output vector o_b (grid B): merge of the SP masked-sum slices, then the two GEMVs.
-// Every load is issued up front (the partials, this lane's V-row and out-projection weights: none depends on
-// another), so the kernel pays one memory round trip instead of three; the arithmetic and its order are unchanged.
+// Every load is issued up front, the weights first (this lane's V-row and out-projection pieces, then the
+// partials: none depends on another), so the kernel pays one memory round trip instead of three; the slice counts
+// come in as one lane-varying load (lane k: slice k) read back with v_readlane — as 32 wave-uniform loads they went
+// through the scalar cache, whose ≤ 15 outstanding loads and lgkmcnt(0) waits split the kernel into several
+// round trips (9–10 us per launch at any B). The arithmetic and its order are unchanged.
 __global__ __launch_bounds__(256) void attn_uni_vec_kernel(int SP, const float* __restrict__ part,
                                                            const bf16* __restrict__ wqkv, int mq, const float* __restrict__ bqkv,
                                                            const bf16* __restrict__ wout, const float* __restrict__ bout,
@@ -390,13 +393,6 @@ __global__ __launch_bounds__(256) void attn_uni_vec_kernel(int SP, const float* 
   const int b = blockIdx.x, tid = threadIdx.x;
   // GEMVs: 4 lanes per output row, each a quarter of K, combined by two lane shuffles
   const int q4 = tid & 3, rq = tid >> 2;  // 64 row slots per pass
-  float zz[UNI_PSMAX], nn[UNI_PSMAX];
-#pragma unroll
-  for (int k = 0; k < UNI_PSMAX; ++k) {
-    const size_t o = ((size_t)b * SP + min(k, SP - 1)) * UNI_PART;
-    zz[k] = part[o + tid];
-    nn[k] = part[o + UNI_C];
-  }
   // V rows 256 .. 383 of the LN-folded QKV image [4 chunks][mq rows][64]; lane quarter q4 = chunk q4
   u32x4 wv[2][8];
 #pragma unroll
@@ -414,13 +410,22 @@ __global__ __launch_bounds__(256) void attn_uni_vec_kernel(int SP, const float* 
 #pragma unroll
     for (int i = 0; i < 4; ++i) wo[pass][i] = *reinterpret_cast<const u32x4*>(wr + 8 * i);
   }
+  float bq[2], bo[4];  // the biases this lane's rows add (q4 == 0 lanes use them)
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) bq[pass] = bqkv[256 + rq + 64 * pass];
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) bo[pass] = bout[rq + 64 * pass];
+  float zz[UNI_PSMAX];
+#pragma unroll
+  for (int k = 0; k < UNI_PSMAX; ++k) zz[k] = part[((size_t)b * SP + min(k, SP - 1)) * UNI_PART + tid];
+  const float nl = part[((size_t)b * SP + min(tid & (UNI_PSMAX - 1), SP - 1)) * UNI_PART + UNI_C];
   {  // merge the utterance's SP part slices in order
     float z = 0.f, n = 0.f;
 #pragma unroll
     for (int k = 0; k < UNI_PSMAX; ++k)
       if (k < SP) {
         z += zz[k];
-        n += nn[k];
+        n += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nl), k));
       }
     zb[tid] = z / n;
   }
@@ -440,7 +445,7 @@ __global__ __launch_bounds__(256) void attn_uni_vec_kernel(int SP, const float* 
     for (int i = 0; i < 8; ++i) v += dot8(wv[pass][i], zb + q4 * 64 + 8 * i);
     v += __shfl_xor(v, 1, 64);
     v += __shfl_xor(v, 2, 64);
-    if (q4 == 0) vb[r] = (float)(bf16)(v + bqkv[256 + r]);
+    if (q4 == 0) vb[r] = (float)(bf16)(v + bq[pass]);
   }
   __syncthreads();
 #pragma unroll
@@ -451,7 +456,7 @@ __global__ __launch_bounds__(256) void attn_uni_vec_kernel(int SP, const float* 
     for (int i = 0; i < 4; ++i) o += dot8(wo[pass][i], vb + ck * 64 + k0 + 8 * i);
     o += __shfl_xor(o, 1, 64);
     o += __shfl_xor(o, 2, 64);
-    if (q4 == 0) ovec[(size_t)b * UNI_C + r] = o + bout[r];
+    if (q4 == 0) ovec[(size_t)b * UNI_C + r] = o + bo[pass];
   }
 }
 
