@@ -87,11 +87,15 @@ template <class T> struct Chunk { static constexpr int CH = 64 / sizeof(T); };
 // ---------------------------------------------------------------------------
 // mish(x) = x * tanh(softplus(x)); with e = exp(x): tanh(log1p(e)) = e(e+2) / (e(e+2)+2).
 // torch's softplus uses threshold 20 (returns x), where tanh(.) == 1 in fp32 anyway.
+// The quotient as n * rcp(n + 2) (v_rcp_f32, ≤ 1 ulp): built without fast-math, __fdividef compiled to the full IEEE
+// division sequence (two v_div_scale, five fma, v_div_fmas, v_div_fixup: ≈ 12 VALU per element), which made the
+// GroupNorm + Mish passes (gn_apply, the final projection's operand transform, VE_GNRES) VALU-bound. Branch-free:
+// past the threshold exp overflows and the unselected side may be NaN.
 __device__ __forceinline__ float mish_f(float x) {
-  if (x > 20.f) return x;
-  float e = __expf(x);
-  float n = e * (e + 2.f);
-  return x * __fdividef(n, n + 2.f);
+  const float e = __expf(x);
+  const float n = e * (e + 2.f);
+  const float m = x * (n * __builtin_amdgcn_rcpf(n + 2.f));
+  return x > 20.f ? x : m;
 }
 __device__ __forceinline__ float lrelu_f(float x, float slope) { return x > 0.f ? x : x * slope; }
 
