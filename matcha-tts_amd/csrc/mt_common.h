@@ -98,6 +98,16 @@ __device__ __forceinline__ float mish_f(float x) {
   return x > 20.f ? x : m;
 }
 __device__ __forceinline__ float lrelu_f(float x, float slope) { return x > 0.f ? x : x * slope; }
+// v / d as the product with rd = RN(1 / d) plus one FMA correction step (Markstein), the sign restored for v = -0
+// (the correction's +0 + -0 is +0): 4 VALU instead of the IEEE division sequence (v_div_scale x 2, v_rcp, 5 FMAs,
+// v_div_fmas, v_div_fixup). Equal to the IEEE quotient for every finite fp32 v at d = 1, 2, 3, 4, 5, 7, 8, checked
+// exhaustively on gfx950 (tools/div_check.hip; d = 6 differs on subnormal results); callers require div_rn_ok(d).
+__device__ __forceinline__ float div_rn(float v, float d, float rd) {
+  const float q = v * rd;
+  const float r = __builtin_fmaf(-q, d, v);
+  return __builtin_copysignf(__builtin_fmaf(r, rd, q), v);
+}
+inline bool div_rn_ok(float d) { return d == 1.f || d == 2.f || d == 3.f || d == 4.f || d == 5.f || d == 7.f || d == 8.f; }
 
 // bf16 epilogue helpers: two channels of one packed word as packed fp32 math (v_pk_add_f32 / v_pk_mul_f32), one
 // v_cvt_pk_bf16_f32 (RNE) per word, lrelu as max(x, slope * x) — equal to x > 0 ? x : slope * x for every non-NaN

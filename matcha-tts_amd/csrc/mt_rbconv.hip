@@ -269,7 +269,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
             f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]} + f32x2{bias4[2 * u], bias4[2 * u + 1]};
             if constexpr ((EF & VE_RESID) != 0) v = v + unpk_bf16(rr[u]);
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
-            if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
+            if constexpr ((EF & VE_DIV) != 0) v = f32x2{div_rn(v.x, a.div, 1.f / a.div), div_rn(v.y, a.div, 1.f / a.div)};
             const uint32_t rb = pk_bf16(v);
             const uint32_t av = (EF & VE_ACT) ? lrelu_pk_f_sel(v, a.slope) : (EF & VE_DUAL) ? lrelu_pk_sel(rb, a.slope) : 0u;
             o1[h][u] = (EF & VE_ACT) ? av : rb;

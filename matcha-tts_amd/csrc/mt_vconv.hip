@@ -455,7 +455,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
               f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]} + f32x2{bias4[2 * u], bias4[2 * u + 1]};
               if constexpr ((EF & VE_RESID) != 0) v = v + unpk_bf16(rr[u]);
               if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
-              if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
+              if constexpr ((EF & VE_DIV) != 0) v = f32x2{div_rn(v.x, a.div, 1.f / a.div), div_rn(v.y, a.div, 1.f / a.div)};
               if constexpr ((EF & VE_MASK) != 0) v = v * mk[fn];
               if constexpr ((EF & VE_PMASK) != 0) v = v * pmk;
               const uint32_t rb = pk_bf16(v);
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
               v = v + bf2(rr[r >> 1], r & 1);
             }
             if constexpr ((EF & VE_ACCUM) != 0) v = bf2(yy[r >> 1], r & 1) + v;
-            if constexpr ((EF & VE_DIV) != 0) v = v / a.div;
+            if constexpr ((EF & VE_DIV) != 0) v = div_rn(v, a.div, 1.f / a.div);
             if constexpr ((EF & VE_GNSTATS) != 0) {
               if (n0 + wn * WNC + fn * 16 + l16 < L) {
                 gs[fp] += (double)v;
@@ -1207,6 +1207,7 @@ static void vlaunch(const VConvArgs& a, int G, hipStream_t st) {
 
 int launch_vconv(int ef, const VConvArgs& a0, hipStream_t st) {
   MT_REQUIRE(a0.x && a0.w && a0.bias && a0.y && a0.zero && a0.trash, "vconv: null pointer");
+  MT_REQUIRE(!(ef & VE_DIV) || div_rn_ok(a0.div), "vconv: VE_DIV divisor %g outside the exactly-checked set (div_rn)", (double)a0.div);
   if (a0.f32) return launch_vconv_f32(ef, a0, st);
   MT_REQUIRE(a0.B > 0 && a0.L > 0 && a0.cin % 64 == 0 && a0.M % 64 == 0 && a0.Mpad == a0.M && a0.M <= MMAX,
              "vconv: geometry");

@@ -495,7 +495,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
             f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]} + f32x2{b4[2 * u], b4[2 * u + 1]};
             v = v + unpk_bf16(rr[u]);
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
-            if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
+            if constexpr ((EF & VE_DIV) != 0) v = f32x2{div_rn(v.x, a.div, 1.f / a.div), div_rn(v.y, a.div, 1.f / a.div)};
             o1[h][u] = pk_bf16(v);
             o2[h][u] = lrelu_pk(o1[h][u], a.slope);  // the stored state's activated copy
           }
@@ -814,7 +814,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
             f32x2 v = f32x2{acc[fm][fn][2 * u], acc[fm][fn][2 * u + 1]} + f32x2{b4[2 * u], b4[2 * u + 1]};
             v = v + unpk_bf16(rr[u]);
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
-            if constexpr ((EF & VE_DIV) != 0) v = f32x2{v.x / a.div, v.y / a.div};
+            if constexpr ((EF & VE_DIV) != 0) v = f32x2{div_rn(v.x, a.div, 1.f / a.div), div_rn(v.y, a.div, 1.f / a.div)};
             o1[h][u] = pk_bf16(v);
             o2[h][u] = lrelu_pk(o1[h][u], a.slope);  // the stored state's activated copy
           }
@@ -871,6 +871,7 @@ static int vp_cu_count() {
 }
 
 int launch_vpair(int ef, const VPairArgs& a, hipStream_t st) {
+  MT_REQUIRE(!(ef & VE_DIV) || div_rn_ok(a.div), "vpair: VE_DIV divisor %g outside the exactly-checked set (div_rn)", (double)a.div);
   MT_REQUIRE(a.x && a.w1 && a.w2 && a.b1 && a.b2 && a.y && a.zero && a.trash && a.B > 0 && a.L > 0,
              "vpair: null argument / empty");
   MT_REQUIRE(vpair_supported(C, a.taps, a.dil) && a.taps % 2 == 1, "vpair: k %d d %d", a.taps, a.dil);
