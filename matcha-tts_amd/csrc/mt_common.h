@@ -102,10 +102,13 @@ __device__ __forceinline__ float lrelu_f(float x, float slope) { return x > 0.f 
 // (the correction's +0 + -0 is +0): 4 VALU instead of the IEEE division sequence (v_div_scale x 2, v_rcp, 5 FMAs,
 // v_div_fmas, v_div_fixup). Equal to the IEEE quotient for every finite fp32 v at d = 1, 2, 3, 4, 5, 7, 8, checked
 // exhaustively on gfx950 (tools/div_check.hip; d = 6 differs on subnormal results); callers require div_rn_ok(d).
+// v = +-inf: q is the IEEE quotient +-inf itself (the correction's inf - inf would make it a NaN); |q| <= |v| for
+// d >= 1, so q is infinite only then and finite v take the 4-VALU path's result.
 __device__ __forceinline__ float div_rn(float v, float d, float rd) {
   const float q = v * rd;
   const float r = __builtin_fmaf(-q, d, v);
-  return __builtin_copysignf(__builtin_fmaf(r, rd, q), v);
+  const float c = __builtin_copysignf(__builtin_fmaf(r, rd, q), v);
+  return __builtin_isinf(q) ? q : c;
 }
 inline bool div_rn_ok(float d) { return d == 1.f || d == 2.f || d == 3.f || d == 4.f || d == 5.f || d == 7.f || d == 8.f; }
 

@@ -10,6 +10,7 @@
 // v_mfma_f32_16x16x4_f32 = an exact fp32 fmaf chain). LDS rows are padded to 80 bytes so the
 // 16-lane ds_read_b128 groups hit 16 distinct 4-bank slots (conflict-free).
 #include "mt_conv.h"
+#include "mt_probe.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -629,6 +630,10 @@ int launch_proj_euler(const ConvArgs& a, hipStream_t stream) {
              "proj_euler: z / estimator-input alignment");
   hipLaunchKernelGGL(proj_euler_kernel<5>, dim3((unsigned)((a.Tin + 63) / 64), (unsigned)a.B), dim3(256), 0, stream, a);
   MT_CHECK_HIP(hipGetLastError());
+  // launch log (tests/test_gpu_decoder_kernels.py: the dedicated kernel, not the generic conv, ran): tag 0x20000
+  const int rec[VCLOG_FIELDS] = {0x20000, 80, 64, 1, (a.Tin + 63) / 64 * a.B, (a.Tin + 63) / 64 * a.B, 1, 80, PJ_C,
+                                 a.B, a.Tin};
+  vclog_record(rec);
   return 0;
 }
 

@@ -27,16 +27,21 @@ struct VPairArgs {
 };
 
 // The compile-time K loop of the ring pair kernels (vpair_kernel<EF, K> and vpair128_kernel<EF, K>, K > 0): per wave
-// and tile of S = 2 NS steps (NS per conv), in program order: step s stages the weights of step s + 2 (2 pieces; past
+// the prologue stages the first tile's rows (NXP pieces), then the weights of steps 0 .. NWS - 2 (2 pieces each); per
+// tile of S = 2 NS steps (NS per conv), in program order: step s stages the weights of step s + NWS - 1 (2 pieces; past
 // the workgroup's last step: phantom copies of valid weights, never read) after its barrier, then step 0 the old-xs
 // loads (VE_ACCUM, 2 FN) and conv2's steps the next tile's rows (NXP pieces, piece i at conv2 step i * XSP / NXP:
 // spread among the MFMAs rather than one burst; a phantom copy of the last tile after it); the tile's epilogue stores
-// NST after step S - 1. So every vmcnt count is a constant (tests/test_vcsched.py replays the same model for mt_vconv
-// / mt_rbconv).
-template <int EF, int NS_, int NXP_, int FN_, int XSP_ = NS_>
+// NST after step S - 1. So every vmcnt count is a constant. Each instantiation a launcher uses is registered
+// (VpkReg, families 2 / 3) and replayed on the CPU against an independent model of that issue order
+// (tests/test_vcsched.py), the first-tile counts included.
+template <int EF, int NS_, int NXP_, int FN_, int XSP_ = NS_, int NWS_ = 3>
 struct VpkSched {
-  static constexpr int NS = NS_, S = 2 * NS, NXP = NXP_, XSP = XSP_;
+  static constexpr int NS = NS_, S = 2 * NS, NXP = NXP_, XSP = XSP_, NWS = NWS_;
   static_assert(XSP >= 1 && XSP <= NS, "rows spread over conv2's steps");
+  // NWS >= 3: the weights a step's wait needs (its successor's) were issued at least one step earlier; NS >= 2: the
+  // only weights the prologue stages that a wait after tile step 0 needs are step 1's, read at step 0's end
+  static_assert(NWS >= 3 && NS >= 2, "ring depth / steps per conv");
   static constexpr int NACC = (EF & VE_ACCUM) ? 2 * FN_ : 0;
   static constexpr int NST = 2 * FN_ * ((EF & VE_DUAL) && !(EF & VE_Y2ONLY) ? 2 : 1);
   static constexpr int md(int q) { return ((q % S) + S) % S; }
@@ -50,20 +55,44 @@ struct VpkSched {
   }
   static constexpr int xlast = NS + (NXP - 1) * XSP / NXP;  // the step issuing the last row piece
   static constexpr int step_ops(int q) { return 2 + after_w(q); }
-  // top of step s: the weights of step v = s + 1 (read at this step's end when s + 1 is in the same conv), else s's
+  // top of step s: the weights of step v = s + 1 (read at this step's end when s + 1 is in the same conv), else s's;
+  // step v's weights were issued first at step v - (NWS - 1)
   static constexpr int wait(int s) {
     const int v = (s % NS) + 1 < NS ? s + 1 : s;
-    int n = after_w(v - 2);
-    for (int u = v - 1; u < s; ++u) n += step_ops(u);
+    int n = after_w(v - (NWS - 1));
+    for (int u = v - (NWS - 2); u < s; ++u) n += step_ops(u);
     return n;
   }
-  // the first tile's step 0: step 1's weights are the prologue's last operation
-  static constexpr int wait_first0 = 0;
+  // the prologue's weight steps 0 .. PW - 1 follow its rows
+  static constexpr int PW = NWS - 1;
+  // the first tile's step 0 needs step 1's weights (NS >= 2): the prologue's weight steps after step 1's
+  static constexpr int wait_first0 = 2 * (PW - 2);
   // tile start: its rows (the last piece issued at the previous tile's step xlast, after that step's weights)
   static constexpr int xwait = 2 * (S - 1 - xlast) + NST;
-  static constexpr int xwait_first = 4;              // the first tile: the prologue's rows, then weights of steps 0, 1
+  static constexpr int xwait_first = 2 * PW;         // the first tile: the prologue's rows, then its weight steps
   static constexpr int accwait = 2 * (S - 1) + NXP;  // the epilogue's old-xs loads (step 0)
 };
+
+// Registry record of a ring pair kernel's schedule (SchedReg's table, mt_vconv.h; tests/test_vcsched.py): family
+// (2 mt_vpair C = 64, 3 mt_vpair128), NS, NXP, XSP, NACC, NST, NWS, EF, then 0s. Waits: w[1 + s] = wait(s) for the
+// tile steps s = 0 .. S - 1; wf = {wait_first0, xwait, xwait_first, accwait}.
+template <int FAM, class SCH, int EF>
+struct VpkReg {
+  static int waits(int* w, int* wf, int cap) {
+    if (cap < SCH::S + 1 || cap < 4) return -1;
+    w[0] = -1;
+    for (int s = 0; s < SCH::S; ++s) w[s + 1] = SCH::wait(s);
+    wf[0] = SCH::wait_first0;
+    wf[1] = SCH::xwait;
+    wf[2] = SCH::xwait_first;
+    wf[3] = SCH::accwait;
+    return SCH::S;
+  }
+  static const int reg;
+};
+template <int FAM, class SCH, int EF>
+const int VpkReg<FAM, SCH, EF>::reg =
+    sched_register({FAM, SCH::NS, SCH::NXP, SCH::XSP, SCH::NACC, SCH::NST, SCH::NWS, EF, 0, 0, 0}, &VpkReg::waits);
 
 // Round-5 pair-kernel variants, each bit-identical to the kernel it replaces (mt_vpair_set_kernels): bit 0 the
 // 64-channel compile-time-K ring kernel (vpair_kernel<EF, 7 | 11>), bit 1 the 128-channel one (vpair128_kernel<EF, 3>).

@@ -57,6 +57,10 @@ constexpr int LDS_BYTES = RAG_OFF + RAG_LDS;
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 }  // namespace
 
+// the compile-time K loop's schedule of vpair_kernel<EF, K> (K > 0; registered by launch_vpair for the CPU replay)
+template <int EF, int K>
+using VpSched = VpkSched<EF, (K > 0 ? (K + 1) / 2 : 2), XROWS / 64, FN, (K > 0 ? (K + 1) / 2 : 2), NWS>;
+
 __device__ __forceinline__ void vp_glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
@@ -285,7 +289,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   // K > 0: conv CV (0: conv1 steps 0 .. NS-1 of the tile, 1: conv2 steps NS .. S-1) unrolled: ring slots from the
   // tile's slot base sb (S % 3 != 0 rotates it per tile), counted waits (VpkSched), step barriers without an lgkmcnt
   // drain (vp_step_barrier) except a conv's first, which also publishes the activated rows / T
-  using SCH = VpkSched<EF, (K > 0 ? (K + 1) / 2 : 2), XROWS / 64, FN>;
+  using SCH = VpSched<EF, K>;
   auto slot_of = [&](int sb, int q) __attribute__((always_inline)) {  // ring slot of tile step q (q may pass S)
     const int v = sb + q % NWS;
     return v >= NWS ? v - NWS : v;
@@ -330,8 +334,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   // ---- prologue ----
   stage_x(0);
   if constexpr (K > 0) {
-    stage_w_ct(std::integral_constant<int, 0>{}, 0);
-    stage_w_ct(std::integral_constant<int, 1>{}, 1);
+    vc_for<0, SCH::PW>([&](auto qc) { stage_w_ct(qc, decltype(qc)::value); });
   } else {
 #pragma unroll
     for (int p = 0; p < NWS - 1; ++p)
@@ -913,8 +916,13 @@ int launch_vpair(int ef, const VPairArgs& a, hipStream_t st) {
     auto ring = [&](auto efc) {
       constexpr int E = decltype(efc)::value;
       if (!ctk) hipLaunchKernelGGL((vpair_kernel<E>), dim3(G), dim3(NT), 0, st, a);
-      else if (a.taps == 7) hipLaunchKernelGGL((vpair_kernel<E, 7>), dim3(G), dim3(NT), 0, st, a);
-      else if (a.taps == 11) hipLaunchKernelGGL((vpair_kernel<E, 11>), dim3(G), dim3(NT), 0, st, a);
+      else if (a.taps == 7) {
+        (void)VpkReg<2, VpSched<E, 7>, E>::reg;
+        hipLaunchKernelGGL((vpair_kernel<E, 7>), dim3(G), dim3(NT), 0, st, a);
+      } else if (a.taps == 11) {
+        (void)VpkReg<2, VpSched<E, 11>, E>::reg;
+        hipLaunchKernelGGL((vpair_kernel<E, 11>), dim3(G), dim3(NT), 0, st, a);
+      }
       else hipLaunchKernelGGL((vpair_kernel<E>), dim3(G), dim3(NT), 0, st, a);
     };
     switch (ef) {

@@ -60,6 +60,13 @@ constexpr int XPW = 7;
 #define VP128_XSP 4
 #endif
 static_assert(32 * XPW <= XROWS, "fixed row staging fits the X planes");
+}  // namespace
+
+// the compile-time K loop's schedule of vpair128_kernel<EF, K> (K > 0; registered by launch_vpair128 for the CPU replay)
+template <int EF, int K>
+using Vp128Sched = VpkSched<EF, 2 * (K > 0 ? K : 1), XPW, FN, (VP128_XSP < 2 * K ? VP128_XSP : 2 * (K > 0 ? K : 1)), NWS>;
+
+namespace {
 
 __device__ __forceinline__ void glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
@@ -277,7 +284,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   };
   // K > 0: conv CV (0: conv1 = tile steps 0 .. NS-1, 1: conv2 = NS .. S-1) unrolled; the tile's ring slots from its
   // slot base sb (S % 3 != 0 rotates it per tile)
-  using SCH = VpkSched<EF, 2 * (K > 0 ? K : 1), XPW, FN, (VP128_XSP < 2 * K ? VP128_XSP : 2 * (K > 0 ? K : 1))>;
+  using SCH = Vp128Sched<EF, K>;
   auto slot_of = [&](int sb, int q) __attribute__((always_inline)) {  // ring slot of tile step q (q may pass S)
     const int v = sb + q % NWS;
     return v >= NWS ? v - NWS : v;
@@ -317,8 +324,7 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
   // ---- prologue ----
   stage_x(0);
   if constexpr (K > 0) {
-    stage_w_ct(std::integral_constant<int, 0>{}, 0);
-    stage_w_ct(std::integral_constant<int, 1>{}, 1);
+    vc_for<0, SCH::PW>([&](auto qc) { stage_w_ct(qc, decltype(qc)::value); });
   } else {
 #pragma unroll
     for (int p = 0; p < NWS - 1; ++p)
@@ -529,7 +535,10 @@ int launch_vpair128(int ef, const VPairArgs& a, hipStream_t st) {
   const bool ct3 = a.taps == 3 && (vpair_kernels() & VPK_CTK128) != 0 && NF1 + 2 * a.dil <= 32 * XPW;
   auto go = [&](auto ec) {
     constexpr int E = decltype(ec)::value;
-    if (ct3) hipLaunchKernelGGL((vpair128_kernel<E, 3>), dim3(G), dim3(NT), 0, st, a);
+    if (ct3) {
+      (void)VpkReg<3, Vp128Sched<E, 3>, E>::reg;
+      hipLaunchKernelGGL((vpair128_kernel<E, 3>), dim3(G), dim3(NT), 0, st, a);
+    }
     else hipLaunchKernelGGL((vpair128_kernel<E>), dim3(G), dim3(NT), 0, st, a);
   };
   switch (ef) {

@@ -18,17 +18,24 @@ def _models():
     return bench.build_models(DEV, "bf16", 1234)
 
 
-def _step(models, x, xl, mask):
+PROJ_TAG = 0x20000  # launch-log record of proj_euler_kernel (mt_conv.hip launch_proj_euler)
+
+
+def _step(models, x, xl, mask, log=None):
     import bench
     from matcha_hip import runtime as rt
     m, g, den, _, _ = models
     prev = rt.set_decoder_kernels(mask)
     try:
         torch.manual_seed(7)  # the same CFM noise z for every run (synthesize draws it with torch.randn_like)
+        if log is not None:
+            rt.vconv_log_start(20000)
         with torch.inference_mode():
             mel, yl, wav = bench.step(m, g, den, x, xl, 10, True)
         torch.cuda.synchronize()
     finally:
+        if log is not None:
+            log.extend(rt.vconv_log_stop(20000))
         rt.set_decoder_kernels(prev)
     return mel.cpu(), yl.cpu(), wav.cpu()
 
@@ -39,10 +46,16 @@ def test_decoder_kernels_bit_identical_bench_step(B):
     models = _models()
     x, xl = bench.shard_inputs(0, 1, B, 4321 + B)
     x, xl = x.to(DEV), xl.to(DEV)
-    base = _step(models, x, xl, 0)
+    log0, log1 = [], []
+    base = _step(models, x, xl, 0, log0)
     assert torch.isfinite(base[0]).all()
-    for mask in (1, 1):
-        got = _step(models, x, xl, mask)
+    # the first run of each selection captures the solve's graph, so its launches are logged: the dedicated kernel
+    # ran once per ODE step with bit 0 on, never with it off (not the generic conv in both runs)
+    assert sum(r["ef"] == PROJ_TAG for r in log0) == 0
+    for i, mask in enumerate((1, 1)):
+        got = _step(models, x, xl, mask, log1 if i == 0 else None)
+        if i == 0:
+            assert sum(r["ef"] == PROJ_TAG for r in log1) == 10, len(log1)
         assert torch.equal(got[1], base[1])
         assert torch.equal(got[0], base[0]), (mask, (got[0] - base[0]).abs().max())
         assert torch.equal(got[2], base[2]), mask

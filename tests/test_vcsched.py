@@ -26,7 +26,7 @@ import ctypes
 TILES = 4  # tiles simulated after the prologue: waits recur with period 1 tile after the first
 
 
-def schedules():
+def all_schedules():
     from matcha_hip import _lib
     L = _lib.lib()
     out = []
@@ -38,6 +38,11 @@ def schedules():
         assert S > 0, _lib.lib().mt_last_error()
         out.append((list(rec), list(w)[:S + 1], list(wf)[:S + 1]))
     return out
+
+
+def schedules():
+    """The VcSched families: 0 mt_vconv's compile-time loops, 1 mt_rbconv (the ring pair kernels: test_vpksched.py)."""
+    return [s for s in all_schedules() if s[0][0] in (0, 1)]
 
 
 def issue_order(p, tiles):
@@ -163,3 +168,141 @@ def test_first_tile_needs_its_own_counts():
         assert violations(p, periodic, allowed), p
         n += 1
     assert n > 20
+
+
+# ---- the ring pair kernels (VpkSched, matcha-tts_amd/csrc/mt_vpair.h): vpair_kernel<EF, 7 | 11> (family 2, the
+# 64-channel stage-3 pairs) and vpair128_kernel<EF, 3> (family 3, stage 2's k = 3 resblock). Record: family, NS (steps
+# per conv), NXP (row pieces per wave and tile), XSP (conv2 steps the rows are spread over), NACC (old-xs loads),
+# NST (epilogue stores), NWS (weight ring slots), EF. Waits: w[1 + s] = the count at the top of tile step s,
+# wf = [first tile's step 0, tile start (rows), first tile's start, the old-xs wait before the epilogue].
+#
+# The model below is written from the kernels' loops (mt_vpair.hip / mt_vpair128.hip: the prologue, conv_ct, the
+# tile loop), not from VpkSched's formulas. Per wave, in program order:
+#   prologue: the first tile's NXP row pieces, then the weights of steps 0 .. NWS - 2 (2 pieces each);
+#   tile ti: [tile-start wait: its rows] then for each tile step st (global step g = ti * S + st):
+#     [wait: the weights of step g, and of g + 1 when it is in the same conv (its first K-slice is read at this
+#      step's end)] [the weights of step g + NWS - 1 (phantom past the last tile: still issued)]
+#     [st == 0: NACC old-xs loads] [conv2 step m = st - NS: row pieces i of the NEXT tile with i * XSP // NXP == m]
+#   then [old-xs wait, VE_ACCUM] [NST stores].
+
+def pair_schedules():
+    return [s for s in all_schedules() if s[0][0] in (2, 3)]
+
+
+def pair_replay(p, tiles):
+    """-> list of (name, tile, step, ops issued before the wait, indices of the operations it must retire)."""
+    fam, NS, NXP, XSP, NACC, NST, NWS = p[:7]
+    S = 2 * NS
+    ops, waits = [], []
+
+    def idx(pred):
+        return [k for k, o in enumerate(ops) if pred(o)]
+
+    for i in range(NXP):
+        ops.append(("x", 0, i))
+    for q in range(NWS - 1):
+        ops += [("w", q, u) for u in range(2)]
+    for ti in range(tiles):
+        waits.append(("xtop", ti, -1, len(ops), idx(lambda o: o[0] == "x" and o[1] == ti)))
+        for st in range(S):
+            g = ti * S + st
+            m = st % NS
+            need = {g, g + 1} if m + 1 < NS else {g}
+            waits.append(("step", ti, st, len(ops), idx(lambda o: o[0] == "w" and o[1] in need)))
+            ops += [("w", g + NWS - 1, u) for u in range(2)]
+            if st == 0:
+                ops += [("acc", ti, i) for i in range(NACC)]
+            if st >= NS:
+                ops += [("x", ti + 1, i) for i in range(NXP) if i * XSP // NXP == st - NS]
+        if NACC:
+            waits.append(("acc", ti, S, len(ops), idx(lambda o: o[0] == "acc" and o[1] == ti)))
+        ops += [("st", ti, i) for i in range(NST)]
+    return waits
+
+
+def pair_allowed(p, tiles):
+    """The largest count each wait may use: the operations issued after the youngest one it must retire."""
+    fam, NS, NXP, XSP, NACC = p[:5]
+    out = {}
+    for name, ti, st, n, need in pair_replay(p, tiles):
+        want = {"xtop": NXP, "acc": NACC}.get(name, 4 if st % NS + 1 < NS else 2)
+        assert len(need) == want, (p, name, ti, st, "staged pieces missing")
+        out[(name, ti, st)] = n - 1 - max(need)
+    return out
+
+
+def pair_kernel_waits(p, w, wf, tiles):
+    """The counts the kernels wait with (first tile: wait_first0 at step 0, xwait_first at its start)."""
+    NS, NACC = p[1], p[4]
+    out = {}
+    for ti in range(tiles):
+        out[("xtop", ti, -1)] = wf[2] if ti == 0 else wf[1]
+        for st in range(2 * NS):
+            out[("step", ti, st)] = wf[0] if (ti == 0 and st == 0) else w[st + 1]
+        if NACC:
+            out[("acc", ti, 2 * NS)] = wf[3]
+    return out
+
+
+def test_pair_schedules_are_registered():
+    recs = [s[0] for s in pair_schedules()]
+    # stage 3's k = 7 / 11 pairs (NS = 4 / 6) for every epilogue the vocoder launches, stage 2's k = 3 pairs
+    assert {r[1] for r in recs if r[0] == 2} == {4, 6}
+    assert {r[1] for r in recs if r[0] == 3} == {6}
+    efs = {r[7] for r in recs if r[0] == 2}
+    assert {0, 2, 6, 22, 2 | 4 | 16 | 32768} <= efs, efs  # plain, ACCUM, ACCUM|DIV, ACCUM|DIV|DUAL, ... |Y2ONLY
+
+
+def test_pair_waits_retire_what_is_read_and_are_tight():
+    for p, w, wf in pair_schedules():
+        allowed = pair_allowed(p, TILES)
+        waits = pair_kernel_waits(p, w, wf, TILES)
+        bad = [(k, waits[k], allowed[k]) for k in waits if waits[k] > allowed[k]]
+        assert not bad, (p, bad[:4])
+        # every count is exact: a tile-start, step, first-tile and old-xs wait with one more left in flight is wrong
+        for kind in ("xtop", "step", "acc"):
+            ks = [k for k in waits if k[0] == kind]
+            if ks:
+                assert any(waits[k] == allowed[k] for k in ks), (p, kind, "not tight")
+        assert waits[("step", 0, 0)] == allowed[("step", 0, 0)], (p, "wait_first0 not tight")
+        assert waits[("xtop", 0, -1)] == allowed[("xtop", 0, -1)], (p, "xwait_first not tight")
+        # the periodic waits: every tile after the first waits the same and is tight everywhere
+        for k in waits:
+            if k[1] >= 1:
+                assert waits[k] == allowed[k], (p, k, waits[k], allowed[k])
+
+
+def test_pair_off_by_one_is_caught():
+    """One more operation left in flight at ANY of the pair kernels' waits (each step's, the tile start's, the old-xs
+    wait and both first-tile counts) is flagged by the replay."""
+    n = 0
+    for p, w, wf in pair_schedules():
+        allowed = pair_allowed(p, TILES)
+        NS = p[1]
+        for s in range(2 * NS):
+            w2 = list(w)
+            w2[s + 1] += 1
+            waits = pair_kernel_waits(p, w2, wf, TILES)
+            assert any(waits[k] > allowed[k] for k in waits), (p, "wait", s)
+            n += 1
+        for j in range(4 if p[4] else 3):
+            wf2 = list(wf)
+            wf2[j] += 1
+            waits = pair_kernel_waits(p, w, wf2, TILES)
+            assert any(waits[k] > allowed[k] for k in waits), (p, "first / tile / acc", j)
+            n += 1
+    assert n > 150
+
+
+def test_pair_model_counts_the_stores_and_the_row_spread():
+    """The replay is not the formula restated: replayed as if a tile stored nothing, or with its rows issued in one
+    burst at conv2's first step, the kernels' counts are wrong somewhere."""
+    for p, w, wf in pair_schedules():
+        waits = pair_kernel_waits(p, w, wf, TILES)
+        nostore = p[:5] + [0] + p[6:]
+        allowed = pair_allowed(nostore, TILES)
+        assert any(waits[k] > allowed[k] for k in waits), p
+        if p[3] > 1:
+            burst = p[:3] + [1] + p[4:]
+            allowed = pair_allowed(burst, TILES)
+            assert any(waits[k] > allowed[k] for k in waits), p

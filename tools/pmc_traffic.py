@@ -14,18 +14,23 @@ import os
 import re
 import sys
 
-# what decides the family's HBM passes: its kernels' sources and the path knobs (bench.py attaches the traffic only
-# to a run whose own family key matches)
-FAMILY_SOURCES = ("mt_rbconv.hip", "mt_vpair.hip", "mt_vpair32.hip", "mt_vpair128.hip", "mt_vpair.h", "mt_vconv.h",
-                  "mt_vconv.hip", "mt_vocoder.hip")
+# what decides the family's HBM passes: its kernels' sources, every header they compile against (mt_common.h's
+# epilogue helpers, mt_ragged.h's tile walk, ...), the Makefile's per-file flags and the path knobs (bench.py attaches
+# the traffic only to a run whose own family key matches)
+FAMILY_SOURCES = ("mt_rbconv.hip", "mt_vpair.hip", "mt_vpair32.hip", "mt_vpair128.hip", "mt_vconv.hip",
+                  "mt_vocoder.hip")
 FAMILY_KNOBS = ("MT_RBCONV", "MT_ACTIN", "MT_VPAIRK", "MT_VPAIR3", "MT_XCD_TILES")
 
 
 def family_key(root):
     h = hashlib.sha1()
-    for f in FAMILY_SOURCES:
-        with open(os.path.join(root, "matcha-tts_amd", "csrc", f), "rb") as fh:
-            h.update(fh.read())
+    csrc = os.path.join(root, "matcha-tts_amd", "csrc")
+    headers = sorted(f for f in os.listdir(csrc) if f.endswith(".h"))
+    for f in list(FAMILY_SOURCES) + headers:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    with open(os.path.join(root, "matcha-tts_amd", "Makefile"), "rb") as fh:
+        h.update(fh.read())
     for k in FAMILY_KNOBS:
         h.update(f"{k}={os.environ.get(k, '')};".encode())
     return h.hexdigest()[:16]
