@@ -112,6 +112,19 @@ __device__ __forceinline__ float div_rn(float v, float d, float rd) {
 }
 inline bool div_rn_ok(float d) { return d == 1.f || d == 2.f || d == 3.f || d == 4.f || d == 5.f || d == 7.f || d == 8.f; }
 
+// Raw buffer resources (gfx9 dword3 0x00020000): a 32-bit per-lane byte offset from a wave-uniform base, range-checked
+// against num_records (an offset at or past it reads zero, also into LDS, and drops a store). Build them from
+// wave-uniform values only (readfirstlane what the compiler cannot prove uniform), or every access through them
+// becomes a readfirstlane loop. The LDS-DMA and store kernels (mt_rbconv, the pair kernels) put each lane's whole
+// offset in voffset, so a negative offset (a frame before the utterance) wraps past the range as well.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, unsigned num_records) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)num_records, 0x00020000);
+}
+// 16 bytes per lane into lds_wave_base + 16 * lane (buffer_load_dwordx4 ... lds)
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff, char* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff, 0, 0);
+}
+
 // bf16 epilogue helpers: two channels of one packed word as packed fp32 math (v_pk_add_f32 / v_pk_mul_f32), one
 // v_cvt_pk_bf16_f32 (RNE) per word, lrelu as max(x, slope * x) — equal to x > 0 ? x : slope * x for every non-NaN
 // x when 0 <= slope <= 1 (files using it build with -mno-amdgpu-ieee so the max needs no NaN canonicalize)

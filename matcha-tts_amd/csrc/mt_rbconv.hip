@@ -45,6 +45,17 @@
 #define RB_DMA_AT 1  // where a step's loader DMA issue sits: 0 after the barrier, 1 between its K-slices, 2 after both
 #endif
 
+#ifndef RB_BUF
+#define RB_BUF 7  // bits: LDS-DMA of 1 the weights, 2 the rows, 4 the epilogue stores through buffer resources (SGPR
+                  // bases: no per-piece 64-bit address VALU; zero padding rows and frames past L by the range check
+                  // instead of compares / selects)
+#endif
+
+#ifndef RB_LMAX
+#define RB_LMAX 1  // 1: the epilogue's lrelu as max(v, slope v) (IEEE mode off; equal to the compare / select form on
+                   // non-NaN values, which mt_vconv uses)
+#endif
+
 #ifndef RB_EXP
 #define RB_EXP 0  // timing experiments (tools/exp_build.sh, tools/rblab): bits drop parts of the work (wrong results):
                   // 1 epilogue operand loads, 2 the y2 store, 4 the K loop's DMA issue, 8 its step barriers, 16 MFMAs
@@ -161,6 +172,12 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
       tl.n0 = (r - tl.b * ntn) * RBN;
       tl.lx = L;
     }
+    // wave-uniform by construction; said so, so that the buffer resources built from them stay scalar (a resource
+    // the compiler thinks may vary per lane costs a readfirstlane loop per DMA)
+    tl.b = __builtin_amdgcn_readfirstlane(tl.b);
+    tl.n0 = __builtin_amdgcn_readfirstlane(tl.n0);
+    tl.m0 = __builtin_amdgcn_readfirstlane(tl.m0);
+    tl.lx = __builtin_amdgcn_readfirstlane(tl.lx);
     return tl;
   };
 
@@ -174,21 +191,32 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
     woff[i] = r * 128 + ((lp ^ (r & 6)) * 16);
   }
   const char* wbase = reinterpret_cast<const char*>(a.w);
+  const auto wrsrc = buf_rsrc(a.w, (unsigned)(C * C * K * 2));  // the whole [C/64][K][C][64] image
   auto issue_w = [&](const Tile& tl, int c, int t, int slot) __attribute__((always_inline)) {
-    const char* base = wbase + ((size_t)(c * K + t) * C + tl.m0) * 128;
     // the LDS destination goes through an opaque copy: with a known constant offset the compiler tracks the DMA's
     // LDS range and puts a vmcnt wait before every ds_read it cannot prove disjoint (all of them), draining the
     // prefetch each step; the ordering is ours (counted waits + barrier)
     int so = slot * RWSLOT + wave * WPW * 1024;
     asm volatile("" : "+s"(so));
+    if constexpr ((RB_BUF & 1) != 0) {
+      // the step's block (chunk c, tap t, rows m0 ..) as the scalar offset; each piece's lane offset is fixed
+      const unsigned sof = (unsigned)(((c * K + t) * C + tl.m0) * 128);
 #pragma unroll
-    for (int i = 0; i < WPW; ++i) {
-      int wo = woff[i];
-      asm volatile("" : "+v"(wo));  // per-step address (see read_frag)
-      rb_glds16(base + wo, smem + so + i * 1024);
+      for (int i = 0; i < WPW; ++i) buf_lds16(wrsrc, (unsigned)woff[i], sof, smem + so + i * 1024);
+    } else {
+      const char* base = wbase + ((size_t)(c * K + t) * C + tl.m0) * 128;
+#pragma unroll
+      for (int i = 0; i < WPW; ++i) {
+        int wo = woff[i];
+        asm volatile("" : "+v"(wo));  // per-step address (see read_frag)
+        rb_glds16(base + wo, smem + so + i * 1024);
+      }
     }
   };
   const int R = RBN + (K - 1) * dil;
+  // RB_BUF: this lane's byte offset within a row piece (row lrow, swizzled 16-byte unit lp ^ (row & 6); a piece's 8
+  // rows start at a multiple of 8, so row & 6 = lrow & 6)
+  const int xlane = lrow * C * 2 + ((lp ^ (lrow & 6)) * 16);
   // the row pieces i (of this loader wave's XPW) with i * TX / XPW == part, of chunk c of a tile
   auto issue_x = [&](const Tile& tl, int c, int buf, auto partc) __attribute__((always_inline)) {
     constexpr int part = decltype(partc)::value;
@@ -198,16 +226,29 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
     int xo = RX_OFF + buf * RXBUF;
     asm volatile("" : "+s"(xo));  // opaque LDS destination (see issue_w)
     char* dst = smem + xo;
+    if constexpr ((RB_BUF & 2) != 0) {
+      // the utterance's chunk-c columns as a buffer of its Lx valid frames: row r = frame f0 + r at byte offset
+      // (f0 + r) * 2C + 16 q, where negative offsets (f < 0) wrap past num_records, so the range check reads the
+      // conv's zero padding on both sides; rows past R are read too (in range or zero) and never used
+      const auto xr = buf_rsrc(xb, (unsigned)Lx * (unsigned)(C * 2));
 #pragma unroll
-    for (int i = 0; i < XPW; ++i) {
-      if (i * TX / XPW != part) continue;
-      const int j = wave + LW * i;
-      const int r = 8 * j + lrow;
-      const int q = lp ^ (r & 6);
-      const int f = f0 + r;
-      const bool ok = r < R && f >= 0 && f < Lx;
-      const char* src = ok ? xb + (size_t)f * C * 2 + q * 16 : reinterpret_cast<const char*>(a.zero) + q * 16;
-      rb_glds16(src, dst + j * 1024);
+      for (int i = 0; i < XPW; ++i) {
+        if (i * TX / XPW != part) continue;
+        const int j = wave + LW * i;
+        buf_lds16(xr, (unsigned)(xlane + (f0 + 8 * j) * C * 2), 0u, dst + j * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < XPW; ++i) {
+        if (i * TX / XPW != part) continue;
+        const int j = wave + LW * i;
+        const int r = 8 * j + lrow;
+        const int q = lp ^ (r & 6);
+        const int f = f0 + r;
+        const bool ok = r < R && f >= 0 && f < Lx;
+        const char* src = ok ? xb + (size_t)f * C * 2 + q * 16 : reinterpret_cast<const char*>(a.zero) + q * 16;
+        rb_glds16(src, dst + j * 1024);
+      }
     }
   };
 
@@ -241,6 +282,11 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   // mt_vconv's packed epilogue (bias, + residual, + old accumulator, / div, then lrelu / dual outputs), the same
   // operations in the same order; every lane stores (frames past L go to the trash line): RNST per tile
   auto epilogue = [&](const Tile& tl, bool real) __attribute__((always_inline)) {
+    // RB_BUF: the utterance's [L][C] rows of y / y2 from the tile's channel m0 on (in the base, not as a scalar
+    // offset: the range check then drops exactly the frames n >= L)
+    const unsigned ylim = (unsigned)L * (unsigned)(C * 2) - (unsigned)(tl.m0 * 2);
+    const auto yr = buf_rsrc(a.y + (size_t)tl.b * L * C + tl.m0, ylim);
+    const auto y2r = buf_rsrc(((EF & VE_DUAL) ? a.y2 : a.y) + (size_t)tl.b * L * C + tl.m0, ylim);
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -271,7 +317,9 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
             if constexpr ((EF & VE_ACCUM) != 0) v = unpk_bf16(yy[u]) + v;
             if constexpr ((EF & VE_DIV) != 0) v = f32x2{div_rn(v.x, a.div, 1.f / a.div), div_rn(v.y, a.div, 1.f / a.div)};
             const uint32_t rb = pk_bf16(v);
-            const uint32_t av = (EF & VE_ACT) ? lrelu_pk_f_sel(v, a.slope) : (EF & VE_DUAL) ? lrelu_pk_sel(rb, a.slope) : 0u;
+            uint32_t av = 0u;
+            if constexpr (RB_LMAX) av = (EF & VE_ACT) ? lrelu_pk_f(v, a.slope) : (EF & VE_DUAL) ? lrelu_pk(rb, a.slope) : 0u;
+            else av = (EF & VE_ACT) ? lrelu_pk_f_sel(v, a.slope) : (EF & VE_DUAL) ? lrelu_pk_sel(rb, a.slope) : 0u;
             o1[h][u] = (EF & VE_ACT) ? av : rb;
             o2[h][u] = av;
           }
@@ -279,6 +327,19 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
         swap16(o1[0][0], o1[1][0]);
         swap16(o1[0][1], o1[1][1]);
         const int n = tl.n0 + wn * RWNC + fn * 16 + l16;
+        if constexpr ((RB_BUF & 4) != 0) {
+          // the utterance's [L][C] output as a buffer: frames past L fall outside the range (store dropped); every
+          // lane still issues its store, so the counted waits' NST is unchanged
+          const unsigned vo = (unsigned)((n * C + ch16 + fp * 32) * 2);
+          if constexpr ((EF & VE_Y2ONLY) == 0)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]}, yr, vo, 0, 0);
+          if constexpr ((EF & VE_DUAL) != 0 && (RB_EXP & 2) == 0) {
+            swap16(o2[0][0], o2[1][0]);
+            swap16(o2[0][1], o2[1][1]);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]}, y2r, vo, 0, 0);
+          }
+          continue;
+        }
         const bool ok = real && n < L;
         const size_t o = ((size_t)tl.b * L + n) * C + tl.m0 + ch16 + fp * 32;
         if constexpr ((EF & VE_Y2ONLY) == 0)

@@ -31,6 +31,11 @@
 #include "mt_ts.h"
 #include "mt_vpair.h"
 
+#ifndef VP_BUF
+#define VP_BUF 1  // 1: the compile-time ring kernel's LDS-DMA and every pair kernel's y / y2 stores through buffer resources
+                  // (mt_common.h buf_rsrc: no per-piece 64-bit address VALU, zero padding by the range check)
+#endif
+
 #ifndef VPAIR_EXP
 #define VPAIR_EXP 0  // timing experiments (tools/exp_build.sh): bits drop parts of the pair kernels' work
 #endif
@@ -143,6 +148,10 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     return t;
   };
   RagTile nxt;  // the tile stage_x staged last (the next tile of the loop)
+  // VP_BUF: this lane's byte offsets within a weight piece (row 8 wave + lrow of a tap block) and a row piece (row
+  // lrow of 8); the 16-byte unit is swizzled by row & 6 = lrow & 6 in both
+  const int wlane = (8 * wave + lrow) * 128 + ((lp ^ (lrow & 6)) * 16);
+  const int xlane = lrow * 128 + ((lp ^ (lrow & 6)) * 16);
   auto stage_w = [&](int s) {  // taps 2m, 2m+1 (clamped to k-1) of conv1 or conv2, m = step within the conv
     const int r2 = s % (2 * ns);
     const int m = r2 < ns ? r2 : r2 - ns;
@@ -167,21 +176,36 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     asm volatile("" : "+s"(so));
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const bf16* base = w + (size_t)min(2 * m + u, k - 1) * C * 64;
-      int off = r * 64 + (lp ^ (r & 6)) * 8;
-      asm volatile("" : "+v"(off));
-      vp_glds16(base + off, smem + so + u * TAPW);
+      if constexpr (VP_BUF && K > 0) {
+        // tap block min(2m + u, k - 1) as the scalar offset, the lane's row unit as the (fixed) vector offset
+        const auto wr = buf_rsrc(w, (unsigned)(K * C * 64 * 2));
+        const unsigned tb = (unsigned)((2 * m + u < K - 1 ? 2 * m + u : K - 1) * C * 64 * 2);
+        buf_lds16(wr, (unsigned)wlane, tb, smem + so + u * TAPW);
+      } else {
+        const bf16* base = w + (size_t)min(2 * m + u, k - 1) * C * 64;
+        int off = r * 64 + (lp ^ (r & 6)) * 8;
+        asm volatile("" : "+v"(off));
+        vp_glds16(base + off, smem + so + u * TAPW);
+      }
     }
   };
   const bf16* sx_xb = a.x;
   int sx_f0 = 0, sx_lv = 0;
   auto stage_x_begin = [&](int ti) {
     nxt = tile_of(K > 0 ? min(ti, nmine - 1) : ti);  // K > 0: past the last tile a phantom copy of it (never read)
-    sx_xb = a.x + (size_t)nxt.b * L * C;
-    sx_f0 = nxt.n0 - HALO2 - h1, sx_lv = nxt.lv;
+    sx_xb = a.x + (size_t)__builtin_amdgcn_readfirstlane(nxt.b) * L * C;
+    sx_f0 = __builtin_amdgcn_readfirstlane(nxt.n0 - HALO2 - h1), sx_lv = __builtin_amdgcn_readfirstlane(nxt.lv);
   };
   auto stage_x_piece = [&](int i) {  // this wave's row piece i (rows 8 j .. 8 j + 7, j = wave + 8 i)
     const int j = wave + 8 * i;
+    if constexpr (VP_BUF && K > 0) {
+      // the utterance as a buffer of its sx_lv valid frames: row r = frame sx_f0 + r; offsets of frames before the
+      // utterance wrap past the range, so the range check reads the zero padding on both sides (rows past
+      // NF1 + 2 h1 are staged too and never read)
+      buf_lds16(buf_rsrc(sx_xb, (unsigned)sx_lv * (C * 2)), (unsigned)(xlane + (sx_f0 + 8 * j) * C * 2), 0u,
+                smem + j * 1024);
+      return;
+    }
     const int r = 8 * j + lrow;
     const int q = lp ^ (r & 6);
     const int f = sx_f0 + r;
@@ -467,6 +491,10 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fp][fn]));  // no use of yv before the wait
     }
     VP_TS(8);
+    static_assert(BN == 8 * WNC - 16 && WNC > 16, "only the last wave's last fragment lies past BN");
+    const size_t ybase = (size_t)__builtin_amdgcn_readfirstlane(b) * L * C;
+    const auto yr = buf_rsrc(a.y + ybase, (unsigned)L * (C * 2));
+    const auto y2r = buf_rsrc(((EF & VE_DUAL) ? a.y2 : a.y) + ybase, (unsigned)L * (C * 2));
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -505,6 +533,20 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
         }
         swap16(o1[0][0], o1[1][0]);
         swap16(o1[0][1], o1[1][1]);
+        if constexpr (VP_BUF) {
+          // the utterance's [L][C] output as a buffer: frames past L fall outside it (store dropped); the discarded
+          // frames i >= BN (the last wave's last fragment) get an offset past any range; every lane still stores
+          const bool keep = !(fn == FN - 1 && wave == 7);
+          const unsigned vo = keep ? (unsigned)(((n0 + i) * C + fp * 32 + ch16) * 2) : 0x80000000u;
+          if constexpr ((EF & VE_Y2ONLY) == 0)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]}, yr, vo, 0, 0);
+          if constexpr ((EF & VE_DUAL) != 0) {
+            swap16(o2[0][0], o2[1][0]);
+            swap16(o2[0][1], o2[1][1]);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]}, y2r, vo, 0, 0);
+          }
+          continue;
+        }
         const bool ok = i < BN && n0 + i < L;
         const size_t o = ((size_t)b * L + n0 + i) * C + fp * 32 + ch16;
         if constexpr ((EF & VE_Y2ONLY) == 0)

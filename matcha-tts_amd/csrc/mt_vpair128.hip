@@ -60,6 +60,9 @@ constexpr int XPW = 7;
 #define VP128_XSP 4
 #endif
 static_assert(32 * XPW <= XROWS, "fixed row staging fits the X planes");
+#ifndef VP128_BUF
+#define VP128_BUF 1  // 1: the compile-time kernel's LDS-DMA and the y / y2 stores through buffer resources (mt_common.h)
+#endif
 }  // namespace
 
 // the compile-time K loop's schedule of vpair128_kernel<EF, K> (K > 0; registered by launch_vpair128 for the CPU replay)
@@ -153,6 +156,10 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
     return t;
   };
   RagTile nxt;  // the tile stage_x staged last (the next tile of the loop)
+  // VP128_BUF: this lane's byte offsets within a weight piece (row 16 wave + lrow of the step's block; + 8 rows for
+  // the second piece) and a row piece (row lrow of 8 of one plane); the 16-byte unit is swizzled by lrow & 6
+  const int wlane = (16 * wave + lrow) * 128 + ((lp ^ (lrow & 6)) * 16);
+  const int xlane = lrow * (C * 2) + ((lp ^ (lrow & 6)) * 16);
   auto stage_w = [&](int s) {  // step m of conv1 or conv2: image block (chunk m / k, tap m % k)
     const int r2 = s % (2 * ns);
     const int m = r2 < ns ? r2 : r2 - ns;
@@ -175,21 +182,35 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
     asm volatile("" : "+s"(so));
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int r = 16 * wave + 8 * u + lrow;
-      int off = r * 64 + (lp ^ (r & 6)) * 8;
-      asm volatile("" : "+v"(off));
-      glds16(w + off, smem + so + 8 * u * 128);
+      if constexpr (VP128_BUF && K > 0) {
+        // the step's [C][64] block as the scalar offset, the lane's row unit as the (fixed) vector offset
+        const auto wr = buf_rsrc(q < NSK ? a.w1 : a.w2, (unsigned)(NSK * C * 64 * 2));
+        buf_lds16(wr, (unsigned)(wlane + u * 8 * 128), (unsigned)(m * C * 64 * 2), smem + so + 8 * u * 128);
+      } else {
+        const int r = 16 * wave + 8 * u + lrow;
+        int off = r * 64 + (lp ^ (r & 6)) * 8;
+        asm volatile("" : "+v"(off));
+        glds16(w + off, smem + so + 8 * u * 128);
+      }
     }
   };
   const bf16* sx_xb = a.x;
   int sx_f0 = 0, sx_lv = 0;
   auto stage_x_begin = [&](int ti) {
     nxt = tile_of(K > 0 ? min(ti, nmine - 1) : ti);  // K > 0: past the last tile a phantom copy of it (never read)
-    sx_xb = a.x + (size_t)nxt.b * L * C;
-    sx_f0 = nxt.n0 - h2 - h1, sx_lv = nxt.lv;
+    sx_xb = a.x + (size_t)__builtin_amdgcn_readfirstlane(nxt.b) * L * C;
+    sx_f0 = __builtin_amdgcn_readfirstlane(nxt.n0 - h2 - h1), sx_lv = __builtin_amdgcn_readfirstlane(nxt.lv);
   };
   auto stage_x_piece = [&](int j) {  // rows 8 blk .. 8 blk + 7 of plane p (j = 2 blk + p)
     const int p = j & 1, blk = j >> 1;
+    if constexpr (VP128_BUF && K > 0) {
+      // the utterance as a buffer of its sx_lv valid frames: row r = frame sx_f0 + r, plane p = channels 64 p ..;
+      // offsets of frames before the utterance wrap past the range (zero padding on both sides); rows past R1 are
+      // staged too and never read
+      buf_lds16(buf_rsrc(sx_xb, (unsigned)sx_lv * (C * 2)), (unsigned)(xlane + (sx_f0 + 8 * blk) * C * 2 + p * 128), 0u,
+                smem + X_OFF + p * XPL + blk * 1024);
+      return;
+    }
     const int r = 8 * blk + lrow;
     const int q = lp ^ (r & 6);
     const int f = sx_f0 + r;
@@ -449,6 +470,9 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
         for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fp][fn]));  // no use of yv before the wait
     }
     VP_TS(8);
+    const size_t ybase = (size_t)__builtin_amdgcn_readfirstlane(b) * L * C;
+    const auto yr = buf_rsrc(a.y + ybase, (unsigned)L * (C * 2));
+    const auto y2r = buf_rsrc(((EF & VE_DUAL) ? a.y2 : a.y) + ybase, (unsigned)L * (C * 2));
 #pragma unroll
     for (int fp = 0; fp < 2; ++fp)
 #pragma unroll
@@ -483,6 +507,18 @@ __global__ __launch_bounds__(NT) void vpair128_kernel(VPairArgs a) {
         }
         swap16(o1[0][0], o1[1][0]);
         swap16(o1[0][1], o1[1][1]);
+        if constexpr (VP128_BUF) {
+          // the utterance's [L][C] output as a buffer: frames past L fall outside it (store dropped), the tile's
+          // discarded frames i >= BN get an offset past any range; every lane still stores
+          const unsigned vo = i < BN ? (unsigned)(((n0 + i) * C + wm * 64 + fp * 32 + ch16) * 2) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]}, yr, vo, 0, 0);
+          if constexpr ((EF & VE_DUAL) != 0) {
+            swap16(o2[0][0], o2[1][0]);
+            swap16(o2[0][1], o2[1][1]);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]}, y2r, vo, 0, 0);
+          }
+          continue;
+        }
         const bool ok = i < BN && n0 + i < L;
         const size_t o = ((size_t)b * L + n0 + i) * C + wm * 64 + fp * 32 + ch16;
         *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};

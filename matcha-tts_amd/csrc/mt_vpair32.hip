@@ -54,6 +54,10 @@ static_assert(XROWS % 128 == 0 && TAPW == 2 * 1024, "two 1 KiB DMAs per tap");
 
 __device__ __forceinline__ int swz(int r) { return (r >> 1) & 2; }
 
+#ifndef VP32_BUF
+#define VP32_BUF 1  // 1: row staging and the y / y2 stores through buffer resources (mt_rbconv's RB_BUF)
+#endif
+
 __device__ __forceinline__ void glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
@@ -133,8 +137,30 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     }
   };
   // raw rows of tile ti: row r = frame n0 - HALO2 - h1 + r (zero rows past this workgroup's last tile)
+  // VP32_BUF: this lane's byte offset within a 16-row piece (row lrow, 16-byte chunk lp ^ swz(row); a piece starts
+  // at a multiple of 16 rows, so swz(row) = swz(lrow))
+  const int xlane = lrow * RB + ((lp ^ swz(lrow)) * 16);
   auto stage_x = [&](int ti) __attribute__((always_inline)) {
     nxt = tile_of(ti);
+    if constexpr (VP32_BUF) {
+      // the utterance as a buffer of its lv valid frames (past the workgroup's last tile: an empty one, zero rows):
+      // row r = frame f0 + r at byte offset (f0 + r) * RB; negative offsets wrap past num_records, so the range
+      // check reads the conv's zero padding on both sides; rows past R1 are staged too and never read
+      const int b = __builtin_amdgcn_readfirstlane(nxt.b);
+      const int f0 = __builtin_amdgcn_readfirstlane(nxt.n0 - HALO2 - h1);
+      const unsigned nrec = ti < nmine ? (unsigned)__builtin_amdgcn_readfirstlane(nxt.lv) * RB : 0u;
+      const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(a.x + (size_t)b * L * C), (short)0, (int)nrec,
+                                                        0x00020000);
+#pragma unroll
+      for (int i = 0; i < XROWS / 128; ++i) {
+        const int j = wave + 8 * i;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(smem + j * 1024), 16,
+                                                 (unsigned)(xlane + (f0 + 16 * j) * RB), 0, 0, 0);
+      }
+      issued += XROWS / 128;
+      xmk = issued;
+      return;
+    }
     const bool live = ti < nmine;
     const bf16* xb = a.x + (size_t)(live ? nxt.b : 0) * L * C;
     const int f0 = nxt.n0 - HALO2 - h1, R1 = live ? NF1 + 2 * h1 : 0, lv = nxt.lv;
@@ -290,6 +316,11 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+v"(yv[fn]));  // no use of yv before the wait
     }
     VP_TS(8);
+    static_assert(BN == 8 * WNC - 16, "only the last wave's last fragment lies past BN");
+    const int bu = __builtin_amdgcn_readfirstlane(b);
+    const auto yr = __builtin_amdgcn_make_buffer_rsrc(a.y + (size_t)bu * L * C, (short)0, (int)((unsigned)L * RB), 0x00020000);
+    const auto y2r = __builtin_amdgcn_make_buffer_rsrc(((EF & VE_DUAL) ? a.y2 : a.y) + (size_t)bu * L * C, (short)0,
+                                                       (int)((unsigned)L * RB), 0x00020000);
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       const int i = wave * WNC + fn * 16 + l16;  // output frame n0 + i
@@ -321,6 +352,20 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       }
       swap16(o1[0][0], o1[1][0]);
       swap16(o1[0][1], o1[1][1]);
+      if constexpr (VP32_BUF) {
+        // the utterance's [L][C] output as a buffer: frames past L fall outside it (store dropped); the discarded
+        // frames i >= BN of the last wave's last fragment get an offset past any range (every lane still stores, so
+        // the issue counts are unchanged)
+        const bool keep = !(fn == FN - 1 && wave == 7);
+        const unsigned vo = keep ? (unsigned)(((n0 + i) * C + ch16) * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]}, yr, vo, 0, 0);
+        if constexpr ((EF & VE_DUAL) != 0) {
+          swap16(o2[0][0], o2[1][0]);
+          swap16(o2[0][1], o2[1][1]);
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]}, y2r, vo, 0, 0);
+        }
+        continue;
+      }
       const bool ok = i < BN && n0 + i < L;
       const size_t o = ((size_t)b * L + n0 + i) * C + ch16;
       *reinterpret_cast<u32x4*>(ok ? a.y + o : a.trash + 8 * lane) = u32x4{o1[0][0], o1[0][1], o1[1][0], o1[1][1]};
