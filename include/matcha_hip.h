@@ -87,6 +87,11 @@ int mt_encoder_set_mfma_attention(mt_encoder* e, int enable);
 /* fp32: 1 (default) runs the prenet / attention-projection / FFN / duration-predictor convs on mt_vconv's fp32 mode
  * (LDS-DMA staging, exact-fp32 MFMA); 0 = the generic implicit-GEMM kernel (A/B, tests). Same arithmetic. */
 int mt_encoder_set_vconv(mt_encoder* e, int enable);
+/* fp32 encoder: 1 runs the FFN convs (model.py:375-393; TextEncoder precision "fp32x3") in mt_vconv's split-bf16 mode:
+ * every fp32 operand is the sum of three bf16 parts and each fp32 product the sum of the six bf16 MFMA products whose
+ * parts reach 2^-16, accumulated in fp32 (the reference's fp32 to a few ulp, at 16x the fp32 MFMA rate per product);
+ * 0 (default) = exact fp32 MFMA. Not a bf16 encoder: its logw stays within 1e-5 of the fp32 reference. */
+int mt_encoder_set_split(mt_encoder* e, int enable);
 /* oov (nullable, device int32): set to 0, then to 1 when any id of x (padding included) lies outside [0, n_vocab):
  * nn.Embedding's IndexError (model.py:522); the caller raises at its next host sync. The embedding reads a clamped
  * row for such an id, so the launch itself stays in bounds. */

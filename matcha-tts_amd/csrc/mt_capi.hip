@@ -111,6 +111,12 @@ int mt_encoder_set_vconv(mt_encoder* e, int enable) {
   e->e.f32vc = enable ? 1 : 0;
   return 0;
 }
+int mt_encoder_set_split(mt_encoder* e, int enable) {
+  MT_REQUIRE(e, "null encoder");
+  MT_REQUIRE(!enable || e->e.dtype == mt::F32, "encoder_set_split: the split-bf16 FFN is an fp32-encoder mode");
+  e->e.split = enable ? 1 : 0;
+  return 0;
+}
 int mt_encoder_forward(const mt_encoder* e, const void* packed, const int64_t* x, const int64_t* x_lengths,
                        const float* spks, int B, int Tx, float* mu, float* logw, float* x_mask, int32_t* oov,
                        void* ws, size_t ws_bytes, void* stream) {

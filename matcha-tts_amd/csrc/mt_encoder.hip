@@ -49,7 +49,7 @@ template <class E, int VPL>
 __global__ __launch_bounds__(256) void rowln_kernel(const E* __restrict__ x, int rows, int C,
                                                     const float* __restrict__ g, const float* __restrict__ bt,
                                                     float eps, const float* __restrict__ mask, int relu,
-                                                    E* __restrict__ y) {
+                                                    E* __restrict__ y, bf16* __restrict__ ys) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -79,6 +79,13 @@ __global__ __launch_bounds__(256) void rowln_kernel(const E* __restrict__ x, int
     float o = (v[i] - mean) * rstd * g[c] + bt[c];
     if (relu) o = fmaxf(o, 0.f);
     y[(size_t)row * C + c] = from_f<E>(o * m);
+    if (ys) {  // the split-bf16 convs' input (VConvArgs::f32 == 2): planes h1 h1 h1 h2 h2 h3 of the stored value
+      bf16 h[3];
+      split3_bf16((float)from_f<E>(o * m), h[0], h[1], h[2]);
+      bf16* yr = ys + (size_t)row * 6 * C + c;
+#pragma unroll
+      for (int pl = 0; pl < 6; ++pl) yr[pl * C] = h[pl < 3 ? 0 : pl < 5 ? 1 : 2];
+    }
   }
 }
 
@@ -588,8 +595,14 @@ int Encoder::init(int n_vocab_, int n_ch, int filt, int heads_, int layers_, int
     };
     for (Pre& q : pre) vc32(q.conv);
     if (prenet) vc32(pre_proj);
-    for (Layer& l : lay)
+    for (Layer& l : lay) {
       for (GemmW* g : {&l.qkv, &l.o, &l.f1, &l.f2}) vc32(*g);
+      // the FFN convs' split-bf16 images (encoder precision "fp32x3", Encoder::split): 6 cin input channels
+      if (l.f1.vc && l.f2.vc && (6 * l.f1.cin) % 384 == 0 && (6 * l.f2.cin) % 384 == 0 && l.f1.k >= 2 && l.f2.k >= 2) {
+        l.s1_off = pk.take(vconv_packed_bytes_split6(l.f1.cin, l.f1.cout, l.f1.k));
+        l.s2_off = pk.take(vconv_packed_bytes_split6(l.f2.cin, l.f2.cout, l.f2.k));
+      }
+    }
     vc32(dp1);
     vc32(dp2);
   }
@@ -638,8 +651,13 @@ int Encoder::pack(const float* const* p, void* packed, hipStream_t st) const {
     };
     for (const Pre& q : pre) PK(rp(q.conv));
     if (prenet) PK(rp(pre_proj));
-    for (const Layer& l : lay)
+    for (const Layer& l : lay) {
       for (const GemmW* g : {&l.qkv, &l.o, &l.f1, &l.f2}) PK(rp(*g));
+      if (l.s1_off) {
+        PK(vconv_repack_split6(P + l.f1.w_off, l.f1.Mpad, l.f1.taps, l.f1.cin_pad, l.f1.cin, l.f1.cout, P + l.s1_off, st));
+        PK(vconv_repack_split6(P + l.f2.w_off, l.f2.Mpad, l.f2.taps, l.f2.cin_pad, l.f2.cin, l.f2.cout, P + l.s2_off, st));
+      }
+    }
     PK(rp(dp1));
     PK(rp(dp2));
   }
@@ -648,22 +666,26 @@ int Encoder::pack(const float* const* p, void* packed, hipStream_t st) const {
   return 0;
 }
 
+// the split-bf16 FFN's 6-plane operands (LN1 output, hidden), bf16
+static size_t split_ws(bool on, size_t n, int W, int F) { return on ? align256(n * 6 * W * 2) + align256(n * 6 * F * 2) : 0; }
+
 size_t Encoder::workspace_bytes(int B, int Tx) const {
   const size_t n = (size_t)B * Tx;
   const int wmax = std::max(std::max(W, 3 * W), std::max(F, DF));
-  return 5 * align256(n * wmax * esize) + align256(n * 80 * esize) + align256(n * 4) + 4096;  // + vconv trash
+  return 5 * align256(n * wmax * esize) + align256(n * 80 * esize) + align256(n * 4) + 4096 +  // + vconv trash
+         split_ws(split && dtype == F32, n, W, F);
 }
 
 template <class E>
 static int rowln(const E* x, int rows, int C, const float* gb, float eps, const float* mask, int relu, E* y,
-                 hipStream_t st) {
+                 hipStream_t st, bf16* ys = nullptr) {
   const dim3 grid((rows + 3) / 4), blk(256);
   if (C <= 256)
-    hipLaunchKernelGGL((rowln_kernel<E, 4>), grid, blk, 0, st, x, rows, C, gb, gb + C, eps, mask, relu, y);
+    hipLaunchKernelGGL((rowln_kernel<E, 4>), grid, blk, 0, st, x, rows, C, gb, gb + C, eps, mask, relu, y, ys);
   else if (C <= 512)
-    hipLaunchKernelGGL((rowln_kernel<E, 8>), grid, blk, 0, st, x, rows, C, gb, gb + C, eps, mask, relu, y);
+    hipLaunchKernelGGL((rowln_kernel<E, 8>), grid, blk, 0, st, x, rows, C, gb, gb + C, eps, mask, relu, y, ys);
   else
-    hipLaunchKernelGGL((rowln_kernel<E, 16>), grid, blk, 0, st, x, rows, C, gb, gb + C, eps, mask, relu, y);
+    hipLaunchKernelGGL((rowln_kernel<E, 16>), grid, blk, 0, st, x, rows, C, gb, gb + C, eps, mask, relu, y, ys);
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -832,6 +854,40 @@ int Encoder::forward_t(const char* P, const long long* ids, const long long* xle
     // FFN (model.py:375-393) on masked operands: LN1 stores x*m, conv 1 stores relu(.)*m, conv 2 adds the
     // (masked) residual and masks; valid frames are unchanged (the reference's unmasked residual only reaches
     // padded frames, which LN2's mask zeroes), and no conv needs a mask prologue
+    if (std::is_same<E, float>::value && split && f32vc && l.s1_off) {
+      // split-bf16 ("fp32x3"): LN1 stores A (fp32, conv 2's residual) and its 6-plane split A6; conv 1 stores the
+      // hidden as its 6-plane split H6; conv 2 sums its six bf16 products per fp32 product in fp32 (mt_vconv.h f32 2)
+      bf16* A6 = (bf16*)(trash + 4096);
+      bf16* H6 = (bf16*)((char*)A6 + align256(n * 6 * W * 2));
+      if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n1_off), eps, xmask, 0, (E*)A, st, A6))) return rc;
+      auto sargs = [&](const GemmW& g, size_t s_off, const void* x, void* y) {
+        VConvArgs a{};
+        a.f32 = 2;
+        a.x = (const bf16*)x;
+        a.B = B;
+        a.L = Tx;
+        a.cin = 6 * g.cin;
+        a.w = (const bf16*)(P + s_off);
+        a.bias = (const float*)(P + g.b_off);
+        a.M = a.Mpad = g.cout;
+        a.taps = g.k;
+        a.dil = 1;
+        a.pad = g.pad;
+        a.y = (bf16*)y;
+        a.emask = xmask;
+        a.div = 1.f;
+        a.zero = (const bf16*)(P + ezero_off);
+        a.trash = (bf16*)trash;
+        a.probe = -1;
+        return a;
+      };
+      if ((rc = launch_vconv(VE_RELU | VE_MASK | VE_SPLIT6, sargs(l.f1, l.s1_off, A6, H6), st))) return rc;
+      VConvArgs f2 = sargs(l.f2, l.s2_off, H6, Bb);
+      f2.resid = (const bf16*)A;
+      if ((rc = launch_vconv(VE_RESID | VE_MASK, f2, st))) return rc;
+      if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n2_off), eps, xmask, 0, (E*)X, st))) return rc;
+      continue;
+    }
     if ((rc = rowln<E>((const E*)Bb, (int)n, W, (const float*)(P + l.n1_off), eps, xmask, 0, (E*)A, st))) return rc;
     if ((rc = v32(l.f1, A, Hh, VE_RELU | VE_MASK, nullptr)) != kNotVc && rc) return rc;
     if (rc == kNotVc) {

@@ -183,6 +183,8 @@ struct Encoder {
   int DF = 256, dpk = 3, prenet = 1, dtype = F32, esize = 4, dk = 96;
   int mfma_attn = 1;  // bf16, dk = 96: the attention core on MFMA (enc_attn_mfma96_kernel); 0: the fp32-VALU kernel
   int f32vc = 1;      // fp32: convs on mt_vconv's fp32 mode (1, default) or the generic conv kernel (0; A/B, tests)
+  int split = 0;      // fp32: the FFN convs on mt_vconv's split-bf16 mode (VConvArgs::f32 == 2; encoder precision
+                      // "fp32x3": fp32-level products on the bf16 MFMA pipe) instead of exact fp32 MFMA
   ParamList params;
   size_t packed_bytes = 0;
   int emb = -1;
@@ -198,6 +200,7 @@ struct Encoder {
     GemmW qkv, o, f1, f2;
     int n1g, n1b, n2g, n2b;
     size_t n1_off, n2_off;
+    size_t s1_off = 0, s2_off = 0;  // fp32: the FFN convs' split-bf16 images (vconv_repack_split6), 0 if none
   };
   std::vector<Layer> lay;
   size_t ezero_off = 0;  // 256 zero bytes (vconv padding rows) when the FFN convs run on vconv (bf16)

@@ -136,7 +136,8 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   if (rag) rag_build(rtc, rlv, a.lens, a.lmul, L, 0, L, a.B, RBN, tid);
   for (int i = tid; i < C; i += RNT) reinterpret_cast<float*>(smem + RBIAS_OFF)[i] = a.bias[i];
   __syncthreads();
-  const int ntiles = rag ? rtc[a.B - 1] * NTM : a.B * ntn * NTM;
+  // (read once into a scalar: everything derived from it — the tile walk included — then stays scalar)
+  const int ntiles = __builtin_amdgcn_readfirstlane(rag ? rtc[a.B - 1] * NTM : a.B * ntn * NTM);
   // tile ownership: mt_vconv's (XCD-major on grids of <= 3 rounds, else the XCD-grouped round-robin walk)
   const int G = gridDim.x, g = blockIdx.x;
   const int xcd = g & 7, lw = g >> 3;
@@ -155,7 +156,8 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
   RagWalk walk;  // RB_RAGWALK: the workgroup's rows r only increase (tile_of(ti) is called for ti = 0, 1, 2, ...)
   auto tile_of = [&](int ti) __attribute__((always_inline)) {
     Tile tl;
-    const int tile = gl + min(ti, nmine - 1) * gstep;  // past the last tile: the last one (phantom prefetches)
+    // past the last tile: the last one (phantom prefetches); a scalar, so the utterance walk below is a scalar loop
+    const int tile = __builtin_amdgcn_readfirstlane(gl + min(ti, nmine - 1) * gstep);
     const int r = tile / NTM;
     tl.m0 = (tile - r * NTM) * RBM;
     if (rag) {

@@ -34,6 +34,9 @@ enum : int {
   VE_Y2ONLY = 32768, // with VE_DUAL: store y2 only (the raw y is dead: the vocoder's stage output, whose next
                      // upsampler reads lrelu(y) alone); mt_rbconv and the 64-channel ring pairs; every other kernel
                      // drops the flag and stores y as well (its launcher strips it)
+  VE_SPLIT6 = 65536, // split-bf16 mode (VConvArgs::f32 == 2) only: the fp32 result is stored as its 3-way bf16 split
+                     // h1 + h2 + h3 in the 6-plane layout [frames][6 M] = (h1, h1, h1, h2, h2, h3), the next split conv's
+                     // input
   VE_GNRES = 8192,   // 1x1 only, with VE_RESID: the residual is the RAW input of a GroupNorm(M/32) + Mish + mask,
                      // applied here: resid := bf16(mish(GN(resid)) * emask[frame]) with the statistics merged
                      // per tile from the producer's VE_GNSTATS partials (ResnetBlock1D block2 -> + res(x),
@@ -184,7 +187,12 @@ struct VConvArgs {
   const float* gn_beta;      // [M]
   float gn_eps;
   // 1: fp32 operands and output (x, w, y, resid, trash hold floats; w is the vconv_repack_f32 image); epilogues
-  // 0 / VE_RELU / VE_MASK / VE_RESID and their combinations only; one source, plain [B][L][M] output
+  // 0 / VE_RELU / VE_MASK / VE_RESID and their combinations only; one source, plain [B][L][M] output.
+  // 2: split-bf16 ("fp32x3"): x is the 6-plane bf16 split of an fp32 input ([B][L][6 cin0], planes h1 h1 h1 h2 h2 h3 of
+  // x = h1 + h2 + h3, each h the bf16 rounding of what the previous parts leave), w the vconv_repack_split6 image
+  // (planes W1 W2 W3 W1 W2 W1), cin = 6 cin0: one bf16 MFMA K loop sums the six products x1 W1 + x1 W2 + x1 W3 + x2 W1
+  // + x2 W2 + x3 W1 in fp32 (fp32-level accuracy on the bf16 MFMA pipe); the epilogue is the fp32 mode's (resid, y
+  // fp32), or with VE_SPLIT6 the 6-plane split of the result
   int f32;
   // diagnostic builds (-DVCONV_TS) only: per-workgroup phase timestamps (s_memrealtime, 100 MHz) of this launch go
   // to ts[(ts_slot * 256 + workgroup) * 4 + 0..3]; set by launch_vconv, unused otherwise
@@ -240,6 +248,17 @@ int vconv_path_id();
 bool vconv_supported_f32(int cin, int cout, int k, int stride);
 size_t vconv_packed_bytes_f32(int cin, int cout, int k);
 int vconv_repack_f32(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st);
+// split-bf16 mode (VConvArgs::f32 == 2): [Mpad0][taps][cin_pad] fp32 -> bf16 image [6 cin / 64][taps][cout][64] of the
+// weight planes W1 W2 W3 W1 W2 W1 (W = W1 + W2 + W3, each part the bf16 rounding of what the previous parts leave)
+size_t vconv_packed_bytes_split6(int cin, int cout, int k);
+int vconv_repack_split6(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st);
+// the 3-way bf16 split of one fp32 value: h1 = RNE(v), h2 = RNE(v - h1), h3 = RNE(v - h1 - h2) (differences exact)
+__device__ __forceinline__ void split3_bf16(float v, bf16& h1, bf16& h2, bf16& h3) {
+  h1 = (bf16)v;
+  const float r1 = v - (float)h1;
+  h2 = (bf16)r1;
+  h3 = (bf16)(r1 - (float)h2);
+}
 // image of a k = 3, stride 2, pad 1 conv (generic [Mpad0][3][cin_pad] source) as a 2-tap stride-1 conv over
 // frame pairs (2C input channels): run it with L = T/2, cin = 2C, taps = 2, pad = 1 on the same [T][C] rows
 int vconv_repack_s2(const void* src, int cin_pad, int C, int cout, void* dst, hipStream_t st);

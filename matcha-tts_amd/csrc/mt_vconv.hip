@@ -133,11 +133,15 @@ struct CtSched {
   using REG = SchedReg<0, NCHC, TAPS, TT::NWSLOT, TT::NXB, TX, WPW, XPW, NST, 1, SCH::wait_first(-1)>;
 };
 
-// F32: fp32 operands (the text encoder, whose duration path must be the reference's fp32 arithmetic): a 128-byte
-// LDS row holds 32 channels, one 16-byte fragment per lane feeds 4 exact-fp32 v_mfma_f32_16x16x4_f32 (mfma16), and
-// the epilogue stores fp32 in the accumulator layout (bias, ReLU, residual, mask only).
-template <int EF, int BMT, bool K1, int BNT = BN, bool F32 = false, int CTN = 0, int CTT = 0>
+// FM (operand mode) 1, fp32 operands (the text encoder, whose duration path must be the reference's fp32
+// arithmetic): a 128-byte LDS row holds 32 channels, one 16-byte fragment per lane feeds 4 exact-fp32
+// v_mfma_f32_16x16x4_f32 (mfma16), and the epilogue stores fp32 in the accumulator layout (bias, ReLU, residual, mask
+// only). FM 2, split-bf16 (VConvArgs::f32 == 2): the bf16 K loop over the 6-plane operands with FM 1's fp32 epilogue
+// (or, VE_SPLIT6, the 6-plane split of its result).
+template <int EF, int BMT, bool K1, int BNT = BN, int FM = 0, int CTN = 0, int CTT = 0>
 __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
+  constexpr bool F32 = FM == 1;   // fp32 K loop (operands, fragments, MFMA)
+  constexpr bool F32E = FM != 0;  // fp32 epilogue (fp32 residual; fp32 output unless VE_SPLIT6)
   using TT = VT<BMT, K1, vc_npar<EF>(), BNT>;
   constexpr int BN = TT::TBN;
   constexpr int BM = TT::BM, WSLOT = TT::WSLOT, NWW = TT::NWW, FN = TT::FN;
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   // residual / accumulator values of the tile, 16 B per lane: loaded at the start of the tile's last
   // step, consumed after its MFMAs
   u32x4 rv[2][FN], yv[2][FN];
-  f32x4 rv32[F32 ? 4 : 1][FN];  // F32: the fp32 residual of each accumulator block (4 channels of one frame)
+  f32x4 rv32[F32E ? 4 : 1][FN];  // F32E: the fp32 residual of each accumulator block (4 channels of one frame)
   float2 lns[FN];  // (mean, rstd) of each fragment column's frame (VE_LN)
   f32x4 lnr[FN][2];  // VE_LNP: raw per-slab partials (s0, q0, s1, q1), (s2, q2, s3, q3)
   float mk[FN];    // frame mask of each fragment column (VE_MASK)
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
       for (int fn = 0; fn < FN; ++fn) {
         const int n = min(n0 + wn * WNC + fn * 16 + l16, L - 1);  // clamped: no per-block branch
         const size_t o = (rowbase + n) * a.M + m0 + ch16 + fp * 32;
-        if constexpr (F32 && (EF & VE_RESID) != 0) {
+        if constexpr (F32E && (EF & VE_RESID) != 0) {
           const float* rp = reinterpret_cast<const float*>(a.resid) + (rowbase + n) * a.M + m0 + wm * 64 + 4 * g4;
           rv32[2 * fp][fn] = *reinterpret_cast<const f32x4*>(rp + (2 * fp) * 16);
           rv32[2 * fp + 1][fn] = *reinterpret_cast<const f32x4*>(rp + (2 * fp + 1) * 16);
@@ -323,7 +327,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   };
   // Every lane stores (frames past L go to a trash line), so the store count per tile is a constant the
   // vmcnt bookkeeping can add: NST younger VMEM operations the next steps' waits may leave in flight.
-  constexpr int NST = F32 ? 4 * FN : 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
+  constexpr int NST = F32E ? ((EF & VE_SPLIT6) ? 12 * FN : 4 * FN) : 2 * FN * ((EF & VE_DUAL) ? 2 : 1);
   // epilogues without per-element transcendental / statistics work run as packed fp32 pairs
   constexpr bool PK = (EF & ~(VE_RESID | VE_ACCUM | VE_DIV | VE_ACT | VE_DUAL | VE_MASK | VE_PMASK)) == 0;
   constexpr bool PKS = (EF & VE_LN) != 0 && (EF & ~(VE_LN | VE_LNP | VE_SNAKE)) == 0;
@@ -334,7 +338,54 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
   auto epilogue = [&](int ti) {
     int b, n0, m0;
     tile_of(ti, b, n0, m0);
-    if constexpr (F32) {
+    if constexpr (F32E && (EF & VE_SPLIT6) != 0) {
+      // split-bf16 output: v as the fp32 epilogue below computes it, then its 3-way split h1 + h2 + h3 (split3_bf16)
+      // stored as the 6 planes (h1, h1, h1, h2, h2, h3) of [frames][6 M]: blocks (2 fp, fn) and (2 fp + 1, fn)
+      // packed per part and permlane16-swapped into 8 consecutive channels per lane (the bf16 epilogue's layout),
+      // one 16-byte store per plane
+      const size_t ld6 = (size_t)6 * a.M;
+#pragma unroll
+      for (int fp = 0; fp < 2; ++fp)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          uint32_t pt[3][2][2];  // part, block (X / Y), word (channels 4 g4 + 0,1 / 2,3)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int fm = 2 * fp + h;
+            const int m = m0 + wm * 64 + fm * 16 + 4 * g4;
+            const f32x4 bias4 = *reinterpret_cast<const f32x4*>(smem + BIAS_OFF + 4 * m);
+            f32x4 v = acc[fm][fn] + bias4;
+            if constexpr ((EF & VE_RELU) != 0)
+              v = f32x4{fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
+            if constexpr ((EF & VE_RESID) != 0) v = v + rv32[fm][fn];
+            if constexpr ((EF & VE_MASK) != 0) v = v * mk[fn];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              bf16 p1[2], p2[2], p3[2];
+              split3_bf16(v[2 * u], p1[0], p2[0], p3[0]);
+              split3_bf16(v[2 * u + 1], p1[1], p2[1], p3[1]);
+              pt[0][h][u] = pack2(p1[0], p1[1]);
+              pt[1][h][u] = pack2(p2[0], p2[1]);
+              pt[2][h][u] = pack2(p3[0], p3[1]);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            swap16(pt[q][0][0], pt[q][1][0]);
+            swap16(pt[q][0][1], pt[q][1][1]);
+          }
+          const int n = n0 + wn * WNC + fn * 16 + l16;
+          const size_t o = ((size_t)b * L + n) * ld6 + m0 + ch16 + fp * 32;
+#pragma unroll
+          for (int pl = 0; pl < 6; ++pl) {
+            const int q = pl < 3 ? 0 : pl < 5 ? 1 : 2;
+            *reinterpret_cast<u32x4*>(n < L ? a.y + o + (size_t)pl * a.M : a.trash + 8 * lane) =
+                u32x4{pt[q][0][0], pt[q][0][1], pt[q][1][0], pt[q][1][1]};
+          }
+        }
+      return;
+    }
+    if constexpr (F32E) {
       // fp32 out in the accumulator layout: lane (g4, l16) of block (fm, fn) holds channels m..m+3 of frame n, one
       // 16-byte store (frames past L go to the trash line, so the store count stays the constant NST)
 #pragma unroll
@@ -701,7 +752,7 @@ __global__ __launch_bounds__(NT) void vconv_kernel(VConvArgs a) {
     using CS = CtSched<EF, BMT, K1, BNT, CTN, CTT>;
     constexpr int TAPS = CTT, NCHC = CTN, SC = CTN * CTT;
     constexpr int LW = CS::LW, WPW = CS::WPW, XPW = CS::XPW, TX = CS::TX;
-    static_assert(CS::NST == NST && !F32, "CtSched matches the kernel");
+    static_assert(CS::NST == NST && FM == 0, "CtSched matches the kernel");
     using SCH = typename CS::SCH;
     const bool loader = wave < LW;
     if (nch != NCHC || taps != TAPS) __builtin_trap();  // the host dispatches on (cin / 64, taps)
@@ -1011,6 +1062,39 @@ int vconv_repack_f32(const void* src, int Mpad0, int taps, int cin_pad, int cin,
   return 0;
 }
 
+// split-bf16 image [6 cin / 64][taps][Mpad][64] bf16: input channel cc = p cin + c of plane p holds part
+// (0, 1, 2, 0, 1, 0)[p] of the 3-way split of W[m][t][c] (the planes W1 W2 W3 W1 W2 W1 that meet the activation planes
+// x1 x1 x1 x2 x2 x3)
+__global__ void vconv_repack_split6_kernel(const float* __restrict__ src, int Mpad0, int taps, int cin_pad, int cin,
+                                           int cout, int Mpad, size_t total, bf16* __restrict__ dst) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int cl = (int)(i & 63);
+    size_t r = i >> 6;
+    const int m = (int)(r % Mpad);
+    r /= Mpad;
+    const int t = (int)(r % taps);
+    const int cc = (int)(r / taps) * 64 + cl;
+    const int p = cc / cin, c = cc - p * cin;
+    const float w = m < cout && m < Mpad0 && c < cin_pad ? src[((size_t)m * taps + t) * cin_pad + c] : 0.f;
+    bf16 h[3];
+    split3_bf16(w, h[0], h[1], h[2]);
+    dst[i] = h[p < 3 ? p : p - 3 < 2 ? p - 3 : 0];
+  }
+}
+
+size_t vconv_packed_bytes_split6(int cin, int cout, int k) { return vconv_packed_bytes(6 * cin, cout, k); }
+
+int vconv_repack_split6(const void* src, int Mpad0, int taps, int cin_pad, int cin, int cout, void* dst, hipStream_t st) {
+  MT_REQUIRE((6 * cin) % 64 == 0 && cin_pad >= cin, "vconv_repack_split6: cin %d", cin);
+  const int Mpad = (cout + BMP - 1) / BMP * BMP;
+  const size_t total = (size_t)(6 * cin / 64) * taps * Mpad * 64;
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 65535);
+  hipLaunchKernelGGL(vconv_repack_split6_kernel, dim3(blocks), dim3(256), 0, st, (const float*)src, Mpad0, taps, cin_pad,
+                     cin, cout, Mpad, total, (bf16*)dst);
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 bool vconv_supported_f32(int cin, int cout, int k, int stride) {
   return stride == 1 && cin % 32 == 0 && cout % 64 == 0 && cout <= MMAX && (k == 1 || BN + (k - 1) <= 320);
 }
@@ -1096,10 +1180,13 @@ static void ts_assign(VConvArgs& a, const int* rec) {
 
 // fp32 operands (mt_encoder): one launch of the F32 kernel; tiles of BM = 128 rows when C_out % 128 == 0, else 64,
 // and 128 frames (k >= 2: 64-row tiles hold 384 / 128 frames as in bf16; 1x1: the cost model's 128 / 192 / 256)
+static int launch_vconv_split(int ef, const VConvArgs& a0, hipStream_t st);
 static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
+  if (a0.f32 == 2) return launch_vconv_split(ef, a0, st);
   MT_REQUIRE(a0.cin % 32 == 0 && a0.M % 64 == 0 && a0.Mpad == a0.M && a0.M <= MMAX && a0.c0 == 0 && !a0.Lout &&
                  !a0.ldy && (a0.taps == 1 || BN + (a0.taps - 1) * a0.dil <= 320),
              "vconv f32: geometry (cin %d, M %d, taps %d)", a0.cin, a0.M, a0.taps);
+  MT_REQUIRE(!(ef & VE_SPLIT6), "vconv f32: VE_SPLIT6 is a split-bf16 (f32 = 2) epilogue");
   MT_REQUIRE(!(ef & VE_RESID) || a0.resid, "vconv f32: resid");
   MT_REQUIRE(!(ef & VE_MASK) || a0.emask, "vconv f32: mask");
   VConvArgs a = a0;
@@ -1139,13 +1226,13 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
 #define MT_F32CASE(E)                                                                                              \
   case E:                                                                                                          \
     if (k1) {                                                                                                      \
-      if (BM == 128 && bn == 256) hipLaunchKernelGGL((vconv_kernel<E, 128, true, 256, true>), dim3(G), dim3(NT), 0, st, a); \
-      else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, true, 128, true>), dim3(G), dim3(NT), 0, st, a); \
-      else hipLaunchKernelGGL((vconv_kernel<E, 64, true, 128, true>), dim3(G), dim3(NT), 0, st, a);                \
+      if (BM == 128 && bn == 256) hipLaunchKernelGGL((vconv_kernel<E, 128, true, 256, 1>), dim3(G), dim3(NT), 0, st, a); \
+      else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, true, 128, 1>), dim3(G), dim3(NT), 0, st, a); \
+      else hipLaunchKernelGGL((vconv_kernel<E, 64, true, 128, 1>), dim3(G), dim3(NT), 0, st, a);                \
     } else {                                                                                                       \
-      if (BM == 128 && bn == 256) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 256, true>), dim3(G), dim3(NT), 0, st, a); \
-      else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 128, true>), dim3(G), dim3(NT), 0, st, a); \
-      else hipLaunchKernelGGL((vconv_kernel<E, 64, false, 128, true>), dim3(G), dim3(NT), 0, st, a);               \
+      if (BM == 128 && bn == 256) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 256, 1>), dim3(G), dim3(NT), 0, st, a); \
+      else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 128, 1>), dim3(G), dim3(NT), 0, st, a); \
+      else hipLaunchKernelGGL((vconv_kernel<E, 64, false, 128, 1>), dim3(G), dim3(NT), 0, st, a);               \
     }                                                                                                              \
     break;
   switch (ef) {
@@ -1158,6 +1245,55 @@ static int launch_vconv_f32(int ef, const VConvArgs& a0, hipStream_t st) {
     default: set_error("vconv f32: epilogue %d not compiled in", ef); return -1;
   }
 #undef MT_F32CASE
+  MT_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// split-bf16 mode (VConvArgs::f32 == 2; the text encoder's FFN convs): the bf16 K loop over cin = 6 cin0 channels
+// (the operands' six planes), the fp32 epilogue; k >= 2 tiles of 128 x 256 frames (C_out % 128 == 0) or 64 x 128,
+// chosen by rounds of tiles as the fp32 launcher does (the K loop is MFMA-bound: 6 bf16 products per fp32 product)
+static int launch_vconv_split(int ef, const VConvArgs& a0, hipStream_t st) {
+  MT_REQUIRE(a0.cin % 384 == 0 && a0.M % 64 == 0 && a0.Mpad == a0.M && a0.M <= MMAX && a0.c0 == 0 && !a0.Lout &&
+                 !a0.ldy && a0.taps >= 2 && BN + (a0.taps - 1) * a0.dil <= 320 && !a0.lens,
+             "vconv split: geometry (cin %d = 6 x a multiple of 64, M %d, taps %d >= 2)", a0.cin, a0.M, a0.taps);
+  MT_REQUIRE(!(ef & VE_RESID) || a0.resid, "vconv split: resid");
+  MT_REQUIRE(!(ef & VE_MASK) || a0.emask, "vconv split: mask");
+  VConvArgs a = a0;
+  a.c0 = a.cin;
+  a.xcd_tiles = xcd_tiles_knob();
+  a.Lout = a.L;
+  a.ldy = a.M;
+  a.ylim = a.L * a.M;
+  a.ystride = (long long)a.L * a.M;
+  const long cu = cu_count();
+  auto rounds = [&](long bm, long f) {
+    return ((long)a.B * ((a.L + f - 1) / f) * (a.Mpad / bm) + cu - 1) / cu * bm * f;
+  };
+  // 64-row tiles (C_out = 192: conv 2) span 384 frames (24 MFMAs per wave per step: the 216-step K loop is bound by
+  // its per-step cost at 128 frames, 776 vs 580 us for the fp32 kernel at B = 256)
+  int BM = a.M % 128 == 0 ? 128 : 64, bn = BM == 128 ? 256 : 384;
+  if (BM == 128 && rounds(128, 128) < rounds(128, 256)) bn = 128;
+  const long ntiles = (long)a.B * ((a.L + bn - 1) / bn) * (a.Mpad / BM);
+  const int G = (int)std::min<long>(ntiles, cu);
+  {
+    const int rec[VCLOG_FIELDS] = {ef | (2 << 20), BM, bn, 0, (int)ntiles, G, a.taps, a.M, a.cin, a.B, a.L};
+    vclog_record(rec);
+#if defined(VCONV_TS)
+    ts_assign(a, rec);
+#endif
+  }
+#define MT_SPLCASE(E)                                                                                            \
+  case E:                                                                                                        \
+    if (BM == 128 && bn == 256) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 256, 2>), dim3(G), dim3(NT), 0, st, a); \
+    else if (BM == 128) hipLaunchKernelGGL((vconv_kernel<E, 128, false, 128, 2>), dim3(G), dim3(NT), 0, st, a); \
+    else hipLaunchKernelGGL((vconv_kernel<E, 64, false, 384, 2>), dim3(G), dim3(NT), 0, st, a);               \
+    break;
+  switch (ef) {
+    MT_SPLCASE(VE_RELU | VE_MASK | VE_SPLIT6)
+    MT_SPLCASE(VE_RESID | VE_MASK)
+    default: set_error("vconv split: epilogue %d not compiled in", ef); return -1;
+  }
+#undef MT_SPLCASE
   MT_CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -1191,7 +1327,7 @@ template <int E, int BMV, bool K1V, int BNV, int N, int T, int... R>
 static void ct_try(const VConvArgs& a, int G, hipStream_t st, bool& done) {
   (void)CtSched<E, BMV, K1V, BNV, N, T>::REG::reg;  // the schedule, for the CPU schedule test
   if (a.cin / 64 == N && a.taps == T) {
-    hipLaunchKernelGGL((vconv_kernel<E, BMV, K1V, BNV, false, N, T>), dim3(G), dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((vconv_kernel<E, BMV, K1V, BNV, 0, N, T>), dim3(G), dim3(NT), 0, st, a);
     done = true;
     return;
   }

@@ -122,7 +122,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
     rag_build(rtc, rlv, a.lens, a.lmul, L, 0, L, a.B, BN, tid);
     __syncthreads();
   }
-  const int ntiles = rag ? rtc[a.B - 1] : a.B * ntn;
+  const int ntiles = __builtin_amdgcn_readfirstlane(rag ? rtc[a.B - 1] : a.B * ntn);  // scalar: so is the tile walk
   const int G = gridDim.x, g = blockIdx.x;
   const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
   const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(NT) void vpair_kernel(VPairArgs a) {
   const int S = nmine * 2 * ns;  // weight steps of this workgroup
   RagWalk walk;
   auto tile_of = [&](int ti) {  // (utterance, first frame, valid frames) of tile ti
-    const int tile = gl + ti * G;
+    const int tile = __builtin_amdgcn_readfirstlane(gl + ti * G);
     if (rag) return walk.at(rtc, rlv, a.B, BN, tile);
     RagTile t;
     t.b = tile / ntn;
@@ -607,7 +607,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
     rag_build(rtc, rlv, a.lens, a.lmul, L, 0, L, a.B, BN, tid);
     __syncthreads();
   }
-  const int ntiles = rag ? rtc[a.B - 1] : a.B * ntn;
+  const int ntiles = __builtin_amdgcn_readfirstlane(rag ? rtc[a.B - 1] : a.B * ntn);  // scalar: so is the tile walk
   const int G = gridDim.x, g = blockIdx.x;
   const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
   const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
@@ -622,7 +622,7 @@ __global__ __launch_bounds__(NT) void vpair3_kernel(VPairArgs a) {
   int xmk[2] = {0, 0};
   RagWalk walk;
   auto tile_of = [&](int ti) {  // (utterance, first frame, valid frames) of tile ti
-    const int tile = gl + ti * G;
+    const int tile = __builtin_amdgcn_readfirstlane(gl + ti * G);
     if (rag) return walk.at(rtc, rlv, a.B, BN, tile);
     RagTile t;
     t.b = tile / ntn;

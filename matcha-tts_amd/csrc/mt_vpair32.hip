@@ -103,7 +103,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     rag_build(rtc, rlv, a.lens, a.lmul, L, 0, L, a.B, BN, tid);
     __syncthreads();
   }
-  const int ntiles = rag ? rtc[a.B - 1] : a.B * ntn;
+  const int ntiles = __builtin_amdgcn_readfirstlane(rag ? rtc[a.B - 1] : a.B * ntn);  // scalar: so is the tile walk
   const int G = gridDim.x, g = blockIdx.x;
   const int gl = (G % 8 == 0) ? (g % 8) * (G / 8) + g / 8 : g;
   const int nmine = gl < ntiles ? (ntiles - gl + G - 1) / G : 0;
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   int issued = 0, xmk = 0;
   RagWalk walk;
   auto tile_of = [&](int ti) __attribute__((always_inline)) {  // (utterance, first frame, valid frames) of tile ti
-    const int tile = gl + ti * G;
+    const int tile = __builtin_amdgcn_readfirstlane(gl + ti * G);
     if (rag) return walk.at(rtc, rlv, a.B, BN, tile);
     RagTile t;
     t.b = tile / ntn;

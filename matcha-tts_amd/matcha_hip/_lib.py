@@ -38,6 +38,7 @@ SIGNATURES = {
     "mt_encoder_workspace_bytes": (c_size_t, [P, c_int, c_int]),
     "mt_encoder_set_mfma_attention": (c_int, [P, c_int]),
     "mt_encoder_set_vconv": (c_int, [P, c_int]),
+    "mt_encoder_set_split": (c_int, [P, c_int]),
     "mt_encoder_forward": (c_int, [P, P, P, P, P, c_int, c_int, P, P, P, P, P, c_size_t, P]),
     "mt_decoder_create": (c_int, [c_int, c_int, c_int, c_int, c_int, POINTER(c_void_p)]),
     "mt_decoder_destroy": (None, [P]),

@@ -16,7 +16,10 @@ from ._lib import (DTYPE_BF16, DTYPE_F32, SOLVER_EULER, SOLVER_MIDPOINT, HipPath
                    ptr, stream_handle)
 
 _DTYPES = {"fp32": DTYPE_F32, "float32": DTYPE_F32, "f32": DTYPE_F32,
-           "bf16": DTYPE_BF16, "bfloat16": DTYPE_BF16}
+           "bf16": DTYPE_BF16, "bfloat16": DTYPE_BF16,
+           # text encoder only: fp32 storage and arithmetic, the FFN convs' products as six bf16 MFMA products of
+           # 3-way bf16 splits (mt_encoder_set_split)
+           "fp32x3": DTYPE_F32}
 
 
 def dtype_code(precision: str) -> int:
@@ -159,6 +162,8 @@ class EncoderEngine:
         self.packed_bytes = lib().mt_encoder_packed_bytes(h)
         self._packed = None
         self._fp = None
+        if precision == "fp32x3":
+            self.set_split(True)
 
     def __del__(self):
         try:
@@ -174,6 +179,10 @@ class EncoderEngine:
     def set_vconv(self, enable) -> None:
         """fp32: convs on mt_vconv's fp32 mode (1, default) or on the generic conv kernel (0)."""
         check(lib().mt_encoder_set_vconv(self.h, int(bool(enable))), "encoder_set_vconv")
+
+    def set_split(self, enable) -> None:
+        """fp32: the FFN convs on mt_vconv's split-bf16 mode (1; precision "fp32x3") or exact fp32 MFMA (0)."""
+        check(lib().mt_encoder_set_split(self.h, int(bool(enable))), "encoder_set_split")
 
     def pack(self, params: Dict[str, torch.Tensor], device: torch.device) -> torch.Tensor:
         """params: TextEncoder-relative reference keys -> tensors."""
