@@ -381,6 +381,10 @@ int mt_vconv_set_ct(int enable);
  * pairs' compile-time K loop, bit 1 the 128-channel k = 3 pairs' one. Default 3 (MT_VPAIRK=<mask> in the
  * environment); process-wide; returns the previous mask. */
 int mt_vpair_set_kernels(int mask);
+/* conv_post (hifigan/models.py:193-195) in the epilogue of the last stage's final ResBlock pair (1, the default: the stage
+ * output xs is never stored) or as its own launch after it (0). Both run the same MFMA arithmetic (bit-identical).
+ * Process-wide; returns the previous setting (MT_POSTFOLD=0 in the environment: off). */
+int mt_vocoder_set_post_fold(int enable);
 /* The stage 1-2 ResBlock conv1s (mt_rbconv) read the raw chain state and apply its leaky ReLU to their staged rows in
  * LDS, so the producing convs store no activated copy (1, the default; bit-identical results), or read an activated
  * copy the producers store (0). Process-wide; returns the previous setting. */

@@ -56,6 +56,7 @@ extern "C" {
 const char* mt_last_error(void) { return mt::last_error(); }
 int mt_abi_version(void) { return 1; }
 int mt_vpair_set_kernels(int mask) { return mt::vpair_set_kernels(mask); }
+int mt_vocoder_set_post_fold(int enable) { return mt::vocoder_set_post_fold(enable); }
 int mt_sched_count(void) { return mt::sched_count(); }
 int mt_sched_get(int i, int* rec, int* wait, int* wait_first, int cap) {
   MT_REQUIRE(rec && wait && wait_first, "null buffer");

@@ -222,6 +222,11 @@ struct Encoder {
 // -------------------------------------------------------------------------------------
 // HiFi-GAN Generator (hifigan/models.py:148-206)
 // -------------------------------------------------------------------------------------
+// conv_post folded into the last stage's final pair (mt_vpair32 VE_POST; 1, the default) or its own launch (0):
+// bit-identical; process-wide, returns the previous setting (MT_POSTFOLD=0 in the environment: off)
+int vocoder_post_fold();
+int vocoder_set_post_fold(int enable);
+
 struct Vocoder {
   int resblock = 1, dtype = BF16, esize = 2;
   int fuse = 1;  // fused ResBlock stages (mt_rbfuse) where supported
@@ -249,10 +254,15 @@ struct Vocoder {
   bool stage_vp(int i) const;  // ... every resblock as fused pairs: the stage input needs no activated copy
   bool stage_vp32(int i) const;  // a 32-channel stage as fused pairs (mt_vpair32, generic weight packing)
   // stage i's ResBlocks as one fused-pair launch per pair: X -> XS (+ lrelu(XS) in RA when act_out)
+  // wav (non-null, the last stage under post_fold): the final pair runs conv_post in its epilogue (VE_POST) and writes
+  // the waveform instead of xs
   int pair_resblock(const char* P, int i, int j, int B, int L, const char* X, char* XS, char* Tb, char* R,
-                    char* RA, char* trash, bool act_out, hipStream_t st, const int* lens = nullptr) const;
+                    char* RA, char* trash, bool act_out, hipStream_t st, const int* lens = nullptr,
+                    float* wav = nullptr) const;
   int pair_chain(const char* P, int i, int B, int L, const char* X, char* XS, char* Tb, char* R, char* RA,
-                 char* trash, bool act_out, hipStream_t st, const int* lens = nullptr) const;
+                 char* trash, bool act_out, hipStream_t st, const int* lens = nullptr, float* wav = nullptr) const;
+  // stage i (the last, a 32-channel pair stage, conv_post 32 -> 1 with k = 7) folds conv_post into its final pair
+  bool post_fold(int i) const;
   // frames per mel frame at the input of upsampler i (the product of the first i upsampling rates)
   int rate_upto(int i) const;
   size_t frame_elems() const;  // max over stages of (samples per mel frame) x channels

@@ -1273,6 +1273,7 @@ static int launch_vconv_split(int ef, const VConvArgs& a0, hipStream_t st) {
   // its per-step cost at 128 frames, 776 vs 580 us for the fp32 kernel at B = 256)
   int BM = a.M % 128 == 0 ? 128 : 64, bn = BM == 128 ? 256 : 384;
   if (BM == 128 && rounds(128, 128) < rounds(128, 256)) bn = 128;
+  if (BM == 64 && rounds(64, 128) < rounds(64, 384)) bn = 128;  // small batches: fill the CUs first
   const long ntiles = (long)a.B * ((a.L + bn - 1) / bn) * (a.Mpad / BM);
   const int G = (int)std::min<long>(ntiles, cu);
   {

@@ -29,9 +29,10 @@ __global__ __launch_bounds__(256) void post_conv_kernel(const bf16* __restrict__
                                                         const bf16* __restrict__ w, const float* __restrict__ bias,
                                                         float slope, float* __restrict__ out, const int* lens,
                                                         int lmul) {
-  __shared__ __attribute__((aligned(16))) float xs[(PC_N + 6) * PC_ROW];
-  __shared__ __attribute__((aligned(16))) float wsm[7 * 32];
-  const int b = blockIdx.y, f0 = blockIdx.x * PC_N, tid = threadIdx.x;
+  // v = bf16(lrelu(x, slope)) of frames f0 - 3 .. f0 + PC_N + 2 (zero outside [0, Lb)) as post_block's LDS image:
+  // 64-byte rows, 16-byte chunk q at slot q ^ ((row >> 1) & 2); each wave then runs 4 blocks of 16 frames on MFMA
+  __shared__ __attribute__((aligned(16))) char rows[(PC_N + 16) * 64];
+  const int b = blockIdx.y, f0 = blockIdx.x * PC_N, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bf16* xb = x + (size_t)b * L * 32;
   const int Lb = lens ? min(max(lens[b] * lmul, 0), L) : L;
   if (f0 >= Lb) {  // wholly past the utterance
@@ -41,42 +42,25 @@ __global__ __launch_bounds__(256) void post_conv_kernel(const bf16* __restrict__
   for (int e = tid; e < (PC_N + 6) * 4; e += 256) {
     const int r = e >> 2, q = e & 3;
     const int f = f0 - 3 + r;
-    float v[8];
+    u32x4 v = {0u, 0u, 0u, 0u};
     if (f >= 0 && f < Lb) {
-      const u32x4 u = *reinterpret_cast<const u32x4*>(xb + (size_t)f * 32 + q * 8);
+      v = *reinterpret_cast<const u32x4*>(xb + (size_t)f * 32 + q * 8);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[2 * j] = (float)(bf16)lrelu_f(__uint_as_float(u[j] << 16), slope);
-        v[2 * j + 1] = (float)(bf16)lrelu_f(__uint_as_float(u[j] & 0xffff0000u), slope);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = 0.f;
+      for (int j = 0; j < 4; ++j) v[j] = lrelu_pk_sel(v[j], slope);
     }
-    float* d = xs + r * PC_ROW + q * 8;
-    *reinterpret_cast<f32x4*>(d) = f32x4{v[0], v[1], v[2], v[3]};
-    *reinterpret_cast<f32x4*>(d + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    *reinterpret_cast<u32x4*>(rows + r * 64 + ((q ^ ((r >> 1) & 2)) * 16)) = v;
   }
-  if (tid < 7 * 32) wsm[tid] = (float)w[tid];
+  bf16x8 wfr[7];
+  post_wfrag(w, lane, wfr);
   __syncthreads();
-  const int f = f0 + tid;
-  if (f >= L) return;
-  if (f >= Lb) {
-    out[(size_t)b * L + f] = 0.f;
-    return;
-  }
-  float acc = 0.f;
+  const float bs = bias[0];
 #pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const float* row = xs + (tid + k) * PC_ROW;
-#pragma unroll
-    for (int c = 0; c < 32; c += 4) {
-      const f32x4 xv = *reinterpret_cast<const f32x4*>(row + c);
-      const f32x4 wv = *reinterpret_cast<const f32x4*>(wsm + k * 32 + c);
-      acc += xv[0] * wv[0] + xv[1] * wv[1] + xv[2] * wv[2] + xv[3] * wv[3];
-    }
+  for (int j = 0; j < PC_N / 64; ++j) {
+    const int r0 = wave * (PC_N / 4) + 16 * j;
+    const f32x4 d = post_block(rows, r0, wfr, lane);
+    const int f = f0 + r0 + lane;
+    if (lane < 16 && f < L) out[(size_t)b * L + f] = f < Lb ? tanhf(d[0] + bs) : 0.f;
   }
-  out[(size_t)b * L + f] = tanhf(acc + bias[0]);
 }
 
 // rows [lens[b], T) of utterance b of a [B][T][C] tensor := 0 (a ragged batch's zero padding)
@@ -294,8 +278,30 @@ bool Vocoder::stage_vp32(int i) const {
 
 // One launch per pair (mt_vpair128 / mt_vpair / mt_vpair32); the chain state ping-pongs between R and Tb (a pair
 // reads its input's halo, so it cannot write in place); the inputs' activations are applied in LDS.
+// conv_post in the last stage's final pair (mt_vpair32 VE_POST): on by default; MT_POSTFOLD=0 in the environment or
+// mt_vocoder_set_post_fold(0): the separate post_conv_kernel (the same post_block arithmetic: bit-identical)
+static int g_postfold = -1;
+int vocoder_post_fold() {
+  if (g_postfold < 0) {
+    const char* e = getenv("MT_POSTFOLD");
+    g_postfold = e && e[0] == '0' ? 0 : 1;
+  }
+  return g_postfold;
+}
+int vocoder_set_post_fold(int enable) {
+  const int prev = vocoder_post_fold();
+  g_postfold = enable ? 1 : 0;
+  return prev;
+}
+
+bool Vocoder::post_fold(int i) const {
+  const int nk = (int)rb_kernels.size();
+  return vocoder_post_fold() && dtype == BF16 && i + 1 == (int)ups.size() && stage_vp32(i) && post.cin == 32 &&
+         post.k == 7 && post.cout == 1 && nk > 0 && (rb_kernels[nk - 1] - 1) / 2 <= 5;
+}
+
 int Vocoder::pair_resblock(const char* P, int i, int j, int B, int L, const char* X, char* XS, char* Tb, char* R,
-                           char* RA, char* trash, bool act_out, hipStream_t st, const int* lens) const {
+                           char* RA, char* trash, bool act_out, hipStream_t st, const int* lens, float* wav) const {
   const int nk = (int)rb_kernels.size();
   const int C = rb1[(size_t)i * nk][0].cout;
   const bool c32 = C == 32;
@@ -333,6 +339,13 @@ int Vocoder::pair_resblock(const char* P, int i, int j, int B, int L, const char
         a.y2 = (bf16*)RA;
         ef |= VE_DUAL | VE_Y2ONLY;  // the upsampler reads RA alone: the raw xs is dead (not stored)
       }
+      if (j == nk - 1 && wav && c32 && !act_out && j > 0) {  // conv_post here; xs is not stored
+        a.post_w = (const bf16*)(P + post.w_off);
+        a.post_b = (const float*)(P + post.b_off);
+        a.post_slope = 0.01f;
+        a.wav = wav;
+        ef |= VE_POST;
+      }
     }
     if ((rc = c32 ? launch_vpair32(ef, a, st) : C == 128 ? launch_vpair128(ef, a, st) : launch_vpair(ef, a, st)))
       return rc;
@@ -342,11 +355,11 @@ int Vocoder::pair_resblock(const char* P, int i, int j, int B, int L, const char
 }
 
 int Vocoder::pair_chain(const char* P, int i, int B, int L, const char* X, char* XS, char* Tb, char* R, char* RA,
-                        char* trash, bool act_out, hipStream_t st, const int* lens) const {
+                        char* trash, bool act_out, hipStream_t st, const int* lens, float* wav) const {
   const int nk = (int)rb_kernels.size();
   int rc;
   for (int j = 0; j < nk; ++j)
-    if ((rc = pair_resblock(P, i, j, B, L, X, XS, Tb, R, RA, trash, act_out, st, lens))) return rc;
+    if ((rc = pair_resblock(P, i, j, B, L, X, XS, Tb, R, RA, trash, act_out, st, lens, wav))) return rc;
   return 0;
 }
 
@@ -586,6 +599,12 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
     if constexpr (std::is_same<E, bf16>::value) {
       if (stage_vp32((int)i)) {
         const bool act_out = i + 1 < ups.size() && ups_vc((int)i + 1);
+        if (post_fold((int)i) && !act_out) {
+          // conv_post in the final pair's epilogue (VE_POST): the pair walks only each utterance's live tiles, so
+          // the samples past them are zeroed here (post_conv_kernel wrote those zeros itself)
+          if (lens) MT_CHECK_HIP(hipMemsetAsync(wav, 0, (size_t)B * L * sizeof(float), st));
+          return pair_chain(P, (int)i, B, L, X, XS, Tb, R, RA, trash, act_out, st, lens, wav);
+        }
         if ((rc = pair_chain(P, (int)i, B, L, X, XS, Tb, R, RA, trash, act_out, st, lens))) return rc;
         continue;
       }

@@ -24,7 +24,39 @@ struct VPairArgs {
   // them, tiles past them not computed); null: every utterance has L
   const int* lens;
   int lmul;
+  // VE_POST (mt_vpair32): conv_post's [7][32] bf16 weights and bias, its lrelu slope, the [B][L] fp32 waveform
+  const bf16* post_w;
+  const float* post_b;
+  float post_slope;
+  float* wav;
 };
+
+// conv_post (32 -> 1 channel, k = 7, pad 3; hifigan/models.py:193-195) of 16 consecutive output frames on MFMA, the one
+// arithmetic of the bf16 path (post_conv_kernel, mt_vocoder.hip, and mt_vpair32's VE_POST epilogue): rows is an LDS
+// image of v = bf16(lrelu(xs, 0.01)) with 64-byte rows (32 channels; 16-byte chunk q at slot q ^ ((row >> 1) & 2),
+// zero outside the utterance), the block's first output frame at row r0 + 3; wfr[t] the A operand of tap t (lanes
+// with lane % 16 == 0 hold w[t][8 (lane / 16) ..], every other lane zeros: output row 0 of the 16 x 16 tile). The
+// seven MFMAs chain the taps in order (K = the 32 channels each) -> lanes 0..15 hold the block's 16 sums in [0].
+__device__ __forceinline__ f32x4 post_block(const char* rows, int r0, const bf16x8 (&wfr)[7], int lane) {
+  const int g4 = lane >> 4, l16 = lane & 15;
+  f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 7; ++t) {
+    const int r = r0 + l16 + t;
+    const bf16x8 bv = *reinterpret_cast<const bf16x8*>(rows + r * 64 + ((g4 ^ ((r >> 1) & 2)) * 16));
+    d = mfma16(wfr[t], bv, d);
+  }
+  return d;
+}
+// the A operands of post_block from conv_post's generic packed weights [1 row][7][32] bf16 (w + t * 32 + c)
+__device__ __forceinline__ void post_wfrag(const bf16* w, int lane, bf16x8 (&wfr)[7]) {
+#pragma unroll
+  for (int t = 0; t < 7; ++t) {
+    bf16x8 v = {};
+    if ((lane & 15) == 0) v = *reinterpret_cast<const bf16x8*>(w + t * 32 + 8 * (lane >> 4));
+    wfr[t] = v;
+  }
+}
 
 // The compile-time K loop of the ring pair kernels (vpair_kernel<EF, K> and vpair128_kernel<EF, K>, K > 0): per wave
 // the prologue stages the first tile's rows (NXP pieces), then the weights of steps 0 .. NWS - 2 (2 pieces each); per

@@ -114,6 +114,14 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
   }
   __syncthreads();
 
+  // VE_POST (the vocoder's last pair): conv2's outputs are frames n0 - PS + i (PS = 3: the 3-frame halo conv_post
+  // reads on each side of the tile's BN outputs lies inside the frames conv2 computes validly, i < NF1 - 2 h2 - ... );
+  // xs goes to LDS as conv_post's input (post_block) and only the waveform is stored
+  constexpr bool POST = (EF & VE_POST) != 0;
+  constexpr int PS = POST ? 3 : 0;
+  static_assert(!POST || ((EF & VE_ACCUM) && (EF & VE_DIV) && !(EF & VE_DUAL)), "VE_POST: the stage's final xs");
+  bf16x8 wfr[POST ? 7 : 1];
+  if constexpr (POST) post_wfrag(a.post_w, lane, wfr);
   int issued = 0, xmk = 0;
   RagWalk walk;
   auto tile_of = [&](int ti) __attribute__((always_inline)) {  // (utterance, first frame, valid frames) of tile ti
@@ -250,7 +258,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     u32x4 rv[FN], yv[FN];  // residual x and (VE_ACCUM) old xs of this lane's outputs
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
-      const int r = wave * WNC + fn * 16 + l16 + HALO2 + h1;
+      const int r = wave * WNC + fn * 16 + l16 + HALO2 + h1 - PS;
       rv[fn] = *reinterpret_cast<const u32x4*>(smem + r * RB + ((qc ^ swz(r)) * 16));
     }
     barrier();
@@ -273,7 +281,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     if constexpr ((EF & VE_ACCUM) != 0) {
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
-        const int i = min(n0 + wave * WNC + fn * 16 + l16, L - 1);
+        const int i = min(max(n0 - PS + wave * WNC + fn * 16 + l16, 0), L - 1);
         asm volatile("global_load_dwordx4 %0, %1, off"
                      : "=v"(yv[fn])
                      : "v"(a.y + ((size_t)b * L + i) * C + ch16)
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     barrier();  // T published; every wave is past conv1's reads of the row buffer: stage the next tile's rows
     stage_x(ti + 1);
     VP_TS(6);
-    conv(1, smem + T_OFF, wave * WNC + l16 + HALO2 - h2, 1);
+    conv(1, smem + T_OFF, wave * WNC + l16 + HALO2 - h2 - PS, 1);
     VP_TS(7);
     // epilogue: + b2 + x [+ xs] [/ nk] -> y [, lrelu(y) -> y2]
     if constexpr ((EF & VE_ACCUM) != 0) {
@@ -321,9 +329,10 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
     const auto yr = __builtin_amdgcn_make_buffer_rsrc(a.y + (size_t)bu * L * C, (short)0, (int)((unsigned)L * RB), 0x00020000);
     const auto y2r = __builtin_amdgcn_make_buffer_rsrc(((EF & VE_DUAL) ? a.y2 : a.y) + (size_t)bu * L * C, (short)0,
                                                        (int)((unsigned)L * RB), 0x00020000);
+    if constexpr (POST) barrier();  // every wave is past conv2's reads of T: xs replaces it as conv_post's input
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
-      const int i = wave * WNC + fn * 16 + l16;  // output frame n0 + i
+      const int i = wave * WNC + fn * 16 + l16;  // output frame n0 - PS + i
       uint32_t rx0 = rv[fn][0], rx1 = rv[fn][1], ry0 = rv[fn][2], ry1 = rv[fn][3];
       swap16(rx0, ry0);  // back to the accumulator layout
       swap16(rx1, ry1);
@@ -352,6 +361,17 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       }
       swap16(o1[0][0], o1[1][0]);
       swap16(o1[0][1], o1[1][1]);
+      if constexpr (POST) {
+        // conv_post's input v = bf16(lrelu(xs, 0.01)) of frame n0 - 3 + i into T row i (zero outside the utterance:
+        // conv_post's zero padding), the layout post_block reads
+        const int f = n0 - PS + i;
+        const bool in = f >= 0 && f < Lt;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (in) v = u32x4{lrelu_pk(o1[0][0], a.post_slope), lrelu_pk(o1[0][1], a.post_slope),
+                          lrelu_pk(o1[1][0], a.post_slope), lrelu_pk(o1[1][1], a.post_slope)};
+        *reinterpret_cast<u32x4*>(smem + T_OFF + i * RB + ((qc ^ swz(i)) * 16)) = v;
+        continue;
+      }
       if constexpr (VP32_BUF) {
         // the utterance's [L][C] output as a buffer: frames past L fall outside it (store dropped); the discarded
         // frames i >= BN of the last wave's last fragment get an offset past any range (every lane still stores, so
@@ -373,6 +393,24 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
         swap16(o2[0][0], o2[1][0]);
         swap16(o2[0][1], o2[1][1]);
         *reinterpret_cast<u32x4*>(ok ? a.y2 + o : a.trash + 8 * lane) = u32x4{o2[0][0], o2[0][1], o2[1][0], o2[1][1]};
+      }
+    }
+    if constexpr (POST) {
+      // conv_post of the tile's BN frames (post_block: 6 blocks of 16 per wave), tanh(. + bias), the waveform stored
+      // (frames past the utterance: 0, as post_conv_kernel; past L or BN: dropped by the range check); every lane
+      // issues one store per block, as many as the plain epilogue's stores
+      barrier();
+      const float* wbase = a.wav + (size_t)bu * L;
+      const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), (short)0, (int)((unsigned)L * 4), 0x00020000);
+      const float pb = a.post_b[0];
+#pragma unroll
+      for (int fb = 0; fb < FN; ++fb) {
+        const int r0 = wave * WNC + fb * 16;
+        const f32x4 dd = post_block(smem + T_OFF, r0, wfr, lane);
+        const int o = r0 + lane;  // output frame n0 + o (lanes 0..15)
+        const float val = n0 + o < Lt ? tanhf(dd[0] + pb) : 0.f;
+        const unsigned vo = lane < 16 && o < BN ? (unsigned)((n0 + o) * 4) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), wr, vo, 0, 0);
       }
     }
     issued += FN * ((EF & VE_DUAL) ? 2 : 1);
@@ -405,6 +443,10 @@ int launch_vpair32(int ef, const VPairArgs& a, hipStream_t st) {
              "vpair32: null argument / empty");
   MT_REQUIRE(vpair32_supported(a.taps, a.dil) && a.taps % 2 == 1, "vpair32: k %d d %d", a.taps, a.dil);
   MT_REQUIRE(!(ef & VE_DUAL) || a.y2, "vpair32: y2");
+  MT_REQUIRE(!(ef & VE_POST) || (a.post_w && a.post_b && a.wav && (ef & ~VE_POST) == (VE_ACCUM | VE_DIV) &&
+                                 (a.taps - 1) / 2 + 3 <= HALO2),
+             "vpair32: VE_POST needs conv_post's weights, bias and the waveform, the stage's final (ACCUM | DIV) pair "
+             "and k <= %d", 2 * (HALO2 - 3) + 1);
   MT_REQUIRE(a.y != a.x, "vpair32: y must not alias x (neighbour tiles read x's halo)");
   const long ntiles = (long)a.B * ((a.L + BN - 1) / BN);
   const int G = (int)std::min<long>(ntiles, cu_count());
@@ -420,6 +462,9 @@ int launch_vpair32(int ef, const VPairArgs& a, hipStream_t st) {
       break;
     case VE_DIV: hipLaunchKernelGGL((vpair32_kernel<VE_DIV>), dim3(G), dim3(NT), 0, st, a); break;
     case VE_DIV | VE_DUAL: hipLaunchKernelGGL((vpair32_kernel<VE_DIV | VE_DUAL>), dim3(G), dim3(NT), 0, st, a); break;
+    case VE_ACCUM | VE_DIV | VE_POST:
+      hipLaunchKernelGGL((vpair32_kernel<VE_ACCUM | VE_DIV | VE_POST>), dim3(G), dim3(NT), 0, st, a);
+      break;
     default: set_error("vpair32: epilogue %d not compiled in", ef); return -1;
   }
   MT_CHECK_HIP(hipGetLastError());

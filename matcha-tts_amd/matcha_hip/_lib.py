@@ -95,6 +95,7 @@ SIGNATURES = {
     "mt_vconv_set_rbconv": (c_int, [c_int]),
     "mt_vconv_set_ct": (c_int, [c_int]),
     "mt_vpair_set_kernels": (c_int, [c_int]),
+    "mt_vocoder_set_post_fold": (c_int, [c_int]),
     "mt_ffn_set": (c_int, [c_int]),
     "mt_vconv_set_actin": (c_int, [c_int]),
     "mt_ffn_set_min_frames": (c_int, [c_int]),

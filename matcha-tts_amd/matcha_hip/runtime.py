@@ -600,6 +600,12 @@ def set_vpair_kernels(mask: int) -> int:
     return int(lib().mt_vpair_set_kernels(int(mask)))
 
 
+def set_post_fold(enable) -> int:
+    """conv_post in the last ResBlock pair's epilogue (1, default) or its own launch (0); bit-identical; returns the
+    previous setting (process-wide)"""
+    return int(lib().mt_vocoder_set_post_fold(int(bool(enable))))
+
+
 def set_ffn(mode) -> int:
     """the bf16 decoder's transformer FeedForward as one fused launch (mt_ffn; 3, the default: serial schedule with the
     frame fragments prefetched; 1: serial, weight and frame fragments prefetched; 2: FF1 epilogues overlapped with FF2
