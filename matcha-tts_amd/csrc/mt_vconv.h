@@ -36,7 +36,7 @@ enum : int {
                      // drops the flag and stores y as well (its launcher strips it)
   VE_POST = 131072,  // mt_vpair32 only, with VE_ACCUM | VE_DIV on the last stage's final pair: the stage output xs feeds
                      // conv_post (hifigan/models.py:193-195: tanh(conv_post(lrelu(xs, 0.01)))) in the same launch and the
-                     // waveform is stored instead of xs (post_block, mt_vpair.h)
+                     // waveform is stored instead of xs (post_taps, mt_vpair.h)
   VE_SPLIT6 = 65536, // split-bf16 mode (VConvArgs::f32 == 2) only: the fp32 result is stored as its 3-way bf16 split
                      // h1 + h2 + h3 in the 6-plane layout [frames][6 M] = (h1, h1, h1, h2, h2, h3), the next split conv's
                      // input

@@ -19,18 +19,18 @@
 namespace mt {
 
 // conv_post (hifigan/models.py:194-196) for bf16 C = 32: tanh(conv_k7(lrelu(x, 0.01)) + b), one output channel.
-// A memory-bound dot product of 7 x 32 inputs per sample: 256 samples per workgroup, their 262 input
-// rows staged once in LDS as lrelu'd fp32 (rounded to bf16 first, as the generic kernel stages them),
-// 144-byte rows so each lane's 16-byte reads of rows t..t+6 hit distinct bank slots.
-constexpr int PC_N = 256, PC_ROW = 36;
+// 256 samples per workgroup: their 262 input rows staged once in LDS as bf16(lrelu(x)), the image post_taps reads
+// (mt_vpair.h; mt_vpair32's VE_POST epilogue runs the same arithmetic on its own tile).
+constexpr int PC_N = 256;
 // Ragged batch (lens != null): utterance b has Lb = lens[b] * lmul samples; rows past Lb are zero padding and its
 // samples past Lb are written as zeros.
 __global__ __launch_bounds__(256) void post_conv_kernel(const bf16* __restrict__ x, int L,
                                                         const bf16* __restrict__ w, const float* __restrict__ bias,
                                                         float slope, float* __restrict__ out, const int* lens,
                                                         int lmul) {
-  // v = bf16(lrelu(x, slope)) of frames f0 - 3 .. f0 + PC_N + 2 (zero outside [0, Lb)) as post_block's LDS image:
+  // v = bf16(lrelu(x, slope)) of frames f0 - 3 .. f0 + PC_N + 2 (zero outside [0, Lb)) as post_taps's LDS image:
   // 64-byte rows, 16-byte chunk q at slot q ^ ((row >> 1) & 2); each wave then runs 4 blocks of 16 frames on MFMA
+  // (rows up to 64 wave + 79 are read: the last 10 never reach a kept sum)
   __shared__ __attribute__((aligned(16))) char rows[(PC_N + 16) * 64];
   const int b = blockIdx.y, f0 = blockIdx.x * PC_N, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bf16* xb = x + (size_t)b * L * 32;
@@ -50,16 +50,18 @@ __global__ __launch_bounds__(256) void post_conv_kernel(const bf16* __restrict__
     }
     *reinterpret_cast<u32x4*>(rows + r * 64 + ((q ^ ((r >> 1) & 2)) * 16)) = v;
   }
-  bf16x8 wfr[7];
-  post_wfrag(w, lane, wfr);
+  const bf16x8 wt = post_wtaps(w, lane);
   __syncthreads();
   const float bs = bias[0];
+  f32x4 dp = post_taps(rows, wave * (PC_N / 4), wt, lane);
 #pragma unroll
   for (int j = 0; j < PC_N / 64; ++j) {
     const int r0 = wave * (PC_N / 4) + 16 * j;
-    const f32x4 d = post_block(rows, r0, wfr, lane);
+    const f32x4 dn = post_taps(rows, r0 + 16, wt, lane);
+    const float s = post_combine(dp, dn, lane);
+    dp = dn;
     const int f = f0 + r0 + lane;
-    if (lane < 16 && f < L) out[(size_t)b * L + f] = f < Lb ? tanhf(d[0] + bs) : 0.f;
+    if (lane < 16 && f < L) out[(size_t)b * L + f] = f < Lb ? tanhf(s + bs) : 0.f;
   }
 }
 
@@ -279,7 +281,7 @@ bool Vocoder::stage_vp32(int i) const {
 // One launch per pair (mt_vpair128 / mt_vpair / mt_vpair32); the chain state ping-pongs between R and Tb (a pair
 // reads its input's halo, so it cannot write in place); the inputs' activations are applied in LDS.
 // conv_post in the last stage's final pair (mt_vpair32 VE_POST): on by default; MT_POSTFOLD=0 in the environment or
-// mt_vocoder_set_post_fold(0): the separate post_conv_kernel (the same post_block arithmetic: bit-identical)
+// mt_vocoder_set_post_fold(0): the separate post_conv_kernel (the same post_taps arithmetic: bit-identical)
 static int g_postfold = -1;
 int vocoder_post_fold() {
   if (g_postfold < 0) {

@@ -31,31 +31,42 @@ struct VPairArgs {
   float* wav;
 };
 
-// conv_post (32 -> 1 channel, k = 7, pad 3; hifigan/models.py:193-195) of 16 consecutive output frames on MFMA, the one
-// arithmetic of the bf16 path (post_conv_kernel, mt_vocoder.hip, and mt_vpair32's VE_POST epilogue): rows is an LDS
-// image of v = bf16(lrelu(xs, 0.01)) with 64-byte rows (32 channels; 16-byte chunk q at slot q ^ ((row >> 1) & 2),
-// zero outside the utterance), the block's first output frame at row r0 + 3; wfr[t] the A operand of tap t (lanes
-// with lane % 16 == 0 hold w[t][8 (lane / 16) ..], every other lane zeros: output row 0 of the 16 x 16 tile). The
-// seven MFMAs chain the taps in order (K = the 32 channels each) -> lanes 0..15 hold the block's 16 sums in [0].
-__device__ __forceinline__ f32x4 post_block(const char* rows, int r0, const bf16x8 (&wfr)[7], int lane) {
-  const int g4 = lane >> 4, l16 = lane & 15;
-  f32x4 d = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int t = 0; t < 7; ++t) {
-    const int r = r0 + l16 + t;
-    const bf16x8 bv = *reinterpret_cast<const bf16x8*>(rows + r * 64 + ((g4 ^ ((r >> 1) & 2)) * 16));
-    d = mfma16(wfr[t], bv, d);
-  }
-  return d;
+// conv_post (32 -> 1 channel, k = 7, pad 3; hifigan/models.py:193-195) on MFMA, the one arithmetic of the bf16 path
+// (post_conv_kernel, mt_vocoder.hip, and mt_vpair32's VE_POST epilogue). rows is an LDS image of v = bf16(lrelu(xs,
+// 0.01)) with 64-byte rows (32 channels; 16-byte chunk q at slot q ^ ((row >> 1) & 2), zero outside the utterance).
+// The seven taps are the A operand's rows (post_wtaps), so one MFMA over 16 rows gives every tap's partial sum of each
+// row, D[t][n] = w[t] . v[r0 + n] (post_taps: one LDS read per row instead of one per tap and row); the output whose
+// window starts at row r0 + o (frame r0 + o + 3 of the image) is sum_t D[t][o + t], gathered from two consecutive
+// blocks by row rotations (post_combine).
+__device__ __forceinline__ bf16x8 post_wtaps(const bf16* w, int lane) {  // lane % 16 = t < 7: w[t][8 (lane / 16) ..]
+  bf16x8 v = {};
+  if ((lane & 15) < 7) v = *reinterpret_cast<const bf16x8*>(w + (lane & 15) * 32 + 8 * (lane >> 4));
+  return v;
 }
-// the A operands of post_block from conv_post's generic packed weights [1 row][7][32] bf16 (w + t * 32 + c)
-__device__ __forceinline__ void post_wfrag(const bf16* w, int lane, bf16x8 (&wfr)[7]) {
-#pragma unroll
-  for (int t = 0; t < 7; ++t) {
-    bf16x8 v = {};
-    if ((lane & 15) == 0) v = *reinterpret_cast<const bf16x8*>(w + t * 32 + 8 * (lane >> 4));
-    wfr[t] = v;
-  }
+__device__ __forceinline__ f32x4 post_taps(const char* rows, int r0, const bf16x8& wt, int lane) {
+  const int r = r0 + (lane & 15);
+  const bf16x8 bv = *reinterpret_cast<const bf16x8*>(rows + r * 64 + (((lane >> 4) ^ ((r >> 1) & 2)) * 16));
+  return mfma16(wt, bv, f32x4{0.f, 0.f, 0.f, 0.f});
+}
+// element I of a post_taps result lives in 16-lane row g (tap 4 g + I): lane o of row 0 takes lane (o + I) & 15, of
+// row 1 lane (o + 4 + I) & 15 (DPP row_ror:m moves lane l - m to lane l, so m = 16 - that shift)
+template <int I>
+__device__ __forceinline__ float post_rot(float x) {
+  const int v = __float_as_int(x);
+  const int r = I == 0 ? v : __builtin_amdgcn_update_dpp(0, v, 0x120 + 16 - I, 0x1, 0xf, false);
+  return __int_as_float(__builtin_amdgcn_update_dpp(r, v, 0x120 + 12 - I, 0x2, 0xf, false));
+}
+// the 16 outputs of rows r0 .. r0 + 15 from da = post_taps(r0) and db = post_taps(r0 + 16): D[t][o + t] lies in da
+// when o + t < 16, i.e. at a source lane l16 >= t, else in db (lane l16 = o + t - 16 < t). Sum order: taps 0..3 and
+// 4..6 in order within rows 0 / 1, then row 0 + row 1; lanes 0..15 hold the block's sums
+__device__ __forceinline__ float post_combine(const f32x4& da, const f32x4& db, int lane) {
+  const int l16 = lane & 15, t0 = 4 * (lane >> 4);
+  float s = post_rot<0>(l16 >= t0 ? da[0] : db[0]);
+  s += post_rot<1>(l16 >= t0 + 1 ? da[1] : db[1]);
+  s += post_rot<2>(l16 >= t0 + 2 ? da[2] : db[2]);
+  s += post_rot<3>(l16 >= t0 + 3 ? da[3] : db[3]);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);  // row 0: (taps 0..3) + (taps 4..6)
 }
 
 // The compile-time K loop of the ring pair kernels (vpair_kernel<EF, K> and vpair128_kernel<EF, K>, K > 0): per wave

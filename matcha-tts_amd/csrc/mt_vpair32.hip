@@ -116,12 +116,10 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
 
   // VE_POST (the vocoder's last pair): conv2's outputs are frames n0 - PS + i (PS = 3: the 3-frame halo conv_post
   // reads on each side of the tile's BN outputs lies inside the frames conv2 computes validly, i < NF1 - 2 h2 - ... );
-  // xs goes to LDS as conv_post's input (post_block) and only the waveform is stored
+  // xs goes to LDS as conv_post's input (post_taps) and only the waveform is stored
   constexpr bool POST = (EF & VE_POST) != 0;
   constexpr int PS = POST ? 3 : 0;
   static_assert(!POST || ((EF & VE_ACCUM) && (EF & VE_DIV) && !(EF & VE_DUAL)), "VE_POST: the stage's final xs");
-  bf16x8 wfr[POST ? 7 : 1];
-  if constexpr (POST) post_wfrag(a.post_w, lane, wfr);
   int issued = 0, xmk = 0;
   RagWalk walk;
   auto tile_of = [&](int ti) __attribute__((always_inline)) {  // (utterance, first frame, valid frames) of tile ti
@@ -363,7 +361,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       swap16(o1[0][1], o1[1][1]);
       if constexpr (POST) {
         // conv_post's input v = bf16(lrelu(xs, 0.01)) of frame n0 - 3 + i into T row i (zero outside the utterance:
-        // conv_post's zero padding), the layout post_block reads
+        // conv_post's zero padding), the layout post_taps reads
         const int f = n0 - PS + i;
         const bool in = f >= 0 && f < Lt;
         u32x4 v = {0u, 0u, 0u, 0u};
@@ -396,24 +394,42 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       }
     }
     if constexpr (POST) {
-      // conv_post of the tile's BN frames (post_block: 6 blocks of 16 per wave), tanh(. + bias), the waveform stored
-      // (frames past the utterance: 0, as post_conv_kernel; past L or BN: dropped by the range check); every lane
-      // issues one store per block, as many as the plain epilogue's stores
+      // conv_post of the tile's BN frames (post_taps / post_combine: 6 blocks of 16 per wave), tanh(. + bias), the
+      // waveform stored (frames past the utterance: 0, as post_conv_kernel; past L or BN: dropped by the range check)
       barrier();
       const float* wbase = a.wav + (size_t)bu * L;
       const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), (short)0, (int)((unsigned)L * 4), 0x00020000);
+      // conv_post's A operand fetched here (cache-resident) rather than held through the tile loop (VGPR pressure)
+      const bf16x8 wt = post_wtaps(a.post_w, lane);
       const float pb = a.post_b[0];
+      // the blocks' sums sit in lanes 0..15 of each result: up to 4 blocks gathered into one register (16-lane row
+      // q = block 4 g + q, by permlane16 / permlane32 swaps) so tanh runs once per 64 outputs, one store per group
+      static_assert(FN == 6, "two groups of blocks: 4 + 2");
+      float sv[FN];
+      f32x4 dp = post_taps(smem + T_OFF, wave * WNC, wt, lane);
 #pragma unroll
-      for (int fb = 0; fb < FN; ++fb) {
-        const int r0 = wave * WNC + fb * 16;
-        const f32x4 dd = post_block(smem + T_OFF, r0, wfr, lane);
-        const int o = r0 + lane;  // output frame n0 + o (lanes 0..15)
-        const float val = n0 + o < Lt ? tanhf(dd[0] + pb) : 0.f;
-        const unsigned vo = lane < 16 && o < BN ? (unsigned)((n0 + o) * 4) : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), wr, vo, 0, 0);
+      for (int fb = 0; fb < FN; ++fb) {  // rows up to wave * WNC + WNC + 15 < TROWS
+        const f32x4 dn = post_taps(smem + T_OFF, wave * WNC + (fb + 1) * 16, wt, lane);
+        sv[fb] = post_combine(dp, dn, lane);
+        dp = dn;
+      }
+      auto gather = [&](float b0, float b1, float b2, float b3) __attribute__((always_inline)) {
+        uint32_t x0 = __float_as_uint(b0), x1 = __float_as_uint(b1), x2 = __float_as_uint(b2), x3 = __float_as_uint(b3);
+        swap16(x0, x1);  // x0 rows: (b0, b1, ., .)
+        swap16(x2, x3);  // x2 rows: (b2, b3, ., .)
+        const auto r = __builtin_amdgcn_permlane32_swap(x0, x2, false, false);
+        return __uint_as_float(r[0]);  // rows (b0, b1, b2, b3)
+      };
+#pragma unroll
+      for (int grp = 0; grp < 2; ++grp) {
+        const float g = grp == 0 ? gather(sv[0], sv[1], sv[2], sv[3]) : gather(sv[4], sv[5], 0.f, 0.f);
+        const int o = wave * WNC + grp * 64 + lane;  // output frame n0 + o
+        const float val = n0 + o < Lt ? tanhf(g + pb) : 0.f;
+        const bool live = (grp == 0 || lane < 32) && o < BN;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), wr, live ? (unsigned)((n0 + o) * 4) : 0x80000000u, 0, 0);
       }
     }
-    issued += FN * ((EF & VE_DUAL) ? 2 : 1);
+    issued += POST ? 2 : FN * ((EF & VE_DUAL) ? 2 : 1);
     VP_TS(9);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing row / weight DMAs land before LDS is freed

@@ -1,6 +1,6 @@
 """conv_post (hifigan/models.py:193-195: tanh(conv_post(leaky_relu(xs)))) folded into the last ResBlock pair of the
 vocoder's final stage (mt_vpair32 VE_POST: the stage output xs never reaches HBM) against its own launch
-(post_conv_kernel). Both run post_block's MFMA arithmetic (mt_vpair.h), so the waveforms must be EQUAL, on ragged and
+(post_conv_kernel). Both run post_taps / post_combine's MFMA arithmetic (mt_vpair.h), so the waveforms must be EQUAL, on ragged and
 padded batches, and the folded launch must really have run (launch log). Against the fp32 oracle the folded path is
 what tests/test_gpu_parity_bf16.py and test_gpu_bench_shapes.py run (it is the default)."""
 import pytest
