@@ -61,7 +61,8 @@ __global__ __launch_bounds__(256) void post_conv_kernel(const bf16* __restrict__
     const float s = post_combine(dp, dn, lane);
     dp = dn;
     const int f = f0 + r0 + lane;
-    if (lane < 16 && f < L) out[(size_t)b * L + f] = f < Lb ? tanhf(s + bs) : 0.f;
+    const float th = post_tanh(s + bs);
+    if (lane < 16 && f < L) out[(size_t)b * L + f] = f < Lb ? th : 0.f;
   }
 }
 

@@ -68,6 +68,13 @@ __device__ __forceinline__ float post_combine(const f32x4& da, const f32x4& db, 
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);  // row 0: (taps 0..3) + (taps 4..6)
 }
+// conv_post's tanh, inline (tanhf is an out-of-line library call: a call sequence and its register saves in the
+// epilogue): 1 - 2 / (2^(2 log2(e) x) + 1) on v_exp_f32 and v_rcp_f32, +-1 at the ends (2^x = inf / 0), absolute
+// error ~2e-7 (the bf16 path's waveform is checked against the oracle at 1e-2)
+__device__ __forceinline__ float post_tanh(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(e + 1.f);
+}
 
 // The compile-time K loop of the ring pair kernels (vpair_kernel<EF, K> and vpair128_kernel<EF, K>, K > 0): per wave
 // the prologue stages the first tile's rows (NXP pieces), then the weights of steps 0 .. NWS - 2 (2 pieces each); per

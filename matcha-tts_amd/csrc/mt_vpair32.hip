@@ -424,7 +424,7 @@ __global__ __launch_bounds__(NT) void vpair32_kernel(VPairArgs a) {
       for (int grp = 0; grp < 2; ++grp) {
         const float g = grp == 0 ? gather(sv[0], sv[1], sv[2], sv[3]) : gather(sv[4], sv[5], 0.f, 0.f);
         const int o = wave * WNC + grp * 64 + lane;  // output frame n0 + o
-        const float val = n0 + o < Lt ? tanhf(g + pb) : 0.f;
+        const float th = post_tanh(g + pb), val = n0 + o < Lt ? th : 0.f;
         const bool live = (grp == 0 || lane < 32) && o < BN;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), wr, live ? (unsigned)((n0 + o) * 4) : 0x80000000u, 0, 0);
       }
