@@ -50,15 +50,19 @@ __device__ __forceinline__ f32x4 post_taps(const char* rows, int r0, const bf16x
 }
 // element I of a post_taps result lives in 16-lane row g (tap 4 g + I): lane o of row 0 takes lane (o + I) & 15, of
 // row 1 lane (o + 4 + I) & 15 (DPP row_ror:m moves lane l - m to lane l, so m = 16 - that shift)
+// row 1's element 3 is tap 7, the A operand's zero row: its D = 0 x B is NaN wherever B holds a non-finite value
+// (LDS rows past the image: post_conv_kernel's last block reads rows it never wrote), so that term is never taken
 template <int I>
 __device__ __forceinline__ float post_rot(float x) {
   const int v = __float_as_int(x);
   const int r = I == 0 ? v : __builtin_amdgcn_update_dpp(0, v, 0x120 + 16 - I, 0x1, 0xf, false);
+  if constexpr (I == 3) return __int_as_float(r);
   return __int_as_float(__builtin_amdgcn_update_dpp(r, v, 0x120 + 12 - I, 0x2, 0xf, false));
 }
 // the 16 outputs of rows r0 .. r0 + 15 from da = post_taps(r0) and db = post_taps(r0 + 16): D[t][o + t] lies in da
-// when o + t < 16, i.e. at a source lane l16 >= t, else in db (lane l16 = o + t - 16 < t). Sum order: taps 0..3 and
-// 4..6 in order within rows 0 / 1, then row 0 + row 1; lanes 0..15 hold the block's sums
+// when o + t < 16, i.e. at a source lane l16 >= t, else in db (lane l16 = o + t - 16 < t), so only rows up to r0 + 21
+// reach a kept sum. Sum order: taps 0..3 and 4..6 in order within rows 0 / 1, then row 0 + row 1; lanes 0..15 hold
+// the block's sums
 __device__ __forceinline__ float post_combine(const f32x4& da, const f32x4& db, int lane) {
   const int l16 = lane & 15, t0 = 4 * (lane >> 4);
   float s = post_rot<0>(l16 >= t0 ? da[0] : db[0]);
