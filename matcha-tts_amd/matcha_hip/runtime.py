@@ -441,6 +441,28 @@ class VocoderEngine:
 
 # ---- index path / small ops ---------------------------------------------------------------
 
+_HOST_BUFS: Dict[tuple, torch.Tensor] = {}
+
+
+def fetch_ints(t: torch.Tensor) -> List[int]:
+    """A few device int64 values -> Python ints (synthesize's one host sync, model.py:1278-1281): an async copy into
+    a pinned buffer, then the host polls the copy's event. A blocking wait lets the host thread sleep, and its
+    wake-up left the GPU idle ≈ 0.16 ms between the durations and the alignment kernels in the B = 32 bench trace
+    (profiles/r06b_kernel_stats.csv's step)."""
+    import threading
+    n = t.numel()
+    key = (str(t.device), n, threading.get_ident())
+    buf = _HOST_BUFS.get(key)
+    if buf is None:
+        buf = _HOST_BUFS[key] = torch.empty(n, dtype=torch.int64, pin_memory=True)
+    buf.copy_(t.reshape(-1).to(torch.int64), non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(t.device))
+    while not ev.query():
+        pass
+    return buf.tolist()
+
+
 def durations(logw: torch.Tensor, x_mask: torch.Tensor, length_scale: float):
     """model.py:1273-1275 -> (w_ceil [B,1,Tx], cum [B,Tx], y_lengths int64 [B])."""
     require_gpu(logw, x_mask, what="durations")

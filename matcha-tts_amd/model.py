@@ -527,7 +527,7 @@ class MatchaTTS(nn.Module):
         try:
             # the reference's host sync (model.py:1278-1281), which also brings back the encoder's out-of-vocabulary
             # flag (one device->host copy for both)
-            y_max, bad = torch.stack((y_lengths.max(), oov[0].to(torch.int64))).tolist()
+            y_max, bad = rt.fetch_ints(torch.stack((y_lengths.max(), oov[0].to(torch.int64))))
             if bad:
                 raise IndexError("index out of range in self (a token id of x lies outside [0, n_vocab))")
             t_pad = fix_len_compatibility(y_max)
