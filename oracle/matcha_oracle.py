@@ -588,8 +588,10 @@ def training_losses(sd: SD, x: Tensor, x_lengths: Tensor, y: Tensor, y_lengths: 
 # §8f rank 4: the log-mel featurizer of the training data path, train_standalone.py:164-201 (identical
 # to hifigan/meldataset.py:52-89) and normalize :204-210. librosa (the filterbank's source) is not
 # installed here: `librosa_mel_basis` restates librosa.filters.mel (htk=False, norm="slaney", float32)
-# element by element — parity of the filterbank values is UNPINNED (no librosa output exists in the
-# reference to check against); the STFT / magnitude / log / normalisation are the reference's torch ops.
+# element by element, pinned against an independent implementation of the same published algorithm that the
+# image carries (transformers 5.15.0 audio_utils.mel_filter_bank, norm / mel_scale "slaney", itself tested
+# against librosa upstream): equal to float32 rounding (tests/test_featurizer.py); no librosa output exists in
+# the reference. The STFT / magnitude / log / normalisation are the reference's torch ops.
 # ---------------------------------------------------------------------------------------------------
 def librosa_mel_basis(sr: int, n_fft: int, n_mels: int, fmin: float, fmax: float) -> Tensor:
     f_sp, min_log_hz = 200.0 / 3, 1000.0

@@ -1,10 +1,14 @@
 """§8f rank 4: the log-mel featurizer (train_standalone.py:164-210 / hifigan/meldataset.py:52-89).
 
 CPU: the product's Slaney filterbank (hifigan/meldataset.librosa_mel_fn, vectorised) against the oracle's
-element-wise restatement of librosa.filters.mel (parity with librosa itself is UNPINNED: librosa is not
-installed and the reference holds no filterbank or mel output to compare with; the filterbank's
-published properties are checked instead), and the oracle's framing against an independent numpy
-rfft. GPU: the one-launch HIP featurizer against the oracle, atol 1e-4 on log-mel (fp32)."""
+element-wise restatement of librosa.filters.mel, and both against an INDEPENDENT implementation of the same
+published algorithm that this image carries: transformers.audio_utils.mel_filter_bank (transformers 5.15.0,
+norm="slaney", mel_scale="slaney"; its own test suite checks it against librosa). librosa itself is not
+installed and the reference holds no filterbank or mel output, so this is the filterbank's pin: agreement to
+float32 rounding (measured ≤ 1.1e-7 relative on every nonzero weight, ≤ 1.6e-9 absolute) at the reference's
+configuration and three others. The filterbank's published properties are checked too, and the oracle's framing
+against an independent numpy rfft. GPU: the one-launch HIP featurizer against the oracle, atol 1e-4 on log-mel
+(fp32)."""
 import math
 
 import numpy as np
@@ -22,6 +26,22 @@ def test_filterbank_matches_elementwise_restatement():
     b = O.librosa_mel_basis(SR, NFFT, NMEL, FMIN, FMAX).numpy()
     assert a.shape == (80, 513) and a.dtype == np.float32
     assert np.abs(a - b).max() <= 2e-9, np.abs(a - b).max()
+
+
+@pytest.mark.parametrize("sr,n_fft,n_mels,fmin,fmax", [(SR, NFFT, NMEL, FMIN, FMAX), (22050, 1024, 80, 0.0, 11025.0),
+                                                    (16000, 512, 64, 20.0, 7600.0), (24000, 2048, 100, 0.0, 12000.0)])
+def test_filterbank_matches_independent_implementation(sr, n_fft, n_mels, fmin, fmax):
+    """Pins librosa.filters.mel(htk=False, norm="slaney") (hifigan/meldataset.py:60) without librosa: the oracle and
+    the product against transformers' mel_filter_bank (float64), each weight to float32 rounding."""
+    audio_utils = pytest.importorskip("transformers.audio_utils")
+    ref = audio_utils.mel_filter_bank(num_frequency_bins=n_fft // 2 + 1, num_mel_filters=n_mels, min_frequency=fmin,
+                                      max_frequency=fmax, sampling_rate=sr, norm="slaney", mel_scale="slaney").T
+    for got in (O.librosa_mel_basis(sr, n_fft, n_mels, fmin, fmax).numpy(), librosa_mel_fn(sr, n_fft, n_mels, fmin, fmax)):
+        assert got.shape == ref.shape
+        d = np.abs(got.astype(np.float64) - ref)
+        nz = ref > 1e-9
+        assert np.all(got[~nz] == 0) or d[~nz].max() <= 1e-12
+        assert (d[nz] / ref[nz]).max() <= 2.5e-7 and d.max() <= 5e-9, ((d[nz] / ref[nz]).max(), d.max())
 
 
 def test_filterbank_properties():
