@@ -51,7 +51,7 @@ def parse(argv=None):
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--no-denoise", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-utterances", type=int, default=3, help="CPU baseline sample size (batch 1)")
+    p.add_argument("--cpu-utterances", type=int, default=6, help="CPU baseline sample size (batch 1; ~20 s of CPU work)")
     p.add_argument("--no-north-star", action="store_true", help="skip the B=256 single-GPU record")
     p.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode record")
     p.add_argument("--quick", action="store_true", help="headline line only: no sub-record, no CPU baseline")
