@@ -58,8 +58,7 @@
 
 #ifndef RB_EXP
 #define RB_EXP 0  // timing experiments (tools/exp_build.sh, tools/rblab): bits drop parts of the work (wrong results):
-                  // 1 epilogue operand loads, 2 the y2 store, 4 the K loop's DMA issue, 8 its step barriers, 16 MFMAs,
-                  // 32 every other step barrier
+                  // 1 epilogue operand loads, 2 the y2 store, 4 the K loop's DMA issue, 8 its step barriers, 16 MFMAs
 #endif
 
 namespace mt {
@@ -473,7 +472,7 @@ __global__ __launch_bounds__(RNT) void rbconv_kernel(VConvArgs a) {
       // writes LDS that other waves read after it
       if constexpr (ACTIN && t == K - 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       VP_TS(0);
-      if constexpr ((RB_EXP & 8) == 0 && ((RB_EXP & 32) == 0 || s % 2 == 0)) rb_barrier();
+      if constexpr ((RB_EXP & 8) == 0) rb_barrier();
       VP_TS(1);
       // the epilogue's residual / old-xs loads, RB_EPI_AT steps before the tile's last (compiler-visible loads: the
       // epilogue's use waits for them, the counted waits leave them out)
