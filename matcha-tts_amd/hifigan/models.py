@@ -149,7 +149,15 @@ class Generator(nn.Module):
             if lengths is None:
                 return eng.forward(self.packed(x.device), x)
             if eng.ragged_supported():
-                return eng.forward(self.packed(x.device), x, lengths=lengths)
+                B = x.shape[0]
+                if B <= rt.RAGGED_MAX_BATCH:
+                    return eng.forward(self.packed(x.device), x, lengths=lengths)
+                # more utterances than one ragged launch chain takes: consecutive chunks, each at the batch's T
+                out = torch.empty((B, 1, x.shape[-1] * eng.hop), dtype=torch.float32, device=x.device)
+                for s in range(0, B, rt.RAGGED_MAX_BATCH):
+                    e = min(B, s + rt.RAGGED_MAX_BATCH)
+                    eng.forward(self.packed(x.device), x[s:e].contiguous(), out=out[s:e], lengths=lengths[s:e])
+                return out
             B, _, T = x.shape
             hop = eng.hop
             out = torch.zeros((B, 1, T * hop), dtype=torch.float32, device=x.device)

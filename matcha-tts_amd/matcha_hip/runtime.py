@@ -441,6 +441,10 @@ class VocoderEngine:
 
 # ---- index path / small ops ---------------------------------------------------------------
 
+# utterances one ragged vocoder launch chain takes (mt_ragged.h RAG_MAXB: the per-utterance tile table lives in LDS);
+# Generator.forward splits larger batches (tests/test_abi_host.py checks the two stay equal)
+RAGGED_MAX_BATCH = 512
+
 _HOST_BUFS: Dict[tuple, torch.Tensor] = {}
 
 

@@ -153,3 +153,12 @@ def test_precision_switch():
     assert make_matcha(1, precision="bf16").encoder.precision == "fp32"
     with pytest.raises(ValueError):
         m.set_precision("int8")
+
+
+def test_ragged_batch_limit_matches_the_kernels():
+    """Generator.forward splits a ragged batch into chunks of runtime.RAGGED_MAX_BATCH utterances: the limit the
+    kernels' LDS tile tables have (mt_ragged.h RAG_MAXB)."""
+    from matcha_hip import runtime as rt
+    src = open(os.path.join(REPO, "matcha-tts_amd", "csrc", "mt_ragged.h")).read()
+    m = re.search(r"constexpr int RAG_MAXB = (\d+);", src)
+    assert m and int(m.group(1)) == rt.RAGGED_MAX_BATCH

@@ -32,6 +32,26 @@ def _mel(B, T, seed=9):
     return torch.randn(B, 80, T, generator=torch.Generator().manual_seed(seed)) * 2.1 - 5.5
 
 
+def test_vocoder_ragged_batch_beyond_one_launch_chain():
+    """More utterances than one ragged launch chain takes (runtime.RAGGED_MAX_BATCH = 512, the kernels' LDS tile
+    tables): Generator.forward vocodes consecutive chunks; every row equals the same row vocoded in a small ragged
+    batch (bit for bit: rows are independent), and is zero past its length."""
+    from matcha_hip import runtime as rt
+    g = _gen("bf16")
+    B, T = rt.RAGGED_MAX_BATCH + 5, 16
+    lens = torch.randint(0, T + 1, (B,), generator=torch.Generator().manual_seed(3))
+    lens[0], lens[-1] = T, 1
+    mel = _mel(B, T, seed=4).to(DEV)
+    wav = g(mel, lengths=lens.to(DEV))
+    torch.cuda.synchronize()
+    assert wav.shape == (B, 1, T * 256) and torch.isfinite(wav).all()
+    for s in (0, rt.RAGGED_MAX_BATCH - 3):  # rows on both sides of the chunk boundary, re-vocoded as one small batch
+        part = g(mel[s:s + 8].contiguous(), lengths=lens[s:s + 8].to(DEV))
+        assert torch.equal(wav[s:s + 8], part), s
+    for b in range(B):
+        assert torch.count_nonzero(wav[b, :, int(lens[b]) * 256:]) == 0, b
+
+
 def test_vocoder_ragged_rows_equal_one_utterance_calls():
     from hifigan.config import v1
     from matcha_hip import runtime as rt
