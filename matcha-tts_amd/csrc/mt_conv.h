@@ -84,6 +84,10 @@ struct ConvArgs {
   // valid frames (zero padding past them); tiles past its output columns exit, outputs past them are not written
   const int* lens;
   int lmul;
+  // 1: the tile configuration from the problem's per-utterance shape only, never from the batch size (the vocoder:
+  // a row's result must not depend on how many other utterances share the launch; TSmall and TConv accumulate K in
+  // different orders)
+  int fixed_tile;
 };
 
 // Host launcher. Picks a tile configuration from (M, N), validates the geometry and

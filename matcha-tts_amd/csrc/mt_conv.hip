@@ -725,8 +725,9 @@ static int launch_sel(const ConvArgs& a, hipStream_t stream, int* ntiles_out) {
       if (a.stride == 1 && a.taps == 1 && (a.cin >= 512 || M <= 384))
         return launch_tile<E, TG6, PF, EF, TAG>(a, stream, ntiles_out);
     if constexpr ((CFGS & CFG_C5) != 0)
-      if (a.stride == 1 && a.taps >= 3 && wgs < 192) return launch_tile<E, TC5, PF, EF, TAG>(a, stream, ntiles_out);
-    if (a.stride == 1 && (wgs >= 192 || (CFGS & CFG_SMALLN) == 0)) {
+      if (a.stride == 1 && a.taps >= 3 && wgs < 192 && !a.fixed_tile)
+        return launch_tile<E, TC5, PF, EF, TAG>(a, stream, ntiles_out);
+    if (a.stride == 1 && (wgs >= 192 || a.fixed_tile || (CFGS & CFG_SMALLN) == 0)) {
       if (a.taps == 1) return launch_tile<E, TGemm, PF, EF, TAG>(a, stream, ntiles_out);
       if (a.taps == 2) return launch_tile<E, TConvT, PF, EF, TAG>(a, stream, ntiles_out);
       return launch_tile<E, TConv, PF, EF, TAG>(a, stream, ntiles_out);

@@ -550,6 +550,7 @@ int Vocoder::forward_t(const char* P, const float* mel, int B, int T, float* wav
   auto rag = [&](ConvArgs& c, int rate) {
     c.lens = lens;
     c.lmul = rate;
+    c.fixed_tile = 1;  // batch-invariant rows: the tile choice may not depend on B
   };
   {
     ConvArgs a = gemm_args(pre, P, B, T);

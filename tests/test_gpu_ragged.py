@@ -32,6 +32,22 @@ def _mel(B, T, seed=9):
     return torch.randn(B, 80, T, generator=torch.Generator().manual_seed(seed)) * 2.1 - 5.5
 
 
+@pytest.mark.parametrize("T", [16, 300])
+def test_vocoder_rows_do_not_depend_on_the_batch(T):
+    """A row's waveform is the same bits whatever else shares the launch: rows 0-7 vocoded alone, inside a batch of
+    64 and inside one of 200, ragged and at full length (the generic conv kernel picked its tile configuration
+    from the batch size, and its two configurations sum K in different orders: conv_pre's rows then moved with B;
+    ConvArgs::fixed_tile)."""
+    g = _gen("bf16")
+    mel = _mel(200, T, seed=12).to(DEV)
+    lens = torch.randint(1, T + 1, (200,), generator=torch.Generator().manual_seed(13)).to(DEV)
+    for ln in (lens, None):
+        ref = g(mel[:8].contiguous(), lengths=None if ln is None else ln[:8])
+        for B in (64, 200):
+            out = g(mel[:B].contiguous(), lengths=None if ln is None else ln[:B])
+            assert torch.equal(out[:8], ref), (B, ln is None)
+
+
 def test_vocoder_ragged_batch_beyond_one_launch_chain():
     """More utterances than one ragged launch chain takes (runtime.RAGGED_MAX_BATCH = 512, the kernels' LDS tile
     tables): Generator.forward vocodes consecutive chunks; every row equals the same row vocoded in a small ragged

@@ -191,6 +191,31 @@ int main(int argc, char** argv) {
            bytes / t[j] * 1e-9, j == 0 ? "" : nd ? "  <-- DIFFERS FROM BASE" : "  bit-identical");
   }
 
+  // batch invariance: the first 8 utterances as a batch of their own (same rows, same lengths) must give the same
+  // valid frames as inside the full batch (rows are independent; mt_ragged.h)
+  if (B > 8) {
+    CK(hipMemset(y, 0, nx * 2));
+    pick(builds[1])(ef, &a, 0);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(ref.data(), y, nx * 2, hipMemcpyDeviceToHost));
+    CK(hipMemset(y, 0, nx * 2));
+    VPairArgs a8 = a;
+    a8.B = 8;
+    pick(builds[1])(ef, &a8, 0);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(out.data(), y, nx * 2, hipMemcpyDeviceToHost));
+    size_t nb = 0, first = (size_t)-1;
+    for (int b = 0; b < 8; ++b)
+      for (size_t i = (size_t)b * L * C; i < ((size_t)b * L + (ragged ? lens[b] : L)) * C; ++i)
+        if (ref[i] != out[i]) {
+          if (first == (size_t)-1) first = i;
+          ++nb;
+        }
+    printf("batch invariance (rows 0-7 alone vs in the B = %d batch): %zu valid outputs differ", B, nb);
+    if (nb) printf(" (first: row %zu frame %zu channel %zu)", first / ((size_t)L * C), first / C % L, first % C);
+    printf("\n");
+  }
+
   // phase stamps (the working tree with -DVPAIR_TS)
   unsigned long long* ts;
   const int G = 256;
