@@ -157,14 +157,14 @@ def test_generator_bf16_bench_length_vs_oracle():
 
 
 # ------------------------------------------------------------------------------- (c) bench step
-def _bench_rows_vs_oracle(batch, rows, tag, rank=0, world=1, vctk=False, n_ts=10):
+def _bench_rows_vs_oracle(batch, rows, tag, rank=0, world=1, vctk=False, n_ts=10, inputs=None):
     from hifigan.config import v1
     from matcha_hip import runtime as rt
     from oracle import matcha_oracle as O
     bench = _bench()
     n_spks = 109 if vctk else 1
     m, g, den, msd, gsd = bench.build_models(torch.device(DEV), "bf16", 1234, n_spks=n_spks)
-    x, xl = bench.shard_inputs(rank, world, batch, 1234)
+    x, xl = bench.shard_inputs(rank, world, batch, 1234) if inputs is None else inputs
     spk = bench.shard_speakers(rank, world, batch, 1234).to(DEV) if vctk else None
     torch.manual_seed(1234 + rank)  # bench.main's per-rank noise seed
     real = torch.randn_like
@@ -252,6 +252,18 @@ def test_bench_step_rows_vs_oracle_vctk_config4():
     """BASELINE configs[3] per GPU: VCTK 109-speaker model with the speaker-embedding condition (the encoder and
     the estimator both read spks), 16 utterances (= 128 over 8 GPUs), 20 ODE steps, bench step rows vs oracle."""
     _bench_rows_vs_oracle(16, [0, 7, 15], "bench_vctk16", vctk=True, n_ts=20)
+
+
+def test_bench_step_long_utterance_vs_oracle():
+    """Size edge: a 600-phoneme utterance (1,800 mel frames with the forced duration head, 460,800 samples, about
+    21 s of audio) batched with a 40-phoneme one (120 frames: 93 % of its row is padding), through the bench step
+    (2 ODE steps keep the CPU oracle short), both rows against the oracle at the bench's bars."""
+    g = torch.Generator().manual_seed(77)
+    x = torch.randint(1, 178, (2, 600), generator=g)
+    xl = torch.tensor([600, 40])
+    x[1, 40:] = 0
+    t_pad = _bench_rows_vs_oracle(2, [0, 1], "bench_long", n_ts=2, inputs=(x, xl))
+    assert t_pad == 1800
 
 
 # ------------------------------------------------------------------------------- (d) fp32 10 steps
