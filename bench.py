@@ -185,6 +185,7 @@ def reduce_over_ranks(elapsed, frames, dist, device):
 
 def step(m, g, den, x, xl, n_ts, denoise, spk=None):
     spks = m.spk_emb(spk) if spk is not None else None  # main.py: the speaker embedding of the requested ids
+    g.prepare(x.device)  # the vocoder's weight-cache check while the GPU runs synthesize, not after it
     mel, yl, attn = m.synthesize(x, xl, n_timesteps=n_ts, temperature=0.667, spks=spks, length_scale=1.0)
     # the reference's per-utterance vocoder + denoiser calls (main.py:198, MOS_audiou_generator.ipynb:276-277) for
     # the whole batch: utterance b at its own yl[b] frames

@@ -127,6 +127,14 @@ class Generator(nn.Module):
                 out[name + ".bias"] = m.bias
         return out
 
+    def prepare(self, device):
+        """Extension: check (or pack) the weights now, e.g. while the GPU still runs the acoustic model, so that the
+        next forward on `device` skips the check at its start (the same cache check, done earlier; synthesize does this
+        for the estimator). Only the next forward is trusted, so a weight update after prepare() is still seen by
+        the forward after that."""
+        self.packed(device)
+        self._pk.trust_next((self.precision, str(device)))
+
     def packed(self, device):
         key = (self.precision, str(device))
         packed = self._pk.get(key)
