@@ -157,13 +157,15 @@ def test_generator_bf16_bench_length_vs_oracle():
 
 
 # ------------------------------------------------------------------------------- (c) bench step
-def _bench_rows_vs_oracle(batch, rows, tag, rank=0, world=1, vctk=False, n_ts=10, inputs=None, row_bar=1e-2):
+def _bench_rows_vs_oracle(batch, rows, tag, rank=0, world=1, vctk=False, n_ts=10, inputs=None, row_bar=1e-2,
+                          solver="euler"):
     from hifigan.config import v1
     from matcha_hip import runtime as rt
     from oracle import matcha_oracle as O
     bench = _bench()
     n_spks = 109 if vctk else 1
     m, g, den, msd, gsd = bench.build_models(torch.device(DEV), "bf16", 1234, n_spks=n_spks)
+    m.decoder.solver = solver
     x, xl = bench.shard_inputs(rank, world, batch, 1234) if inputs is None else inputs
     spk = bench.shard_speakers(rank, world, batch, 1234).to(DEV) if vctk else None
     torch.manual_seed(1234 + rank)  # bench.main's per-rank noise seed
@@ -199,7 +201,7 @@ def _bench_rows_vs_oracle(batch, rows, tag, rank=0, world=1, vctk=False, n_ts=10
         y_mask = O.sequence_mask(y_ref, t_pad).unsqueeze(1).float()
         attn = O.generate_path(w_ceil.squeeze(1), (x_mask.unsqueeze(-1) * y_mask.unsqueeze(2)).squeeze(1))
         mu_y = torch.matmul(attn.transpose(1, 2), mu.transpose(1, 2)).transpose(1, 2)
-        zr = O.cfm_solve(O.sub(sd, "decoder.estimator"), mu_y, y_mask, n_ts, z[rows], spks)
+        zr = O.cfm_solve(O.sub(sd, "decoder.estimator"), mu_y, y_mask, n_ts, z[rows], spks, solver)
         mel_ref = O.denormalize(zr, sd["mel_mean"], sd["mel_std"])[:, :, :t_y]
         gs = {k: v.detach().cpu() for k, v in gsd.items()}
         bias = O.denoiser_bias_spec(gs, v1)
@@ -254,6 +256,12 @@ def test_bench_step_rows_vs_oracle_vctk_config4():
     """BASELINE configs[3] per GPU: VCTK 109-speaker model with the speaker-embedding condition (the encoder and
     the estimator both read spks), 16 utterances (= 128 over 8 GPUs), 20 ODE steps, bench step rows vs oracle."""
     _bench_rows_vs_oracle(16, [0, 7, 15], "bench_vctk16", vctk=True, n_ts=20)
+
+
+def test_bench_step_midpoint_solver_rows_vs_oracle():
+    """The CFM's other solver (model.py:1096-1101, 'midpoint') at the bench's batch: 5 midpoint steps = the bench's
+    10 estimator evaluations, bf16, rows against the oracle's midpoint solve at the bench bars."""
+    _bench_rows_vs_oracle(32, [0, 13, 31], "bench32_midpoint", n_ts=5, solver="midpoint")
 
 
 def test_bench_step_long_utterance_vs_oracle():
