@@ -130,8 +130,8 @@ class Generator(nn.Module):
     def prepare(self, device):
         """Extension: check (or pack) the weights now, e.g. while the GPU still runs the acoustic model, so that the
         next forward on `device` skips the check at its start (the same cache check, done earlier; synthesize does this
-        for the estimator). Only the next forward is trusted, so a weight update after prepare() is still seen by
-        the forward after that."""
+        for the estimator). Only the next forward is trusted: the weights must not change between prepare() and that
+        forward (an update after it is seen from the forward after that on)."""
         self.packed(device)
         self._pk.trust_next((self.precision, str(device)))
 

@@ -7,6 +7,7 @@ library only enqueues kernels on the current stream. All entry points require CU
 from __future__ import annotations
 
 import math
+import time
 from ctypes import byref, c_char_p, c_int, c_int64, c_void_p, create_string_buffer
 from typing import Dict, List, Optional, Tuple
 
@@ -462,8 +463,11 @@ def fetch_ints(t: torch.Tensor) -> List[int]:
     buf.copy_(t.reshape(-1).to(torch.int64), non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(t.device))
+    polls = 0
     while not ev.query():
-        pass
+        polls += 1
+        if polls > 256:  # past the first ~0.5 ms: yield the core between polls (a long encoder at large B)
+            time.sleep(0)
     return buf.tolist()
 
 
